@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""Benchmark: rendered Mpix/s, forward+backward, 1M Gaussians @ 1920x1080 (BASELINE.json).
+
+One step = for each view this rank owns: forward + backward of the differentiable rasterizer
+through the drop-in surface (diff_gaussian_rasterization.GaussianRasterizer + autograd),
+gradients accumulated into the replicated Gaussian parameters; then, with N>1 ranks, one
+RCCL all_reduce(SUM) of the 236 B/Gaussian parameter-gradient bucket.
+Each rank owns `--views-per-rank` views (default 1) of the 8-view ring, so per-GPU work is
+fixed as N grows (weak scaling; N=8 is BASELINE config 4's 8 views).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-npu_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import synthetic  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--views-per-rank", type=int, default=1)
+    ap.add_argument("--antialiasing", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(P, M, L, N, T, P_vis):
+    """Compulsory HBM bytes per launch of each kernel (split per kernel)."""
+    params = 4 * (11 + 3 * M)  # means 12 + scales 12 + rot 16 + opacity 4 + SH 12M
+    return {
+        "preprocess_fwd": P * params + P_vis * 44 + P * 4,     # params in; 44 B splat record + tile count out
+        "scan": P * 8,
+        "duplicate_with_keys": P * 16 + L * 12,                # rect inputs + 12 B key/value per instance
+        "sort_pairs": L * 24,                                  # one read + one write of (key, value)
+        "identify_tile_ranges": L * 8 + T * 8,
+        "render_fwd": L * 44 + N * 24 + T * 8,                 # id + 40 B record per instance; 24 B/pixel out
+        "render_bwd": L * 44 + N * 24 + P_vis * 48 + T * 8,    # id + record per instance; 24 B/pixel in; 48 B/G grads
+        "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    import diff_gaussian_rasterization as dgr
+    lib = dgr._C.lib
+    lib.gsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.gsr_profile_kernel_name.restype = ctypes.c_char_p
+
+    H, W, P = args.height, args.width, args.P
+    scene = synthetic.make_scene(P, seed=0)
+    params = {k: v.to(dev).requires_grad_(True) for k, v in scene.items()}
+    M = params["shs"].shape[1]
+    views = [(rank + i * world) % 8 for i in range(args.views_per_rank)]
+    cams, grads = [], []
+    for v in views:
+        cam = synthetic.Camera(W, H, view=v)
+        s = dgr.GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+            bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform.to(dev),
+            projmatrix=cam.full_proj_transform.to(dev), sh_degree=3, campos=cam.camera_center.to(dev),
+            prefiltered=False, debug=False, antialiasing=args.antialiasing)
+        cams.append(s)
+        gc, gi = synthetic.make_grads(H, W, seed=1 + v)
+        grads.append((gc.to(dev), gi.to(dev)))
+    order = ["means3D", "shs", "opacities", "scales", "rotations"]
+    last_L = [0]
+
+    def step():
+        for p in params.values():
+            p.grad = None
+        for s, (gc, gi) in zip(cams, grads):
+            rast = dgr.GaussianRasterizer(raster_settings=s)
+            means2D = torch.zeros_like(params["means3D"], requires_grad=True)
+            color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
+                                     opacities=params["opacities"], scales=params["scales"],
+                                     rotations=params["rotations"])
+            torch.autograd.backward([color, inv], [gc, gi])
+            last_L[0] = color.grad_fn.num_rendered if hasattr(color.grad_fn, "num_rendered") else last_L[0]
+        if world > 1:
+            flat = torch.cat([params[k].grad.reshape(-1) for k in order])
+            dist.all_reduce(flat)
+            off = 0
+            for k in order:
+                n = params[k].numel()
+                params[k].grad.copy_(flat[off:off + n].view_as(params[k]))
+                off += n
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not args.no_profile:
+        lib.gsr_profile_enable(1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    # per-kernel HIP-event timings over the timed region
+    kern = {}
+    if not args.no_profile:
+        nk = 16
+        tot = (ctypes.c_double * nk)()
+        cnt = (ctypes.c_int * nk)()
+        n = lib.gsr_profile_read(tot, cnt, nk)
+        lib.gsr_profile_enable(0)
+        for k in range(n):
+            if cnt[k]:
+                kern[lib.gsr_profile_kernel_name(k).decode()] = {"avg_ms": tot[k] / cnt[k], "launches": cnt[k]}
+
+    # geometry of the workload (one extra forward outside the timed region)
+    with torch.no_grad():
+        s = cams[0]
+        out = dgr._C.rasterize_gaussians(s.bg, params["means3D"], torch.Tensor([]), params["opacities"],
+                                         params["scales"], params["rotations"], 1.0, torch.Tensor([]), s.viewmatrix,
+                                         s.projmatrix, s.tanfovx, s.tanfovy, H, W, params["shs"], 3, s.campos, False,
+                                         args.antialiasing, False)
+        L = int(out[0])
+        P_vis = int((out[2] > 0).sum().item())
+    N = H * W
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    pix_total = world * len(views) * N * args.steps
+    value = pix_total / elapsed / 1e6
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    roofline = None
+    if kern:
+        ab = algorithmic_bytes(P, M, L, N, T, P_vis)
+        dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+        achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get(dom)
+            except Exception:
+                traffic = None
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "algorithmic_bytes": ab[dom],
+                    "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
+                                    "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1)} for k, v in kern.items()}}
+
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(args, scene, cams[0], grads[0])
+
+    res = {
+        "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
+        "value": round(value, 2),
+        "unit": "Mpix/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seed-0 Gaussian cloud, SURVEY.md §8d; ring camera views)",
+        "config": {"workload": f"{P} Gaussians, SH deg 3, {W}x{H}, {len(views)} view(s)/rank, fwd+bwd"
+                               + (" + RCCL grad all-reduce" if world > 1 else ""),
+                   "P": P, "width": W, "height": H, "views_per_rank": len(views), "num_rendered": L,
+                   "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, scene, s, grad):
+    """The CPU oracle (oracle/gsr_oracle.c, OpenMP) on the same view: one forward+backward."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        gc, gi = grad
+        t = time.perf_counter()
+        o = oracle.OracleRaster(scene["means3D"], scene["opacities"], s.bg.cpu(), s.viewmatrix.cpu(),
+                                s.projmatrix.cpu(), s.campos.cpu(), s.tanfovx, s.tanfovy, s.image_height,
+                                s.image_width, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
+                                rotations=scene["rotations"], antialiasing=args.antialiasing, nthreads=threads)
+        o.backward(gc.cpu(), gi.cpu())
+        dt = time.perf_counter() - t
+        return {"value": round(s.image_height * s.image_width / dt / 1e6, 3), "unit": "Mpix/s", "cores": threads,
+                "kind": "port", "seconds": round(dt, 2),
+                "sample": f"one full fwd+bwd of the bench view ({args.P} Gaussians, "
+                          f"{s.image_width}x{s.image_height}) by the C/OpenMP oracle"}
+    except Exception as e:  # the baseline must never take the GPU result down
+        return {"value": None, "unit": "Mpix/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
+
+
+if __name__ == "__main__":
+    main()

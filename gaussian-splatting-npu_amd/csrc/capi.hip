@@ -1,0 +1,446 @@
+// capi.hip -- C-ABI entry points (include/gsr.h).  Host-side orchestration that
+// replaces CudaRasterizer::Rasterizer::{markVisible, forward, backward}
+// (rasterizer_impl.cu:141-450): state-buffer carving, launch order, the one
+// stream-ordered D2H of num_rendered, and error reporting.  No exceptions
+// cross the ABI; every launch goes to the caller's stream.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "gsr.h"
+#include "gsr_common.h"
+#include "gsr_kernels.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+thread_local uint32_t* g_pinned = nullptr;
+
+int fail(int code, const char* msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int fail_hip(hipError_t e, int line)
+{
+    char buf[256];
+    snprintf(buf, sizeof(buf), "HIP error: %s (capi.hip:%d)", hipGetErrorString(e), line);
+    g_err = buf;
+    return GSR_ERR_HIP;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail_hip(e_, __LINE__);                                   \
+    } while (0)
+
+#define DEBUG_SYNC(stream)                                                                    \
+    do {                                                                                      \
+        if (debug) {                                                                          \
+            HIP_TRY(hipStreamSynchronize(stream));                                            \
+            HIP_TRY(hipGetLastError());                                                       \
+        }                                                                                     \
+    } while (0)
+
+int pinned(uint32_t** out)
+{
+    if (!g_pinned) {
+        hipError_t e = hipHostMalloc((void**)&g_pinned, 64, hipHostMallocDefault);
+        if (e != hipSuccess) return fail_hip(e, __LINE__);
+    }
+    *out = g_pinned;
+    return GSR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Optional per-kernel timing with HIP events recorded on the launch stream
+// (bench.py's roofline leg).  Off by default; costs two event records per
+// launch when on.
+// ---------------------------------------------------------------------------
+enum ProfKernel {
+    PK_PREPROCESS = 0, PK_SCAN, PK_DUPLICATE, PK_SORT, PK_RANGES, PK_RENDER_FWD, PK_RENDER_BWD, PK_PREPROCESS_BWD,
+    PK_COUNT
+};
+const char* kProfNames[PK_COUNT] = {"preprocess_fwd", "scan", "duplicate_with_keys", "sort_pairs",
+                                    "identify_tile_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
+struct Prof {
+    bool on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool[PK_COUNT];
+    size_t used[PK_COUNT] = {};
+};
+Prof g_prof;
+
+hipEvent_t prof_begin(int k, hipStream_t s)
+{
+    if (!g_prof.on) return nullptr;
+    auto& pool = g_prof.pool[k];
+    if (g_prof.used[k] == pool.size()) {
+        hipEvent_t a, b;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) return nullptr;
+        pool.push_back({a, b});
+    }
+    hipEvent_t e = pool[g_prof.used[k]].first;
+    (void)hipEventRecord(e, s);
+    return e;
+}
+
+void prof_end(int k, hipStream_t s, hipEvent_t begun)
+{
+    if (!g_prof.on || !begun) return;
+    (void)hipEventRecord(g_prof.pool[k][g_prof.used[k]].second, s);
+    g_prof.used[k]++;
+}
+
+struct ProfScope {
+    int k; hipStream_t s; hipEvent_t e;
+    ProfScope(int k_, hipStream_t s_) : k(k_), s(s_), e(prof_begin(k_, s_)) {}
+    ~ProfScope() { prof_end(k, s, e); }
+};
+
+template <typename T>
+T* at(char* base, size_t off) { return reinterpret_cast<T*>(base + off); }
+template <typename T>
+const T* at(const char* base, size_t off) { return reinterpret_cast<const T*>(base + off); }
+
+}  // namespace
+
+extern "C" {
+
+const char* gsr_last_error(void) { return g_err.c_str(); }
+
+const char* gsr_version(void) { return "gsr-hip 0.1 gfx950"; }
+
+int gsr_profile_enable(int on)
+{
+    g_prof.on = on != 0;
+    for (int k = 0; k < PK_COUNT; k++) g_prof.used[k] = 0;
+    return PK_COUNT;
+}
+
+const char* gsr_profile_kernel_name(int k) { return (k >= 0 && k < PK_COUNT) ? kProfNames[k] : ""; }
+
+// Waits for every recorded event, returns per-kernel summed milliseconds and launch counts
+// since the last enable/read, and resets the counters.
+int gsr_profile_read(double* total_ms, int* counts, int n)
+{
+    for (int k = 0; k < PK_COUNT && k < n; k++) {
+        double acc = 0.0;
+        for (size_t j = 0; j < g_prof.used[k]; j++) {
+            auto& ev = g_prof.pool[k][j];
+            HIP_TRY(hipEventSynchronize(ev.second));
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, ev.first, ev.second));
+            acc += ms;
+        }
+        total_ms[k] = acc;
+        counts[k] = (int)g_prof.used[k];
+        g_prof.used[k] = 0;
+    }
+    return PK_COUNT;
+}
+
+size_t gsr_geometry_buffer_size(int P) { return geom_layout(P).off[GEOM_COUNT] + 256; }
+size_t gsr_image_buffer_size(int width, int height) { return image_layout(width, height).off[IMG_COUNT] + 256; }
+size_t gsr_binning_buffer_size(int num_rendered) { return bin_layout(num_rendered).off[BIN_COUNT] + 256; }
+
+// Byte offsets of the arrays inside each state buffer (test/debug introspection).
+int gsr_geometry_layout(int P, size_t* offsets, int n)
+{
+    GeomLayout l = geom_layout(P);
+    for (int i = 0; i < n && i <= GEOM_COUNT; i++) offsets[i] = l.off[i];
+    return GEOM_COUNT;
+}
+int gsr_image_layout(int W, int H, size_t* offsets, int n)
+{
+    ImageLayout l = image_layout(W, H);
+    for (int i = 0; i < n && i <= IMG_COUNT; i++) offsets[i] = l.off[i];
+    return IMG_COUNT;
+}
+int gsr_binning_layout(int L, size_t* offsets, int n)
+{
+    BinLayout l = bin_layout(L);
+    for (int i = 0; i < n && i <= BIN_COUNT; i++) offsets[i] = l.off[i];
+    return BIN_COUNT;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, bool* present,
+                     gsr_stream_t stream)
+{
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_ERR_INVALID, "P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!means3D || !viewmatrix || !present) return fail(GSR_ERR_INVALID, "null pointer");
+    HIP_TRY(launch_mark_visible(P, means3D, viewmatrix, present, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
+                         const float* means3D, const float* shs, const float* colors_precomp,
+                         const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                         bool prefiltered, bool antialiasing, int* radii, bool debug, gsr_stream_t stream,
+                         int* num_rendered)
+{
+    hipStream_t s = (hipStream_t)stream;
+    *num_rendered = 0;
+    if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
+    if (width <= 0 || height <= 0) return fail(GSR_ERR_INVALID, "image size must be positive");
+    if (!colors_precomp && (!shs || M <= 0))
+        return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
+    if (!cov3D_precomp && (!scales || !rotations))
+        return fail(GSR_ERR_INVALID,
+                    "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (!geometry_buffer || !image_buffer) return fail(GSR_ERR_ALLOC, "null state buffer");
+
+    const GeomLayout g = geom_layout(P);
+    char* gb = geometry_buffer;
+    uint32_t* flags = at<uint32_t>(gb, g.off[GEOM_FLAGS]);
+    HIP_TRY(hipMemsetAsync(flags, 0, 256, s));
+
+    PreprocessArgs a;
+    a.P = P; a.D = D; a.M = M; a.W = width; a.H = height;
+    a.means3D = means3D; a.scales = scales; a.scale_modifier = scale_modifier; a.rotations = rotations;
+    a.opacities = opacities; a.shs = shs; a.cov3D_precomp = cov3D_precomp; a.colors_precomp = colors_precomp;
+    a.view = viewmatrix; a.proj = projmatrix; a.campos = cam_pos;
+    a.tan_fovx = tan_fovx; a.tan_fovy = tan_fovy;
+    a.focal_y = height / (2.0f * tan_fovy);
+    a.focal_x = width / (2.0f * tan_fovx);
+    a.grid_x = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    a.grid_y = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    a.prefiltered = prefiltered; a.antialiasing = antialiasing;
+    a.radii = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
+    a.means2D = at<float>(gb, g.off[GEOM_MEANS2D]);
+    a.depths = at<float>(gb, g.off[GEOM_DEPTH]);
+    a.cov3D_out = at<float>(gb, g.off[GEOM_COV3D]);
+    a.rgb = at<float>(gb, g.off[GEOM_RGB]);
+    a.conic_opacity = at<float>(gb, g.off[GEOM_CONIC_OPACITY]);
+    a.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
+    a.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
+    a.flags = flags;
+    {
+        ProfScope ps_(PK_PREPROCESS, s);
+        HIP_TRY(launch_preprocess(a, s));
+    }
+    DEBUG_SYNC(s);
+
+    uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    {
+        ProfScope ps_(PK_SCAN, s);
+        HIP_TRY(launch_inclusive_scan(a.tiles_touched, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]), s));
+    }
+    DEBUG_SYNC(s);
+
+    uint32_t* h;
+    int rc = pinned(&h);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(h, offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h + 1, flags, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (h[1] & 1u)
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (h[0] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
+    *num_rendered = (int)h[0];
+    return GSR_OK;
+}
+
+int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P, int num_rendered,
+                       const float* background, int width, int height, const float* colors_precomp,
+                       float* out_color, float* depth, int* radii, bool debug, gsr_stream_t stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (P <= 0) return GSR_OK;
+    const int L = num_rendered;
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const BinLayout b = bin_layout(L);
+    char* gb = geometry_buffer;
+    char* ib = image_buffer;
+    char* bb = binning_buffer;
+    if (L > 0 && !bb) return fail(GSR_ERR_ALLOC, "null binning buffer");
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const int T = (int)(gx * gy);
+    const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
+
+    uint64_t* keys_unsorted = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS_UNSORTED]) : nullptr;
+    uint64_t* keys = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS]) : nullptr;
+    uint32_t* vals_unsorted = L > 0 ? at<uint32_t>(bb, b.off[BIN_VALS_UNSORTED]) : nullptr;
+    uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
+    if (L > 0) {
+        {
+            ProfScope ps_(PK_DUPLICATE, s);
+            HIP_TRY(launch_duplicate_with_keys(P, at<float2>(gb, g.off[GEOM_MEANS2D]), at<float>(gb, g.off[GEOM_DEPTH]),
+                                               at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), rad, gx, gy, keys_unsorted,
+                                               vals_unsorted, s));
+        }
+        DEBUG_SYNC(s);
+        const int bit = (int)higher_msb(gx * gy);
+        {
+            ProfScope ps_(PK_SORT, s);
+            HIP_TRY(launch_sort_pairs(at<void>(bb, b.off[BIN_SORT_SCRATCH]),
+                                      b.off[BIN_SORT_SCRATCH + 1] - b.off[BIN_SORT_SCRATCH], keys_unsorted, keys,
+                                      vals_unsorted, point_list, L, 32 + bit, s));
+        }
+        DEBUG_SYNC(s);
+    }
+    uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    {
+        ProfScope ps_(PK_RANGES, s);
+        HIP_TRY(launch_identify_tile_ranges(L, keys, ranges, T, s));
+    }
+    DEBUG_SYNC(s);
+
+    RenderFwdArgs r;
+    r.ranges = ranges;
+    r.point_list = point_list;
+    r.W = width; r.H = height; r.grid_x = gx;
+    r.means2D = at<float2>(gb, g.off[GEOM_MEANS2D]);
+    r.features = colors_precomp ? colors_precomp : at<float>(gb, g.off[GEOM_RGB]);
+    r.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
+    r.depths = at<float>(gb, g.off[GEOM_DEPTH]);
+    r.bg = background;
+    r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
+    r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.out_color = out_color;
+    r.invdepth = depth;
+    {
+        ProfScope ps_(PK_RENDER_FWD, s);
+        HIP_TRY(launch_render_fwd(r, T, s));
+    }
+    DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn binningBuffer, void* binning_ctx,
+                gsr_resize_fn imageBuffer, void* image_ctx, int P, int D, int M, const float* background, int width,
+                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                float tan_fovx, float tan_fovy, bool prefiltered, float* out_color, float* depth, bool antialiasing,
+                int* radii, bool debug, gsr_stream_t stream, int* num_rendered)
+{
+    *num_rendered = 0;
+    if (P == 0) return GSR_OK;  // rasterize_points.cu:88 -- outputs stay as allocated
+    char* gb = geometryBuffer(geometry_ctx, gsr_geometry_buffer_size(P));
+    char* ib = imageBuffer(image_ctx, gsr_image_buffer_size(width, height));
+    if (!gb || !ib) return fail(GSR_ERR_ALLOC, "resize callback returned NULL");
+    int L = 0;
+    int rc = gsr_forward_geometry(gb, ib, P, D, M, width, height, means3D, shs, colors_precomp, opacities, scales,
+                                  scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx,
+                                  tan_fovy, prefiltered, antialiasing, radii, debug, stream, &L);
+    if (rc) return rc;
+    char* bb = binningBuffer(binning_ctx, gsr_binning_buffer_size(L));
+    if (!bb) return fail(GSR_ERR_ALLOC, "resize callback returned NULL");
+    rc = gsr_forward_render(gb, bb, ib, P, L, background, width, height, colors_precomp, out_color, depth, radii,
+                            debug, stream);
+    if (rc) return rc;
+    *num_rendered = L;
+    return GSR_OK;
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                 float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                 char* geom_buffer, char* binning_buffer, char* image_buffer, const float* dL_dpix,
+                 const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                 float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (P <= 0) return GSR_OK;
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const BinLayout b = bin_layout(R);
+    char* gb = geom_buffer;
+    char* ib = image_buffer;
+    char* bb = binning_buffer;
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const int T = (int)(gx * gy);
+    const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
+    if ((dL_invdepths == nullptr) != (dL_dinvdepth == nullptr))
+        return fail(GSR_ERR_INVALID, "dL_invdepths and dL_dinvdepth must both be given or both NULL");
+
+    RenderBwdArgs r;
+    r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
+    r.W = width; r.H = height; r.grid_x = gx;
+    r.bg = background;
+    r.means2D = at<float2>(gb, g.off[GEOM_MEANS2D]);
+    r.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
+    r.colors = colors_precomp ? colors_precomp : at<float>(gb, g.off[GEOM_RGB]);
+    r.depths = at<float>(gb, g.off[GEOM_DEPTH]);
+    r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
+    r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.dL_dpixels = dL_dpix;
+    r.dL_invdepths = dL_invdepths;
+    r.dL_dmean2D = dL_dmean2D;
+    r.dL_dconic2D = dL_dconic;
+    r.dL_dopacity = dL_dopacity;
+    r.dL_dcolors = dL_dcolor;
+    r.dL_dinvdepths = dL_dinvdepth;
+    if (R > 0) {
+        {
+            ProfScope ps_(PK_RENDER_BWD, s);
+            HIP_TRY(launch_render_bwd(r, T, s));
+        }
+        DEBUG_SYNC(s);
+    }
+
+    PreprocessBwdArgs p;
+    p.P = P; p.D = D; p.M = M;
+    p.means3D = means3D; p.radii = rad; p.shs = shs;
+    p.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
+    p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
+    p.cov3Ds = cov3D_precomp ? cov3D_precomp : at<float>(gb, g.off[GEOM_COV3D]);
+    p.view = viewmatrix; p.proj = projmatrix;
+    p.focal_y = height / (2.0f * tan_fovy);
+    p.focal_x = width / (2.0f * tan_fovx);
+    p.tan_fovx = tan_fovx; p.tan_fovy = tan_fovy;
+    p.campos = campos;
+    p.antialiasing = antialiasing;
+    p.dL_dmean2D = dL_dmean2D; p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
+    p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
+    p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;
+    p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;
+    {
+        ProfScope ps_(PK_PREPROCESS_BWD, s);
+        HIP_TRY(launch_preprocess_bwd(p, s));
+    }
+    DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffer, const char* image_buffer, int P,
+                          int num_rendered, int width, int height, uint64_t* keys_out, uint32_t* vals_out,
+                          uint32_t* ranges_out, gsr_stream_t stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    (void)geometry_buffer; (void)P;
+    const BinLayout b = bin_layout(num_rendered);
+    const ImageLayout im = image_layout(width, height);
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    if (num_rendered > 0) {
+        if (keys_out)
+            HIP_TRY(hipMemcpyAsync(keys_out, binning_buffer + b.off[BIN_KEYS], 8 * (size_t)num_rendered,
+                                   hipMemcpyDeviceToDevice, s));
+        if (vals_out)
+            HIP_TRY(hipMemcpyAsync(vals_out, binning_buffer + b.off[BIN_POINT_LIST], 4 * (size_t)num_rendered,
+                                   hipMemcpyDeviceToDevice, s));
+    }
+    if (ranges_out)
+        HIP_TRY(hipMemcpyAsync(ranges_out, image_buffer + im.off[IMG_RANGES], 8 * (size_t)gx * gy,
+                               hipMemcpyDeviceToDevice, s));
+    return GSR_OK;
+}
+
+}  // extern "C"

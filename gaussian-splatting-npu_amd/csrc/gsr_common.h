@@ -1,0 +1,225 @@
+// gsr_common.h -- shared device helpers and state-buffer layouts for the
+// gfx950 rasterizer.  Device math restates the reference helpers in
+// cuda_rasterizer/auxiliary.h and the GLM 0.9.9.9 mat3 products the
+// reference kernels use (forward.cu, backward.cu); the floating-point
+// expression order is kept so that, with -ffp-contract=off (this library's
+// default), preprocess outputs are bit-identical to oracle/gsr_oracle.c.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#define GSR_BLOCK_X 16
+#define GSR_BLOCK_Y 16
+#define GSR_TILE_PIX (GSR_BLOCK_X * GSR_BLOCK_Y)
+
+namespace gsr {
+
+// auxiliary.h:21-38
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+struct f3 { float x, y, z; };
+
+// glm::mat3 storage m[col][row]
+struct mat3 { float m[3][3]; };
+
+__device__ __forceinline__ mat3 mat3_cols(float a, float b, float c, float d, float e, float f, float g,
+                                          float h, float i)
+{
+    mat3 r;
+    r.m[0][0] = a; r.m[0][1] = b; r.m[0][2] = c;
+    r.m[1][0] = d; r.m[1][1] = e; r.m[1][2] = f;
+    r.m[2][0] = g; r.m[2][1] = h; r.m[2][2] = i;
+    return r;
+}
+
+// glm type_mat3x3.inl operator*(mat3, mat3)
+__device__ __forceinline__ mat3 mat3_mul(const mat3& a, const mat3& b)
+{
+    mat3 r;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int w = 0; w < 3; w++)
+            r.m[c][w] = a.m[0][w] * b.m[c][0] + a.m[1][w] * b.m[c][1] + a.m[2][w] * b.m[c][2];
+    return r;
+}
+
+__device__ __forceinline__ mat3 mat3_T(const mat3& a)
+{
+    mat3 r;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) r.m[c][w] = a.m[w][c];
+    return r;
+}
+
+// auxiliary.h:70-78
+__device__ __forceinline__ f3 transformPoint4x3(const f3 p, const float* m)
+{
+    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+            m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
+}
+
+// auxiliary.h:80-89
+__device__ __forceinline__ float4 transformPoint4x4(const f3 p, const float* m)
+{
+    return make_float4(m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
+                       m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+                       m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14],
+                       m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]);
+}
+
+// auxiliary.h:101-109
+__device__ __forceinline__ f3 transformVec4x3Transpose(const f3 p, const float* m)
+{
+    return {m[0] * p.x + m[1] * p.y + m[2] * p.z,
+            m[4] * p.x + m[5] * p.y + m[6] * p.z,
+            m[8] * p.x + m[9] * p.y + m[10] * p.z};
+}
+
+// auxiliary.h:119-129
+__device__ __forceinline__ f3 dnormvdv(const f3 v, const f3 dv)
+{
+    float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    f3 r;
+    r.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+    r.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+    r.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+    return r;
+}
+
+// auxiliary.h:40-43 (double arithmetic, as the reference's 1.0 literals imply)
+__device__ __forceinline__ float ndc2Pix(float v, int S)
+{
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+// auxiliary.h:45-55
+__device__ __forceinline__ void getRect(float px, float py, int max_radius, uint32_t gx, uint32_t gy,
+                                        uint32_t& rminx, uint32_t& rminy, uint32_t& rmaxx, uint32_t& rmaxy)
+{
+    int a;
+    a = (int)((px - (float)max_radius) / (float)GSR_BLOCK_X); a = a > 0 ? a : 0;
+    rminx = (uint32_t)a < gx ? (uint32_t)a : gx;
+    a = (int)((py - (float)max_radius) / (float)GSR_BLOCK_Y); a = a > 0 ? a : 0;
+    rminy = (uint32_t)a < gy ? (uint32_t)a : gy;
+    a = (int)((px + (float)max_radius + (float)GSR_BLOCK_X - 1.0f) / (float)GSR_BLOCK_X); a = a > 0 ? a : 0;
+    rmaxx = (uint32_t)a < gx ? (uint32_t)a : gx;
+    a = (int)((py + (float)max_radius + (float)GSR_BLOCK_Y - 1.0f) / (float)GSR_BLOCK_Y); a = a > 0 ? a : 0;
+    rmaxy = (uint32_t)a < gy ? (uint32_t)a : gy;
+}
+
+// ----------------------------------------------------------------------------
+// State-buffer layouts (the reference's GeometryState / ImageState /
+// BinningState, rasterizer_impl.h:29-65, re-laid out for this implementation).
+// Every array starts on a 256-byte boundary.
+// ----------------------------------------------------------------------------
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+
+enum GeomArray {
+    GEOM_DEPTH = 0,       // f32[P] view-space z
+    GEOM_RADII,           // i32[P] internal radii (used when caller passes radii=NULL)
+    GEOM_CLAMPED,         // u8[P]  bit c <=> rgb channel c was clamped (forward.cu:67-69)
+    GEOM_MEANS2D,         // f32x2[P]
+    GEOM_CONIC_OPACITY,   // f32x4[P]
+    GEOM_RGB,             // f32[3P]
+    GEOM_TILES_TOUCHED,   // u32[P]
+    GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched
+    GEOM_COV3D,           // f32[6P]
+    GEOM_SCAN_SCRATCH,    // u32[scan blocks + 64]
+    GEOM_FLAGS,           // u32[64] error flags / misc
+    GEOM_COUNT
+};
+
+enum ImageArray {
+    IMG_RANGES = 0,       // u32x2[T]
+    IMG_FINAL_T,          // f32[N]
+    IMG_N_CONTRIB,        // u32[N]
+    IMG_COUNT
+};
+
+enum BinArray {
+    BIN_KEYS_UNSORTED = 0, // u64[L]
+    BIN_KEYS,              // u64[L]
+    BIN_VALS_UNSORTED,     // u32[L]
+    BIN_POINT_LIST,        // u32[L]
+    BIN_SORT_SCRATCH,      // bytes
+    BIN_COUNT
+};
+
+constexpr int SCAN_ITEMS = 4096;  // items per scan block (256 threads x 16)
+
+struct GeomLayout { size_t off[GEOM_COUNT + 1]; };
+struct ImageLayout { size_t off[IMG_COUNT + 1]; };
+struct BinLayout { size_t off[BIN_COUNT + 1]; };
+
+inline GeomLayout geom_layout(int P)
+{
+    size_t p = (size_t)(P > 0 ? P : 0);
+    size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p,
+                                4 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 64), 4 * 64};
+    GeomLayout l;
+    size_t o = 0;
+    for (int i = 0; i < GEOM_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
+    l.off[GEOM_COUNT] = o;
+    return l;
+}
+
+inline ImageLayout image_layout(int W, int H)
+{
+    size_t n = (size_t)W * H;
+    size_t t = (size_t)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X) * ((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n};
+    ImageLayout l;
+    size_t o = 0;
+    for (int i = 0; i < IMG_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
+    l.off[IMG_COUNT] = o;
+    return l;
+}
+
+size_t sort_scratch_bytes(int L);
+
+inline BinLayout bin_layout(int L)
+{
+    size_t n = (size_t)(L > 0 ? L : 0);
+    size_t sizes[BIN_COUNT] = {8 * n, 8 * n, 4 * n, 4 * n, sort_scratch_bytes(L)};
+    BinLayout l;
+    size_t o = 0;
+    for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
+    l.off[BIN_COUNT] = o;
+    return l;
+}
+
+// Reference getHigherMsb (rasterizer_impl.cu:35-50)
+inline uint32_t higher_msb(uint32_t n)
+{
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+}  // namespace gsr

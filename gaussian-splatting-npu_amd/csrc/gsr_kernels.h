@@ -1,0 +1,116 @@
+// gsr_kernels.h -- kernel argument blocks and host launchers (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsr {
+
+struct PreprocessArgs {
+    int P, D, M, W, H;
+    const float* means3D;
+    const float* scales;
+    float scale_modifier;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    uint32_t grid_x, grid_y;
+    int prefiltered, antialiasing;
+    // outputs
+    int* radii;
+    float* means2D;
+    float* depths;
+    float* cov3D_out;
+    float* rgb;
+    float* conic_opacity;
+    uint8_t* clamped;
+    uint32_t* tiles_touched;
+    uint32_t* flags;
+};
+
+struct RenderFwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    int W, H;
+    uint32_t grid_x;
+    const float2* means2D;
+    const float* features;
+    const float4* conic_opacity;
+    const float* depths;
+    const float* bg;
+    float* final_T;
+    uint32_t* n_contrib;
+    float* out_color;
+    float* invdepth;
+};
+
+struct RenderBwdArgs {
+    const uint2* ranges;
+    const uint32_t* point_list;
+    int W, H;
+    uint32_t grid_x;
+    const float* bg;
+    const float2* means2D;
+    const float4* conic_opacity;
+    const float* colors;
+    const float* depths;
+    const float* final_Ts;
+    const uint32_t* n_contrib;
+    const float* dL_dpixels;
+    const float* dL_invdepths;
+    float* dL_dmean2D;   // (P,3)
+    float* dL_dconic2D;  // (P,4)
+    float* dL_dopacity;  // (P)
+    float* dL_dcolors;   // (P,3)
+    float* dL_dinvdepths;  // (P) or null
+};
+
+struct PreprocessBwdArgs {
+    int P, D, M;
+    const float* means3D;
+    const int* radii;
+    const float* shs;
+    const uint8_t* clamped;
+    const float* opacities;
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    const float* cov3Ds;
+    const float* view;
+    const float* proj;
+    float focal_x, focal_y, tan_fovx, tan_fovy;
+    const float* campos;
+    int antialiasing;
+    const float* dL_dmean2D;
+    const float* dL_dconic;
+    const float* dL_dinvdepth;
+    float* dL_dopacity;
+    float* dL_dcolor;
+    float* dL_dmean3D;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dscale;
+    float* dL_drot;
+};
+
+hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
+hipError_t launch_inclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* scratch, hipStream_t s);
+
+hipError_t launch_duplicate_with_keys(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
+                                      const int* radii, uint32_t gx, uint32_t gy, uint64_t* keys,
+                                      uint32_t* vals, hipStream_t s);
+hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                             const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit, hipStream_t s);
+hipError_t launch_identify_tile_ranges(int L, const uint64_t* keys, uint2* ranges, int T, hipStream_t s);
+
+hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
+hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
+hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
+
+}  // namespace gsr

@@ -1,0 +1,300 @@
+// preprocess.hip -- FORWARD::preprocess (forward.cu:154-272, launch :459-486),
+// markVisible/checkFrustum (rasterizer_impl.cu:54-66, 141-153) and the
+// inclusive scan of tiles_touched (cub::DeviceScan::InclusiveSum,
+// rasterizer_impl.cu:280) for gfx950.
+//
+// Compiled with -ffp-contract=off: every value on the key-producing path is
+// bit-identical to oracle/gsr_oracle.c (depth bits, radii, rect, tile counts).
+// One thread per Gaussian, 256-thread blocks (4 wave64s).  HBM-bound: the
+// per-Gaussian input is 236 B at SH degree 3 (means 12, scales 12, rot 16,
+// opacity 4, SH 192); output record 44 B (+24 B cov3D).
+#include "gsr_common.h"
+#include "gsr_kernels.h"
+
+namespace gsr {
+
+// forward.cu:114-151
+__device__ __forceinline__ void computeCov3D(const float* scale, float mod, const float4 rot, float* cov3D)
+{
+    mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+    S.m[0][0] = mod * scale[0];
+    S.m[1][1] = mod * scale[1];
+    S.m[2][2] = mod * scale[2];
+    const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
+    mat3 R = mat3_cols(
+        1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+        2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+        2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    mat3 M = mat3_mul(S, R);
+    mat3 Sigma = mat3_mul(mat3_T(M), M);
+    cov3D[0] = Sigma.m[0][0];
+    cov3D[1] = Sigma.m[0][1];
+    cov3D[2] = Sigma.m[0][2];
+    cov3D[3] = Sigma.m[1][1];
+    cov3D[4] = Sigma.m[1][2];
+    cov3D[5] = Sigma.m[2][2];
+}
+
+// forward.cu:74-109
+__device__ __forceinline__ f3 computeCov2D(const f3 mean, float focal_x, float focal_y, float tan_fovx,
+                                           float tan_fovy, const float* cov3D, const float* v)
+{
+    f3 t = transformPoint4x3(mean, v);
+    const float limx = 1.3f * tan_fovx;
+    const float limy = 1.3f * tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    mat3 J = mat3_cols(focal_x / t.z, 0.0f, -(focal_x * t.x) / (t.z * t.z),
+                       0.0f, focal_y / t.z, -(focal_y * t.y) / (t.z * t.z),
+                       0, 0, 0);
+    mat3 W = mat3_cols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
+    mat3 T = mat3_mul(W, J);
+    mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
+                         cov3D[5]);
+    mat3 cov = mat3_mul(mat3_mul(mat3_T(T), mat3_T(Vrk)), T);
+    return {cov.m[0][0], cov.m[0][1], cov.m[1][1]};
+}
+
+// forward.cu:20-71
+__device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const float* sh, const float* campos,
+                                                 uint8_t& clamped)
+{
+    f3 dir = {pos.x - campos[0], pos.y - campos[1], pos.z - campos[2]};
+    const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+    dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
+    float res[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) res[c] = SH_C0 * sh[0 * 3 + c];
+    if (deg > 0) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            res[c] = res[c] - SH_C1 * y * sh[1 * 3 + c] + SH_C1 * z * sh[2 * 3 + c] - SH_C1 * x * sh[3 * 3 + c];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+                res[c] = res[c] + SH_C2_0 * xy * sh[4 * 3 + c] + SH_C2_1 * yz * sh[5 * 3 + c] +
+                         SH_C2_2 * (2.0f * zz - xx - yy) * sh[6 * 3 + c] + SH_C2_3 * xz * sh[7 * 3 + c] +
+                         SH_C2_4 * (xx - yy) * sh[8 * 3 + c];
+            if (deg > 2) {
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    res[c] = res[c] + SH_C3_0 * y * (3.0f * xx - yy) * sh[9 * 3 + c] +
+                             SH_C3_1 * xy * z * sh[10 * 3 + c] +
+                             SH_C3_2 * y * (4.0f * zz - xx - yy) * sh[11 * 3 + c] +
+                             SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12 * 3 + c] +
+                             SH_C3_4 * x * (4.0f * zz - xx - yy) * sh[13 * 3 + c] +
+                             SH_C3_5 * z * (xx - yy) * sh[14 * 3 + c] +
+                             SH_C3_6 * x * (xx - 3.0f * yy) * sh[15 * 3 + c];
+            }
+        }
+    }
+    uint8_t cl = 0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        res[c] += 0.5f;
+        if (res[c] < 0) cl |= (uint8_t)(1u << c);
+        res[c] = res[c] < 0.0f ? 0.0f : res[c];
+    }
+    clamped = cl;
+    return {res[0], res[1], res[2]};
+}
+
+__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+
+    a.radii[idx] = 0;
+    a.tiles_touched[idx] = 0;
+
+    const f3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    // in_frustum (auxiliary.h:151-176)
+    const f3 p_view = transformPoint4x3(p_orig, a.view);
+    if (p_view.z <= 0.2f) {
+        if (a.prefiltered) atomicOr(a.flags, 1u);
+        return;
+    }
+    const float4 p_hom = transformPoint4x4(p_orig, a.proj);
+    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+    const float ppx = p_hom.x * p_w, ppy = p_hom.y * p_w;
+
+    float cov3D_local[6];
+    const float* cov3D;
+    if (a.cov3D_precomp) {
+        cov3D = a.cov3D_precomp + (size_t)idx * 6;
+    } else {
+        const float* rp = a.rotations + 4 * (size_t)idx;
+        const float4 rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        computeCov3D(a.scales + 3 * (size_t)idx, a.scale_modifier, rot, cov3D_local);
+#pragma unroll
+        for (int i = 0; i < 6; i++) a.cov3D_out[(size_t)idx * 6 + i] = cov3D_local[i];
+        cov3D = cov3D_local;
+    }
+
+    f3 cov = computeCov2D(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3D, a.view);
+    const float h_var = 0.3f;
+    const float det_cov = cov.x * cov.z - cov.y * cov.y;
+    cov.x += h_var;
+    cov.z += h_var;
+    const float det_cov_plus_h_cov = cov.x * cov.z - cov.y * cov.y;
+    float h_convolution_scaling = 1.0f;
+    if (a.antialiasing) h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
+
+    const float det = det_cov_plus_h_cov;
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cov.z * det_inv, conic_y = -cov.y * det_inv, conic_z = cov.x * det_inv;
+
+    const float mid = 0.5f * (cov.x + cov.z);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const float pix_x = ndc2Pix(ppx, a.W), pix_y = ndc2Pix(ppy, a.H);
+    uint32_t rminx, rminy, rmaxx, rmaxy;
+    getRect(pix_x, pix_y, (int)my_radius, a.grid_x, a.grid_y, rminx, rminy, rmaxx, rmaxy);
+    if ((rmaxx - rminx) * (rmaxy - rminy) == 0) return;
+
+    if (!a.colors_precomp) {
+        uint8_t cl;
+        const f3 rgb = computeColorFromSH(p_orig, a.D, a.shs + (size_t)idx * a.M * 3, a.campos, cl);
+        a.rgb[3 * (size_t)idx + 0] = rgb.x;
+        a.rgb[3 * (size_t)idx + 1] = rgb.y;
+        a.rgb[3 * (size_t)idx + 2] = rgb.z;
+        a.clamped[idx] = cl;
+    }
+    a.depths[idx] = p_view.z;
+    a.radii[idx] = (int)my_radius;
+    reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
+    const float opacity = a.opacities[idx];
+    reinterpret_cast<float4*>(a.conic_opacity)[idx] =
+        make_float4(conic_x, conic_y, conic_z, opacity * h_convolution_scaling);
+    a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
+}
+
+__global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,
+                                                           bool* present)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const f3 p = {means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]};
+    present[idx] = !(transformPoint4x3(p, view).z <= 0.2f);
+}
+
+// ---------------------------------------------------------------------------
+// Inclusive scan of u32 counts (reduce-then-scan, 3 launches, no inter-block
+// spinning).  SCAN_ITEMS = 256 threads x 16 items per block.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
+{
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t n = __shfl_up(v, d, 64);
+        if (lane >= d) v += n;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one value per thread (256 threads); returns exclusive prefix, total in *tot
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds4, uint32_t& total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) lds4[wid] = inc;
+    __syncthreads();
+    uint32_t wprefix = 0;
+    total = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+        uint32_t s = lds4[w];
+        if (w < wid) wprefix += s;
+        total += s;
+    }
+    __syncthreads();
+    return wprefix + inc - v;
+}
+
+__global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, int n, uint32_t* block_sums)
+{
+    __shared__ uint32_t lds4[4];
+    const size_t base = (size_t)blockIdx.x * SCAN_ITEMS;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_ITEMS / 256; k++) {
+        size_t i = base + k * 256 + threadIdx.x;
+        if (i < (size_t)n) s += in[i];
+    }
+    uint32_t total;
+    block_excl_scan256(s, lds4, total);
+    if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+}
+
+// single block: exclusive scan of block sums in place (nb can exceed 256; loop)
+__global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sums, int nb)
+{
+    __shared__ uint32_t lds4[4];
+    uint32_t carry = 0;
+    for (int base = 0; base < nb; base += 256) {
+        int i = base + threadIdx.x;
+        uint32_t v = i < nb ? block_sums[i] : 0;
+        uint32_t total;
+        uint32_t ex = block_excl_scan256(v, lds4, total);
+        if (i < nb) block_sums[i] = carry + ex;
+        carry += total;
+    }
+}
+
+__global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, int n, const uint32_t* block_offsets,
+                                                         uint32_t* out)
+{
+    __shared__ uint32_t lds4[4];
+    // each thread owns 16 consecutive items
+    const size_t base = (size_t)blockIdx.x * SCAN_ITEMS + (size_t)threadIdx.x * 16;
+    uint32_t v[16];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        size_t i = base + k;
+        v[k] = i < (size_t)n ? in[i] : 0;
+        s += v[k];
+    }
+    uint32_t total;
+    uint32_t ex = block_excl_scan256(s, lds4, total) + block_offsets[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        ex += v[k];
+        size_t i = base + k;
+        if (i < (size_t)n) out[i] = ex;
+    }
+}
+
+hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
+{
+    if (a.P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s)
+{
+    if (P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, view, present);
+    return hipGetLastError();
+}
+
+hipError_t launch_inclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* scratch, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(256), 0, s, in, n, scratch);
+    hipLaunchKernelGGL(scan_blocksums_kernel, dim3(1), dim3(256), 0, s, scratch, nb);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, n, scratch, out);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,295 @@
+// preprocess_bwd.hip -- BACKWARD::preprocess (backward.cu:640-712): the
+// reference's two per-Gaussian kernels computeCov2DCUDA (backward.cu:147-326)
+// and preprocessCUDA (backward.cu:398-449, with computeColorFromSH :23-142 and
+// computeCov3D :330-393) fused into one gfx950 kernel, one thread per
+// Gaussian.  Every output row is written (zeros for culled Gaussians), so the
+// caller does not have to pre-zero dL_dmean3D / dL_dcov3D / dL_dsh /
+// dL_dscale / dL_drot.  HBM-bound: reads ~236 B/G of parameters + the 44 B/G
+// gradient record, writes ~232 B/G.
+#include "gsr_common.h"
+#include "gsr_kernels.h"
+
+namespace gsr {
+
+__device__ __forceinline__ float sq(float x) { return x * x; }
+
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const size_t i = (size_t)idx;
+    float* dmean = a.dL_dmean3D + 3 * i;
+    float* dcov = a.dL_dcov3D + 6 * i;
+    float* dsh = a.dL_dsh ? a.dL_dsh + i * a.M * 3 : nullptr;
+
+    if (!(a.radii[idx] > 0)) {
+        dmean[0] = 0.f; dmean[1] = 0.f; dmean[2] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) dcov[k] = 0.f;
+        if (dsh)
+            for (int k = 0; k < a.M * 3; k++) dsh[k] = 0.f;
+        if (a.dL_dscale) { a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f; }
+        if (a.dL_drot) { float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f; }
+        return;
+    }
+
+    // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
+    const float* cov3D = a.cov3Ds + 6 * i;
+    const f3 mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
+    const f3 dL_dconic = {a.dL_dconic[4 * i], a.dL_dconic[4 * i + 1], a.dL_dconic[4 * i + 3]};
+    const float* view = a.view;
+    f3 t = transformPoint4x3(mean, view);
+    const float limx = 1.3f * a.tan_fovx;
+    const float limy = 1.3f * a.tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+    const float h_x = a.focal_x, h_y = a.focal_y;
+    const mat3 J = mat3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z),
+                             0.0f, h_y / t.z, -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
+    const mat3 Wm = mat3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
+    const mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
+                               cov3D[5]);
+    const mat3 T = mat3_mul(Wm, J);
+    const mat3 cov2D = mat3_mul(mat3_mul(mat3_T(T), mat3_T(Vrk)), T);
+    float c_xx = cov2D.m[0][0];
+    float c_xy = cov2D.m[0][1];
+    float c_yy = cov2D.m[1][1];
+    const float h_var = 0.3f;
+    float d_inside_root = 0.f;
+    if (a.antialiasing) {
+        const float det_cov = c_xx * c_yy - c_xy * c_xy;
+        c_xx += h_var;
+        c_yy += h_var;
+        const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
+        const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
+        const float dL_dopacity_v = a.dL_dopacity[idx];
+        const float d_h_convolution_scaling = dL_dopacity_v * a.opacities[idx];
+        a.dL_dopacity[idx] = dL_dopacity_v * h_convolution_scaling;
+        d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
+                                                                    : d_h_convolution_scaling / (2 * h_convolution_scaling);
+    } else {
+        c_xx += h_var;
+        c_yy += h_var;
+    }
+    float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
+    if (a.antialiasing) {
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float denom_f = d_inside_root / sq(w * w + w * (x + y) + x * y - z * z);
+        dL_dc_xx = w * (w * y + y * y + z * z) * denom_f;
+        dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
+        dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float(*Tm)[3] = T.m;
+    if (denom2inv != 0) {
+        dL_dc_xx += denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
+                                 (denom - c_xx * c_yy) * dL_dconic.z);
+        dL_dc_yy += denom2inv * (-c_xx * c_xx * dL_dconic.z + 2 * c_xx * c_xy * dL_dconic.y +
+                                 (denom - c_xx * c_yy) * dL_dconic.x);
+        dL_dc_xy += denom2inv * 2 *
+                    (c_xy * c_yy * dL_dconic.x - (denom + 2 * c_xy * c_xy) * dL_dconic.y + c_xx * c_xy * dL_dconic.z);
+        dcov[0] = (Tm[0][0] * Tm[0][0] * dL_dc_xx + Tm[0][0] * Tm[1][0] * dL_dc_xy + Tm[1][0] * Tm[1][0] * dL_dc_yy);
+        dcov[3] = (Tm[0][1] * Tm[0][1] * dL_dc_xx + Tm[0][1] * Tm[1][1] * dL_dc_xy + Tm[1][1] * Tm[1][1] * dL_dc_yy);
+        dcov[5] = (Tm[0][2] * Tm[0][2] * dL_dc_xx + Tm[0][2] * Tm[1][2] * dL_dc_xy + Tm[1][2] * Tm[1][2] * dL_dc_yy);
+        dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_dc_xx + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_dc_xy +
+                  2 * Tm[1][0] * Tm[1][1] * dL_dc_yy;
+        dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_dc_xx + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_dc_xy +
+                  2 * Tm[1][0] * Tm[1][2] * dL_dc_yy;
+        dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_dc_xx + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_dc_xy +
+                  2 * Tm[1][1] * Tm[1][2] * dL_dc_yy;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; k++) dcov[k] = 0;
+    }
+    const float(*V)[3] = Vrk.m;
+    const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
+    const float dL_dT01 = 2 * (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_xy;
+    const float dL_dT02 = 2 * (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_xy;
+    const float dL_dT10 = 2 * (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xy;
+    const float dL_dT11 = 2 * (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xy;
+    const float dL_dT12 = 2 * (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xy;
+    const float(*Wq)[3] = Wm.m;
+    const float dL_dJ00 = Wq[0][0] * dL_dT00 + Wq[0][1] * dL_dT01 + Wq[0][2] * dL_dT02;
+    const float dL_dJ02 = Wq[2][0] * dL_dT00 + Wq[2][1] * dL_dT01 + Wq[2][2] * dL_dT02;
+    const float dL_dJ11 = Wq[1][0] * dL_dT10 + Wq[1][1] * dL_dT11 + Wq[1][2] * dL_dT12;
+    const float dL_dJ12 = Wq[2][0] * dL_dT10 + Wq[2][1] * dL_dT11 + Wq[2][2] * dL_dT12;
+    const float tz = 1.f / t.z;
+    const float tz2 = tz * tz;
+    const float tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                   (2 * h_y * t.y) * tz3 * dL_dJ12;
+    if (a.dL_dinvdepth) dL_dtz -= a.dL_dinvdepth[idx] / (t.z * t.z);
+    const f3 dm_cov = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, view);
+    float dmx = dm_cov.x, dmy = dm_cov.y, dmz = dm_cov.z;
+
+    // ---------------- preprocessCUDA (backward.cu:423-440) ----------------
+    {
+        const float* proj = a.proj;
+        const f3 m = mean;
+        const float4 m_hom = transformPoint4x4(m, proj);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        const float g2x = a.dL_dmean2D[3 * i], g2y = a.dL_dmean2D[3 * i + 1];
+        dmx += (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
+        dmy += (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
+        dmz += (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
+    }
+
+    // ---------------- computeColorFromSH backward (backward.cu:23-142) ----------------
+    if (a.shs) {
+        const int deg = a.D;
+        const float* sh = a.shs + i * a.M * 3;
+        const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
+        const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+        const uint8_t cl = a.clamped[idx];
+        float dRGB[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            dRGB[c] = a.dL_dcolor[3 * i + c];
+            dRGB[c] *= (cl >> c) & 1 ? 0 : 1;
+        }
+        float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
+        for (int k = 0; k < a.M * 3; k++) dsh[k] = 0.f;
+#define SETSH(k, coef)                                             \
+    _Pragma("unroll") for (int c = 0; c < 3; c++) dsh[(k) * 3 + c] = (coef) * dRGB[c]
+        const float dRGBdsh0 = SH_C0;
+        SETSH(0, dRGBdsh0);
+        if (deg > 0) {
+            const float dRGBdsh1 = -SH_C1 * y;
+            const float dRGBdsh2 = SH_C1 * z;
+            const float dRGBdsh3 = -SH_C1 * x;
+            SETSH(1, dRGBdsh1);
+            SETSH(2, dRGBdsh2);
+            SETSH(3, dRGBdsh3);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                ddx[c] = -SH_C1 * sh[3 * 3 + c];
+                ddy[c] = -SH_C1 * sh[1 * 3 + c];
+                ddz[c] = SH_C1 * sh[2 * 3 + c];
+            }
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+                SETSH(4, SH_C2_0 * xy);
+                SETSH(5, SH_C2_1 * yz);
+                SETSH(6, SH_C2_2 * (2.f * zz - xx - yy));
+                SETSH(7, SH_C2_3 * xz);
+                SETSH(8, SH_C2_4 * (xx - yy));
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    const float* s = sh + c;
+                    ddx[c] += SH_C2_0 * y * s[4 * 3] + SH_C2_2 * 2.f * -x * s[6 * 3] + SH_C2_3 * z * s[7 * 3] +
+                              SH_C2_4 * 2.f * x * s[8 * 3];
+                    ddy[c] += SH_C2_0 * x * s[4 * 3] + SH_C2_1 * z * s[5 * 3] + SH_C2_2 * 2.f * -y * s[6 * 3] +
+                              SH_C2_4 * 2.f * -y * s[8 * 3];
+                    ddz[c] += SH_C2_1 * y * s[5 * 3] + SH_C2_2 * 2.f * 2.f * z * s[6 * 3] + SH_C2_3 * x * s[7 * 3];
+                }
+                if (deg > 2) {
+                    SETSH(9, SH_C3_0 * y * (3.f * xx - yy));
+                    SETSH(10, SH_C3_1 * xy * z);
+                    SETSH(11, SH_C3_2 * y * (4.f * zz - xx - yy));
+                    SETSH(12, SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy));
+                    SETSH(13, SH_C3_4 * x * (4.f * zz - xx - yy));
+                    SETSH(14, SH_C3_5 * z * (xx - yy));
+                    SETSH(15, SH_C3_6 * x * (xx - 3.f * yy));
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const float* s = sh + c;
+                        ddx[c] += (SH_C3_0 * s[9 * 3] * 3.f * 2.f * xy + SH_C3_1 * s[10 * 3] * yz +
+                                   SH_C3_2 * s[11 * 3] * -2.f * xy + SH_C3_3 * s[12 * 3] * -3.f * 2.f * xz +
+                                   SH_C3_4 * s[13 * 3] * (-3.f * xx + 4.f * zz - yy) +
+                                   SH_C3_5 * s[14 * 3] * 2.f * xz + SH_C3_6 * s[15 * 3] * 3.f * (xx - yy));
+                        ddy[c] += (SH_C3_0 * s[9 * 3] * 3.f * (xx - yy) + SH_C3_1 * s[10 * 3] * xz +
+                                   SH_C3_2 * s[11 * 3] * (-3.f * yy + 4.f * zz - xx) +
+                                   SH_C3_3 * s[12 * 3] * -3.f * 2.f * yz + SH_C3_4 * s[13 * 3] * -2.f * xy +
+                                   SH_C3_5 * s[14 * 3] * -2.f * yz + SH_C3_6 * s[15 * 3] * -3.f * 2.f * xy);
+                        ddz[c] += (SH_C3_1 * s[10 * 3] * xy + SH_C3_2 * s[11 * 3] * 4.f * 2.f * yz +
+                                   SH_C3_3 * s[12 * 3] * 3.f * (2.f * zz - xx - yy) +
+                                   SH_C3_4 * s[13 * 3] * 4.f * 2.f * xz + SH_C3_5 * s[14 * 3] * (xx - yy));
+                    }
+                }
+            }
+        }
+#undef SETSH
+        const f3 dL_ddir = {ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2],
+                            ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2],
+                            ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2]};
+        const f3 dn = dnormvdv(dir_orig, dL_ddir);
+        dmx += dn.x;
+        dmy += dn.y;
+        dmz += dn.z;
+    }
+    dmean[0] = dmx;
+    dmean[1] = dmy;
+    dmean[2] = dmz;
+
+    // ---------------- computeCov3D backward (backward.cu:330-393) ----------------
+    if (a.scales) {
+        const float* rp = a.rotations + 4 * i;
+        const float r = rp[0], x = rp[1], y = rp[2], z = rp[3];
+        const mat3 R = mat3_cols(
+            1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+            2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+            2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+        mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+        const float mod = a.scale_modifier;
+        const f3 s = {mod * a.scales[3 * i], mod * a.scales[3 * i + 1], mod * a.scales[3 * i + 2]};
+        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+        const mat3 M = mat3_mul(S, R);
+        const float* d = dcov;
+        const mat3 dL_dSigma = mat3_cols(d[0], 0.5f * d[1], 0.5f * d[2], 0.5f * d[1], d[3], 0.5f * d[4],
+                                         0.5f * d[2], 0.5f * d[4], d[5]);
+        mat3 M2;
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int w = 0; w < 3; w++) M2.m[c][w] = 2.0f * M.m[c][w];
+        const mat3 dL_dM = mat3_mul(M2, dL_dSigma);
+        const mat3 Rt = mat3_T(R);
+        mat3 G = mat3_T(dL_dM);
+        float* ds = a.dL_dscale + 3 * i;
+        ds[0] = Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2];
+        ds[1] = Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2];
+        ds[2] = Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2];
+#pragma unroll
+        for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
+        const float(*g)[3] = G.m;
+        float4 dq;
+        dq.x = 2 * z * (g[0][1] - g[1][0]) + 2 * y * (g[2][0] - g[0][2]) + 2 * x * (g[1][2] - g[2][1]);
+        dq.y = 2 * y * (g[1][0] + g[0][1]) + 2 * z * (g[2][0] + g[0][2]) + 2 * r * (g[1][2] - g[2][1]) -
+               4 * x * (g[2][2] + g[1][1]);
+        dq.z = 2 * x * (g[1][0] + g[0][1]) + 2 * r * (g[2][0] - g[0][2]) + 2 * z * (g[1][2] + g[2][1]) -
+               4 * y * (g[2][2] + g[0][0]);
+        dq.w = 2 * r * (g[0][1] - g[1][0]) + 2 * x * (g[2][0] + g[0][2]) + 2 * y * (g[1][2] + g[2][1]) -
+               4 * z * (g[1][1] + g[0][0]);
+        float* dr = a.dL_drot + 4 * i;
+        dr[0] = dq.x; dr[1] = dq.y; dr[2] = dq.z; dr[3] = dq.w;
+    } else {
+        if (a.dL_dscale) { a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f; }
+        if (a.dL_drot) { float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f; }
+    }
+}
+
+hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
+{
+    if (a.P <= 0) return hipSuccess;
+    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace gsr

@@ -1,0 +1,217 @@
+"""Host binding of libgsr_hip.so (include/gsr.h) behind the reference's `_C` op surface.
+
+Mirrors the three ops the reference's torch glue exposes
+(diff-gaussian-rasterization-npu/rasterize_points.cu:35-244, bound in ext.cpp:15-19):
+``rasterize_gaussians``, ``rasterize_gaussians_backward`` and ``mark_visible`` -- same
+argument order, same returned tuples, same shape errors.  PyTorch only provides device
+memory and the current HIP stream; all compute runs in the HIP library.  There is no
+CPU fallback: a missing library, a non-GPU tensor or a HIP failure raises.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgsr_hip.so")
+
+_vp, _i, _f, _b, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_bool, ctypes.c_size_t
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"diff_gaussian_rasterization: native library {LIB_PATH} is missing; build it with "
+            "`make -C gaussian-splatting-npu_amd` (or __graft_entry__.build()). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.gsr_last_error.restype = ctypes.c_char_p
+    lib.gsr_version.restype = ctypes.c_char_p
+    for n in ("gsr_geometry_buffer_size", "gsr_binning_buffer_size"):
+        getattr(lib, n).restype = _sz
+        getattr(lib, n).argtypes = [_i]
+    lib.gsr_image_buffer_size.restype = _sz
+    lib.gsr_image_buffer_size.argtypes = [_i, _i]
+    lib.gsr_mark_visible.argtypes = [_i, _vp, _vp, _vp, _vp, _vp]
+    lib.gsr_forward_geometry.argtypes = [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                         _vp, _vp, _f, _f, _b, _b, _vp, _b, _vp, ctypes.POINTER(_i)]
+    lib.gsr_forward_render.argtypes = [_vp, _vp, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _b, _vp]
+    lib.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
+                                 _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                 _vp, _b, _b, _vp]
+    lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
+    for n in ("gsr_geometry_layout", "gsr_binning_layout"):
+        getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
+    lib.gsr_image_layout.argtypes = [_i, _i, ctypes.POINTER(_sz), _i]
+    return lib
+
+
+lib = _load()
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(f"diff_gaussian_rasterization (HIP): {lib.gsr_last_error().decode()} [status {rc}]")
+
+
+def _ptr(t, name, device):
+    """Device pointer of a float32 tensor, or None for an absent (empty) input -- the
+    reference passes `.data<float>()` of `torch.Tensor([])`, i.e. nullptr."""
+    if t is None or t.numel() == 0:
+        return None, None
+    if t.device != device:
+        raise RuntimeError(f"{name} must be on {device}, got {t.device}")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32, got {t.dtype}")
+    t = t.contiguous()
+    return t.data_ptr(), t
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_gpu(t):
+    if t.device.type != "cuda":
+        raise RuntimeError("diff_gaussian_rasterization runs on the GPU only (HIP); got a tensor on "
+                           f"{t.device}. There is no CPU path.")
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered, antialiasing, debug):
+    """RasterizeGaussiansNPU (rasterize_points.cu:35-124)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _require_gpu(means3D)
+    dev = means3D.device
+    P, H, W = means3D.size(0), int(image_height), int(image_width)
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    out_invdepth = torch.zeros((1, H, W), dtype=torch.float32, device=dev)
+    empty = lambda: torch.empty((0,), dtype=torch.uint8, device=dev)  # noqa: E731
+    if P == 0:
+        out_color = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
+        return 0, out_color, radii, empty(), empty(), empty(), out_invdepth
+
+    out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    keep = []
+
+    def p(t, name):
+        ptr, tt = _ptr(t, name, dev)
+        keep.append(tt)
+        return ptr
+
+    geom = torch.empty((lib.gsr_geometry_buffer_size(P),), dtype=torch.uint8, device=dev)
+    img = torch.empty((lib.gsr_image_buffer_size(W, H),), dtype=torch.uint8, device=dev)
+    stream = _stream(dev)
+    nr = ctypes.c_int(0)
+    bg_p, means_p = p(background, "bg"), p(means3D, "means3D")
+    colors_p, op_p = p(colors, "colors_precomp"), p(opacity, "opacities")
+    sc_p, rot_p, cov_p = p(scales, "scales"), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp")
+    vm_p, pm_p = p(viewmatrix, "viewmatrix"), p(projmatrix, "projmatrix")
+    sh_p, cam_p = p(sh, "sh"), p(campos, "campos")
+    _check(lib.gsr_forward_geometry(
+        geom.data_ptr(), img.data_ptr(), P, int(degree), M, W, H, means_p, sh_p, colors_p, op_p, sc_p,
+        float(scale_modifier), rot_p, cov_p, vm_p, pm_p, cam_p, float(tan_fovx), float(tan_fovy),
+        bool(prefiltered), bool(antialiasing), radii.data_ptr(), bool(debug), stream, ctypes.byref(nr)))
+    L = nr.value
+    binning = torch.empty((lib.gsr_binning_buffer_size(L),), dtype=torch.uint8, device=dev)
+    _check(lib.gsr_forward_render(geom.data_ptr(), binning.data_ptr(), img.data_ptr(), P, L, bg_p, W, H, colors_p,
+                                  out_color.data_ptr(), out_invdepth.data_ptr(), radii.data_ptr(), bool(debug),
+                                  stream))
+    return L, out_color, radii, geom, binning, img, out_invdepth
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+                                 dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
+                                 antialiasing, debug):
+    """RasterizeGaussiansBackwardNPU (rasterize_points.cu:126-223)."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    # Render-pass accumulators (zeroed, one allocation): mean2D 3 | colors 3 | conic 4 | opacity 1 | invdepth 1
+    acc = torch.zeros((P * 12,), dtype=torch.float32, device=dev)
+    dL_dmeans2D = acc[0:3 * P].view(P, 3)
+    dL_dcolors = acc[3 * P:6 * P].view(P, 3)
+    dL_dconic = acc[6 * P:10 * P].view(P, 2, 2)
+    dL_dopacity = acc[10 * P:11 * P].view(P, 1)
+    has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
+    dL_dinvdepths = acc[11 * P:12 * P].view(P, 1)
+    # Fully written by the HIP kernel (zeros for culled Gaussians)
+    dL_dmeans3D = torch.empty((P, 3), dtype=torch.float32, device=dev)
+    dL_dcov3D = torch.empty((P, 6), dtype=torch.float32, device=dev)
+    dL_dsh = (torch.empty if M else torch.zeros)((P, M, 3), dtype=torch.float32, device=dev)
+    dL_dscales = torch.empty((P, 3), dtype=torch.float32, device=dev)
+    dL_drotations = torch.empty((P, 4), dtype=torch.float32, device=dev)
+    if P == 0:
+        return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+    keep = []
+
+    def p(t, name):
+        ptr, tt = _ptr(t, name, dev)
+        keep.append(tt)
+        return ptr
+
+    dpix = p(dL_dout_color, "dL_dout_color")
+    dinv = p(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None
+    _check(lib.gsr_backward(
+        P, int(degree), M, int(R), p(background, "bg"), W, H, p(means3D, "means3D"), p(sh, "sh"),
+        p(colors, "colors_precomp"), p(opacities, "opacities"), p(scales, "scales"), float(scale_modifier),
+        p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp"), p(viewmatrix, "viewmatrix"),
+        p(projmatrix, "projmatrix"), p(campos, "campos"), float(tan_fovx), float(tan_fovy), radii.data_ptr(),
+        geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+        dpix, dinv, dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(), dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
+        dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
+        dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(), bool(antialiasing),
+        bool(debug), _stream(dev)))
+    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (rasterize_points.cu:225-244)."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    present = torch.zeros((P,), dtype=torch.bool, device=dev)
+    if P != 0:
+        m, mt = _ptr(means3D, "means3D", dev)
+        v, vt = _ptr(viewmatrix, "viewmatrix", dev)
+        pr, pt = _ptr(projmatrix, "projmatrix", dev)
+        _check(lib.gsr_mark_visible(P, m, v, pr, present.data_ptr(), _stream(dev)))
+    return present
+
+
+# ---- parity/debug introspection (tests only) -------------------------------------------------
+def _layout(fn, *args, n=16):
+    offs = (_sz * n)()
+    cnt = fn(*args, offs, n)
+    return [offs[i] for i in range(cnt + 1)]
+
+
+def geometry_layout(P):
+    return _layout(lib.gsr_geometry_layout, P)
+
+
+def image_layout(W, H):
+    return _layout(lib.gsr_image_layout, W, H)
+
+
+def binning_layout(L):
+    return _layout(lib.gsr_binning_layout, L)
+
+
+def sorted_keys(geomBuffer, binningBuffer, imgBuffer, P, L, W, H):
+    """Sorted tile|depth keys, sorted Gaussian ids and per-tile ranges of the last forward."""
+    dev = geomBuffer.device
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    keys = torch.empty((max(L, 0),), dtype=torch.int64, device=dev)
+    vals = torch.empty((max(L, 0),), dtype=torch.int32, device=dev)
+    ranges = torch.empty((T, 2), dtype=torch.int32, device=dev)
+    _check(lib.gsr_debug_sorted_keys(geomBuffer.data_ptr(), binningBuffer.data_ptr() if L else None,
+                                     imgBuffer.data_ptr(), P, L, W, H, keys.data_ptr() if L else None,
+                                     vals.data_ptr() if L else None, ranges.data_ptr(), _stream(dev)))
+    return keys, vals, ranges

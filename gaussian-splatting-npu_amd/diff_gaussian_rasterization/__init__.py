@@ -1,0 +1,104 @@
+"""MI355X-native drop-in for the reference's ``diff_gaussian_rasterization`` package.
+
+Public surface kept verbatim from diff-gaussian-rasterization-npu/diff_gaussian_rasterization/
+__init__.py: ``GaussianRasterizationSettings`` (:143-156), ``GaussianRasterizer`` (:158-207),
+``rasterize_gaussians`` (:21-42) and the autograd function ``_RasterizeGaussians`` (:44-141), so
+``gaussian_renderer/__init__.py`` (and therefore train.py / render.py) import and call it
+unchanged.  ``SparseGaussianAdam`` is deliberately not exported (the caller would
+then pass a ``dc=`` argument this surface does not take).  All compute is the HIP library
+behind ``_C`` (gfx950); there is no CPU path.
+"""
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+    debug: bool
+    antialiasing: bool
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    """Forward returns (color (3,H,W), radii int32 (P), invdepth (1,H,W)); backward returns the
+    nine input gradients in input order, with d(means2D) = the screen-space gradient (P,3)
+    that the caller's densification statistics read (scene/gaussian_model.py:471-473)."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        s = raster_settings
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepths = _C.rasterize_gaussians(
+            s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+            s.campos, s.prefiltered, s.antialiasing, s.debug)
+        ctx.raster_settings = s
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities,
+                              geomBuffer, binningBuffer, imgBuffer)
+        return color, radii, invdepths
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii, grad_out_depth):
+        s = ctx.raster_settings
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geomBuffer,
+         binningBuffer, imgBuffer) = ctx.saved_tensors
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+         grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(
+            s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth, sh, s.sh_degree,
+            s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug)
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                grad_rotations, grad_cov3Ds_precomp, None)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        """Frustum near-plane test (z_view > 0.2) per point, as a bool tensor, without autograd."""
+        with torch.no_grad():
+            s = self.raster_settings
+            return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        s = self.raster_settings
+        if (shs is None) == (colors_precomp is None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        absent = torch.Tensor([])
+        return rasterize_gaussians(
+            means3D, means2D,
+            absent if shs is None else shs,
+            absent if colors_precomp is None else colors_precomp,
+            opacities,
+            absent if scales is None else scales,
+            absent if rotations is None else rotations,
+            absent if cov3D_precomp is None else cov3D_precomp,
+            s)

@@ -1,0 +1,181 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native differentiable Gaussian-splatting
+ * rasterizer (libgsr_hip.so, built for gfx950).
+ *
+ * This is the drop-in boundary for the reference's native rasterizer
+ * `CudaRasterizer::Rasterizer` (diff-gaussian-rasterization-npu/
+ * cuda_rasterizer/rasterizer.h:20-91).  Argument order and meaning follow the
+ * reference one-for-one; the differences are C-ABI plumbing only:
+ *   - std::function<char*(size_t)> resize lambdas (rasterize_points.cu:27-33)
+ *     become a C function pointer + context (gsr_resize_fn);
+ *   - every entry point takes the HIP stream it must run on (hipStream_t as
+ *     void*; NULL = legacy default stream, as in the reference);
+ *   - errors are returned as an int status (0 = ok) with a thread-local
+ *     message from gsr_last_error(); nothing throws across the ABI.
+ * All data pointers are DEVICE pointers owned by the caller.  Absent optional
+ * inputs are NULL, exactly like `.data<float>()` of the empty tensors the
+ * reference passes (shs / colors_precomp / scales+rotations / cov3D_precomp,
+ * rasterize_points.cu:104-110).  No torch types cross this boundary.
+ */
+#ifndef GSR_H_INCLUDED
+#define GSR_H_INCLUDED
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* gsr_stream_t; /* hipStream_t */
+
+/* Resize callback: must return a device pointer to at least `bytes` bytes
+ * (rasterize_points.cu:27-33 resizeFunctional). */
+typedef char* (*gsr_resize_fn)(void* ctx, size_t bytes);
+
+enum {
+    GSR_OK = 0,
+    GSR_ERR_INVALID = 1,     /* bad argument / shape                          */
+    GSR_ERR_HIP = 2,         /* HIP runtime error (launch, memcpy, sync)      */
+    GSR_ERR_ALLOC = 3,       /* a resize callback returned NULL               */
+    GSR_ERR_PREFILTERED = 4  /* prefiltered=true but a point was near-culled  */
+                             /* (reference: printf + __trap, auxiliary.h:168-172) */
+};
+
+/* Thread-local description of the last error returned on this thread. */
+const char* gsr_last_error(void);
+/* Build identification string ("gsr-hip <version> gfx950"). */
+const char* gsr_version(void);
+
+/* Scratch sizes (bytes) of the three opaque state buffers.  They replace
+ * required<GeometryState/ImageState/BinningState> (rasterizer_impl.h:67-73). */
+size_t gsr_geometry_buffer_size(int P);
+size_t gsr_image_buffer_size(int width, int height);
+size_t gsr_binning_buffer_size(int num_rendered);
+
+/* Replaces Rasterizer::markVisible (rasterizer.h:24-29; kernel
+ * rasterizer_impl.cu:54-66): present[i] = view-space z of point i > 0.2. */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     bool* present, gsr_stream_t stream);
+
+/* Replaces Rasterizer::forward (rasterizer.h:31-55; rasterizer_impl.cu:198-341).
+ * Writes out_color (3,H,W), depth = inverse depth (1,H,W) (may be NULL),
+ * radii (P) (may be NULL: an internal array is used), and *num_rendered. */
+int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx,
+                gsr_resize_fn binningBuffer, void* binning_ctx,
+                gsr_resize_fn imageBuffer, void* image_ctx,
+                int P, int D, int M,
+                const float* background,
+                int width, int height,
+                const float* means3D,
+                const float* shs,
+                const float* colors_precomp,
+                const float* opacities,
+                const float* scales,
+                float scale_modifier,
+                const float* rotations,
+                const float* cov3D_precomp,
+                const float* viewmatrix,
+                const float* projmatrix,
+                const float* cam_pos,
+                float tan_fovx, float tan_fovy,
+                bool prefiltered,
+                float* out_color,
+                float* depth,
+                bool antialiasing,
+                int* radii,
+                bool debug,
+                gsr_stream_t stream,
+                int* num_rendered);
+
+/* Two-phase form of gsr_forward for hosts that own allocation (the Python
+ * package): phase 1 = preprocess + tile-count scan + the one D2H of
+ * num_rendered (rasterizer_impl.cu:250-284) into caller buffers of
+ * gsr_geometry_buffer_size(P) / gsr_image_buffer_size(W,H) bytes; phase 2 =
+ * key emission, tile|depth sort, tile ranges and render
+ * (rasterizer_impl.cu:286-338) with a binning buffer of
+ * gsr_binning_buffer_size(num_rendered) bytes. */
+int gsr_forward_geometry(char* geometry_buffer, char* image_buffer,
+                         int P, int D, int M, int width, int height,
+                         const float* means3D, const float* shs, const float* colors_precomp,
+                         const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                         float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing,
+                         int* radii, bool debug, gsr_stream_t stream, int* num_rendered);
+
+int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_buffer,
+                       int P, int num_rendered, const float* background, int width, int height,
+                       const float* colors_precomp, float* out_color, float* depth, int* radii,
+                       bool debug, gsr_stream_t stream);
+
+/* Replaces Rasterizer::backward (rasterizer.h:57-90; rasterizer_impl.cu:345-450).
+ * dL_dinvdepths / dL_dinvdepth may both be NULL (rasterize_points.cu:174-182).
+ * Accumulated outputs (dL_dmean2D (P,3), dL_dconic (P,2,2), dL_dopacity (P),
+ * dL_dcolor (P,3), dL_dinvdepth (P)) must be zero on entry, as the reference's
+ * glue guarantees (rasterize_points.cu:163-172).  dL_dmean3D, dL_dcov3D,
+ * dL_dsh, dL_dscale, dL_drot are fully written (zeros for culled Gaussians). */
+int gsr_backward(int P, int D, int M, int R,
+                 const float* background,
+                 int width, int height,
+                 const float* means3D,
+                 const float* shs,
+                 const float* colors_precomp,
+                 const float* opacities,
+                 const float* scales,
+                 float scale_modifier,
+                 const float* rotations,
+                 const float* cov3D_precomp,
+                 const float* viewmatrix,
+                 const float* projmatrix,
+                 const float* campos,
+                 float tan_fovx, float tan_fovy,
+                 const int* radii,
+                 char* geom_buffer,
+                 char* binning_buffer,
+                 char* image_buffer,
+                 const float* dL_dpix,
+                 const float* dL_invdepths,
+                 float* dL_dmean2D,
+                 float* dL_dconic,
+                 float* dL_dopacity,
+                 float* dL_dcolor,
+                 float* dL_dinvdepth,
+                 float* dL_dmean3D,
+                 float* dL_dcov3D,
+                 float* dL_dsh,
+                 float* dL_dscale,
+                 float* dL_drot,
+                 bool antialiasing,
+                 bool debug,
+                 gsr_stream_t stream);
+
+/* Debug / parity helper: writes the sorted 64-bit tile|depth keys
+ * (rasterizer_impl.cu:102-104 layout, after the sort of :306-311) and the
+ * sorted Gaussian ids of the last forward held in these buffers. */
+int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffer, const char* image_buffer,
+                          int P, int num_rendered, int width, int height,
+                          uint64_t* keys_out, uint32_t* vals_out, uint32_t* ranges_out,
+                          gsr_stream_t stream);
+
+/* Byte offsets of the arrays inside each opaque state buffer (n entries
+ * written, count of arrays returned; entry [count] is the total size).  For
+ * parity tests and debugging only; the layout is private to this library. */
+int gsr_geometry_layout(int P, size_t* offsets, int n);
+int gsr_image_layout(int width, int height, size_t* offsets, int n);
+int gsr_binning_layout(int num_rendered, size_t* offsets, int n);
+
+/* Per-kernel timing with HIP events recorded on the launch stream (used by
+ * bench.py's roofline measurement).  gsr_profile_enable(1) starts recording
+ * (and resets); gsr_profile_read waits for the recorded events and returns,
+ * per kernel id, the summed milliseconds and launch counts since the last
+ * enable/read.  Both return the number of kernel ids. */
+int gsr_profile_enable(int on);
+int gsr_profile_read(double* total_ms, int* counts, int n);
+const char* gsr_profile_kernel_name(int kernel_id);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H_INCLUDED */

@@ -1,0 +1,211 @@
+"""HIP path vs CPU oracle parity (needs an MI355X: -m gpu).
+
+Every comparison goes through the drop-in surface (diff_gaussian_rasterization -> _C ->
+libgsr_hip.so C ABI).  Preprocess outputs and the sorted tile|depth keys are compared
+bit-exactly; images and gradients with the fp32 tolerances stated in tests/common.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+import common
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+
+
+def _dgr():
+    import diff_gaussian_rasterization as dgr
+    return dgr
+
+
+def _settings(case, antialiasing=False, prefiltered=False, scale_modifier=1.0, debug=False):
+    dgr = _dgr()
+    cam = case["cam"]
+    return dgr.GaussianRasterizationSettings(
+        image_height=case["H"], image_width=case["W"], tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=case["bg"].to(DEV), scale_modifier=scale_modifier, viewmatrix=cam.world_view_transform.to(DEV),
+        projmatrix=cam.full_proj_transform.to(DEV), sh_degree=case["sh_degree"], campos=cam.camera_center.to(DEV),
+        prefiltered=prefiltered, debug=debug, antialiasing=antialiasing)
+
+
+def _inputs(case, mode):
+    sc = case["scene"]
+    t = {k: v.to(DEV).clone().requires_grad_(True) for k, v in sc.items()}
+    kw = dict(means3D=t["means3D"], opacities=t["opacities"])
+    if mode in ("sh_scales", "sh_cov"):
+        kw["shs"] = t["shs"]
+    else:
+        t["colors_precomp"] = case["colors_precomp"].to(DEV).clone().requires_grad_(True)
+        kw["colors_precomp"] = t["colors_precomp"]
+    if mode in ("sh_scales", "colors_scales"):
+        kw["scales"], kw["rotations"] = t["scales"], t["rotations"]
+    else:
+        t["cov3D_precomp"] = case["cov3D_precomp"].to(DEV).clone().requires_grad_(True)
+        kw["cov3D_precomp"] = t["cov3D_precomp"]
+    return t, kw
+
+
+def run_hip(case, mode="sh_scales", antialiasing=False):
+    dgr = _dgr()
+    rast = dgr.GaussianRasterizer(_settings(case, antialiasing))
+    t, kw = _inputs(case, mode)
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    means2D.retain_grad()
+    color, radii, invdepth = rast(means2D=means2D, **kw)
+    loss = (color * case["grad_color"].to(DEV)).sum() + (invdepth * case["grad_invdepth"].to(DEV)).sum()
+    loss.backward()
+    torch.cuda.synchronize()
+    g = {k: v.grad.detach().cpu().numpy() for k, v in t.items()}
+    g["means2D"] = means2D.grad.detach().cpu().numpy()
+    return color.detach().cpu().numpy(), radii.cpu().numpy(), invdepth.detach().cpu().numpy(), g
+
+
+def _with_precomp(case):
+    g = torch.Generator().manual_seed(7)
+    P = case["scene"]["means3D"].shape[0]
+    case["colors_precomp"] = torch.rand(P, 3, generator=g)
+    o, _ = common.run_oracle(case, "sh_scales", backward=False)
+    case["cov3D_precomp"] = torch.from_numpy(o.get("cov3D").copy())
+    return case
+
+
+def _check_image(hip_img, ora_img, name):
+    err = np.abs(hip_img - ora_img)
+    bad = (err > common.IMG_ATOL).reshape(err.shape[0], -1).any(0) if err.ndim == 3 else err > common.IMG_ATOL
+    frac = bad.mean()
+    assert frac <= common.FLIP_FRACTION, f"{name}: {frac:.2e} of pixels differ > {common.IMG_ATOL} (max {err.max():.3e})"
+
+
+@pytest.mark.parametrize("antialiasing", [False, True])
+def test_preprocess_and_keys_bit_exact(antialiasing):
+    """radii, means2D, depth, conic+opacity, rgb, tile counts and the sorted tile|depth keys
+    are bit-identical to the oracle (rasterizer_impl.cu:250-320)."""
+    dgr = _dgr()
+    case = common.make_case()
+    o, _ = common.run_oracle(case, antialiasing=antialiasing, backward=False)
+    s = _settings(case, antialiasing)
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    L, color, radii, geom, binning, img, inv = dgr._C.rasterize_gaussians(
+        s.bg, sc["means3D"], torch.Tensor([]), sc["opacities"], sc["scales"], sc["rotations"], 1.0,
+        torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width,
+        sc["shs"], s.sh_degree, s.campos, False, antialiasing, False)
+    torch.cuda.synchronize()
+    P = sc["means3D"].shape[0]
+    assert L == o.num_rendered
+    r = radii.cpu().numpy()
+    np.testing.assert_array_equal(r, o.radii)
+    vis = r > 0
+    lay = dgr._C.geometry_layout(P)
+    gb = geom.cpu().numpy()
+
+    def arr(i, dt, shape):
+        n = int(np.prod(shape)) * np.dtype(dt).itemsize
+        return gb[lay[i]:lay[i] + n].view(dt).reshape(shape)
+
+    np.testing.assert_array_equal(arr(0, np.uint32, (P,))[vis], o.get("depths").view(np.uint32)[vis])
+    np.testing.assert_array_equal(arr(3, np.uint32, (P, 2))[vis], o.get("means2D").view(np.uint32)[vis])
+    np.testing.assert_array_equal(arr(4, np.uint32, (P, 4))[vis], o.get("conic_opacity").view(np.uint32)[vis])
+    np.testing.assert_array_equal(arr(5, np.uint32, (P, 3))[vis], o.get("rgb").view(np.uint32)[vis])
+    np.testing.assert_array_equal(arr(6, np.uint32, (P,)), o.get("tiles_touched"))
+    keys, vals, ranges = dgr._C.sorted_keys(geom, binning, img, P, L, s.image_width, s.image_height)
+    np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
+    np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+
+
+@pytest.mark.parametrize("mode", ["sh_scales", "colors_scales", "sh_cov", "colors_cov"])
+@pytest.mark.parametrize("antialiasing", [False, True])
+def test_forward_backward_parity(mode, antialiasing):
+    case = _with_precomp(common.make_case())
+    o, og = common.run_oracle(case, mode, antialiasing=antialiasing)
+    color, radii, inv, g = run_hip(case, mode, antialiasing)
+    np.testing.assert_array_equal(radii, o.radii)
+    _check_image(color, o.color, "color")
+    _check_image(inv, o.invdepth, "invdepth")
+    checks = {"means3D": "dL_dmeans3D", "opacities": "dL_dopacity", "means2D": "dL_dmean2D"}
+    if mode.startswith("sh"):
+        checks["shs"] = "dL_dsh"
+    else:
+        checks["colors_precomp"] = "dL_dcolors"
+    if mode.endswith("scales"):
+        checks.update(scales="dL_dscales", rotations="dL_drotations")
+    else:
+        checks["cov3D_precomp"] = "dL_dcov3D"
+    for hk, ok in checks.items():
+        a, b = g[hk], og[ok].reshape(g[hk].shape)
+        ok_, rel = common.allclose_rel(a, b)
+        assert ok_, f"{mode} aa={antialiasing}: grad {hk} rel err {rel:.3e}"
+
+
+def test_1080p_view_properties():
+    """Full-size view: image/grad parity on a 50k-Gaussian 1080p frame (oracle multi-threaded)."""
+    case = common.make_case(P=50000, H=1080, W=1920)
+    o, og = common.run_oracle(case, nthreads=8)
+    color, radii, inv, g = run_hip(case)
+    np.testing.assert_array_equal(radii, o.radii)
+    _check_image(color, o.color, "color")
+    for hk, ok in {"means3D": "dL_dmeans3D", "shs": "dL_dsh", "opacities": "dL_dopacity",
+                   "scales": "dL_dscales", "rotations": "dL_drotations"}.items():
+        ok_, rel = common.allclose_rel(g[hk], og[ok].reshape(g[hk].shape), rtol=5e-4)
+        assert ok_, f"grad {hk} rel err {rel:.3e}"
+
+
+def test_mark_visible():
+    import oracle
+    dgr = _dgr()
+    case = common.make_case()
+    rast = dgr.GaussianRasterizer(_settings(case))
+    vis = rast.markVisible(case["scene"]["means3D"].to(DEV)).cpu().numpy()
+    np.testing.assert_array_equal(vis, oracle.mark_visible(case["scene"]["means3D"], case["cam"].world_view_transform,
+                                                           case["cam"].full_proj_transform))
+
+
+def test_empty_and_all_culled():
+    dgr = _dgr()
+    case = common.make_case(P=10)
+    s = _settings(case)
+    rast = dgr.GaussianRasterizer(s)
+    z = torch.zeros((0, 3), device=DEV)
+    color, radii, inv = rast(means3D=z, means2D=z, opacities=torch.zeros((0, 1), device=DEV),
+                             shs=torch.zeros((0, 16, 3), device=DEV), scales=z, rotations=torch.zeros((0, 4), device=DEV))
+    assert color.shape == (3, case["H"], case["W"]) and float(color.abs().sum()) == 0.0 and radii.numel() == 0
+    # every point behind the camera: nothing rendered, image = background
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    cam_c = case["cam"].camera_center.to(DEV)
+    behind = cam_c + (cam_c - 0.0) * 0.5 + 0.0 * sc["means3D"]
+    color, radii, inv = rast(means3D=behind, means2D=torch.zeros_like(behind), opacities=sc["opacities"],
+                             shs=sc["shs"], scales=sc["scales"], rotations=sc["rotations"])
+    assert int(radii.abs().sum()) == 0
+    assert torch.allclose(color, s.bg.view(3, 1, 1).expand_as(color))
+
+
+def test_prefiltered_violation_raises():
+    dgr = _dgr()
+    case = common.make_case(P=10)
+    s = _settings(case, prefiltered=True)
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    cam_c = case["cam"].camera_center.to(DEV)
+    pts = sc["means3D"].clone()
+    pts[0] = cam_c * 1.5  # behind the camera -> near-culled although prefiltered
+    with pytest.raises(RuntimeError, match="prefiltered"):
+        dgr.GaussianRasterizer(s)(means3D=pts, means2D=torch.zeros_like(pts), opacities=sc["opacities"],
+                                  shs=sc["shs"], scales=sc["scales"], rotations=sc["rotations"])
+
+
+def test_argument_errors_match_reference():
+    dgr = _dgr()
+    case = common.make_case(P=10)
+    rast = dgr.GaussianRasterizer(_settings(case))
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    with pytest.raises(Exception, match="excatly one of either SHs"):
+        rast(means3D=sc["means3D"], means2D=sc["means3D"], opacities=sc["opacities"], scales=sc["scales"],
+             rotations=sc["rotations"])
+    with pytest.raises(Exception, match="scale/rotation pair"):
+        rast(means3D=sc["means3D"], means2D=sc["means3D"], opacities=sc["opacities"], shs=sc["shs"])
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        dgr._C.rasterize_gaussians(sc["means3D"].new_zeros(4), sc["means3D"].new_zeros(4), torch.Tensor([]),
+                                   sc["opacities"], sc["scales"], sc["rotations"], 1.0, torch.Tensor([]),
+                                   sc["means3D"], sc["means3D"], 1.0, 1.0, 8, 8, sc["shs"], 3, sc["means3D"][0],
+                                   False, False, False)
