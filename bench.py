@@ -54,10 +54,10 @@ def algorithmic_bytes(P, M, L, N, T, P_vis):
         "scan": P * 8,
         "duplicate_with_keys": P * 16 + L * 12,                # rect inputs + 12 B key/value per instance
         "sort_pairs": L * 24,                                  # one read + one write of (key, value)
-        "identify_tile_ranges": L * 8 + T * 8,
+        "finalize_ranges": L * 24 + T * 8,                     # sorted key + id out + inverse map + ranges
         "render_fwd": L * 44 + N * 24 + T * 8,                 # id + 40 B record per instance; 24 B/pixel out
-        "render_bwd": L * 44 + N * 24 + P_vis * 48 + T * 8,    # id + record per instance; 24 B/pixel in; 48 B/G grads
-        "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),
+        "render_bwd": L * 44 + N * 24 + T * 8,                 # id + record per instance; 24 B/pixel in
+        "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in
     }
 
 
@@ -95,7 +95,6 @@ def main():
         gc, gi = synthetic.make_grads(H, W, seed=1 + v)
         grads.append((gc.to(dev), gi.to(dev)))
     order = ["means3D", "shs", "opacities", "scales", "rotations"]
-    last_L = [0]
 
     def step():
         for p in params.values():
@@ -107,7 +106,6 @@ def main():
                                      opacities=params["opacities"], scales=params["scales"],
                                      rotations=params["rotations"])
             torch.autograd.backward([color, inv], [gc, gi])
-            last_L[0] = color.grad_fn.num_rendered if hasattr(color.grad_fn, "num_rendered") else last_L[0]
         if world > 1:
             flat = torch.cat([params[k].grad.reshape(-1) for k in order])
             dist.all_reduce(flat)

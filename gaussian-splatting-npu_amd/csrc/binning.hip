@@ -14,7 +14,7 @@ namespace gsr {
 __global__ void __launch_bounds__(256) duplicate_with_keys_kernel(int P, const float2* means2D, const float* depths,
                                                                   const uint32_t* offsets, const int* radii,
                                                                   uint32_t gx, uint32_t gy, uint64_t* keys,
-                                                                  uint32_t* vals)
+                                                                  uint32_t* emit_gid, uint32_t* emit_e)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
@@ -28,15 +28,24 @@ __global__ void __launch_bounds__(256) duplicate_with_keys_kernel(int P, const f
     for (uint32_t y = rminy; y < rmaxy; y++)
         for (uint32_t x = rminx; x < rmaxx; x++) {
             keys[off] = ((uint64_t)(y * gx + x) << 32) | dbits;
-            vals[off] = (uint32_t)idx;
+            emit_gid[off] = (uint32_t)idx;
+            emit_e[off] = off;
             off++;
         }
 }
 
-__global__ void __launch_bounds__(256) identify_tile_ranges_kernel(int L, const uint64_t* keys, uint2* ranges)
+// After the sort: point_list[pos] = Gaussian of the sorted entry, inv[e] = pos (the
+// emission-slot -> sorted-position map the deterministic backward gathers through),
+// and the tile ranges of identifyTileRanges (rasterizer_impl.cu:116-138).
+__global__ void __launch_bounds__(256) finalize_kernel(int L, const uint64_t* keys, const uint32_t* sorted_e,
+                                                       const uint32_t* emit_gid, uint32_t* point_list, uint32_t* inv,
+                                                       uint2* ranges)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= L) return;
+    const uint32_t e = sorted_e[idx];
+    point_list[idx] = emit_gid[e];
+    inv[e] = (uint32_t)idx;
     const uint32_t currtile = (uint32_t)(keys[idx] >> 32);
     if (idx == 0) ranges[currtile].x = 0;
     else {
@@ -59,12 +68,12 @@ size_t sort_scratch_bytes(int L)
 }
 
 hipError_t launch_duplicate_with_keys(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
-                                      const int* radii, uint32_t gx, uint32_t gy, uint64_t* keys, uint32_t* vals,
-                                      hipStream_t s)
+                                      const int* radii, uint32_t gx, uint32_t gy, uint64_t* keys, uint32_t* emit_gid,
+                                      uint32_t* emit_e, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(duplicate_with_keys_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means2D, depths,
-                       offsets, radii, gx, gy, keys, vals);
+                       offsets, radii, gx, gy, keys, emit_gid, emit_e);
     return hipGetLastError();
 }
 
@@ -77,11 +86,13 @@ hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint64_t
                                               s);
 }
 
-hipError_t launch_identify_tile_ranges(int L, const uint64_t* keys, uint2* ranges, int T, hipStream_t s)
+hipError_t launch_finalize(int L, const uint64_t* keys, const uint32_t* sorted_e, const uint32_t* emit_gid,
+                           uint32_t* point_list, uint32_t* inv, uint2* ranges, int T, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);
     if (e != hipSuccess || L <= 0) return e;
-    hipLaunchKernelGGL(identify_tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, keys, ranges);
+    hipLaunchKernelGGL(finalize_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, keys, sorted_e, emit_gid,
+                       point_list, inv, ranges);
     return hipGetLastError();
 }
 

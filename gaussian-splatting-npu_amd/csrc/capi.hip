@@ -68,7 +68,7 @@ enum ProfKernel {
     PK_COUNT
 };
 const char* kProfNames[PK_COUNT] = {"preprocess_fwd", "scan", "duplicate_with_keys", "sort_pairs",
-                                    "identify_tile_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
+                                    "finalize_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
 struct Prof {
     bool on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool[PK_COUNT];
@@ -224,6 +224,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     a.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
     a.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     a.flags = flags;
+    a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     {
         ProfScope ps_(PK_PREPROCESS, s);
         HIP_TRY(launch_preprocess(a, s));
@@ -271,14 +272,17 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
 
     uint64_t* keys_unsorted = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS_UNSORTED]) : nullptr;
     uint64_t* keys = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS]) : nullptr;
-    uint32_t* vals_unsorted = L > 0 ? at<uint32_t>(bb, b.off[BIN_VALS_UNSORTED]) : nullptr;
+    uint32_t* emit_gid = L > 0 ? at<uint32_t>(bb, b.off[BIN_EMIT_GID]) : nullptr;
+    uint32_t* emit_e = L > 0 ? at<uint32_t>(bb, b.off[BIN_EMIT_E]) : nullptr;
+    uint32_t* sorted_e = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_E]) : nullptr;
     uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
+    uint32_t* inv = L > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
     if (L > 0) {
         {
             ProfScope ps_(PK_DUPLICATE, s);
             HIP_TRY(launch_duplicate_with_keys(P, at<float2>(gb, g.off[GEOM_MEANS2D]), at<float>(gb, g.off[GEOM_DEPTH]),
                                                at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), rad, gx, gy, keys_unsorted,
-                                               vals_unsorted, s));
+                                               emit_gid, emit_e, s));
         }
         DEBUG_SYNC(s);
         const int bit = (int)higher_msb(gx * gy);
@@ -286,14 +290,14 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
             ProfScope ps_(PK_SORT, s);
             HIP_TRY(launch_sort_pairs(at<void>(bb, b.off[BIN_SORT_SCRATCH]),
                                       b.off[BIN_SORT_SCRATCH + 1] - b.off[BIN_SORT_SCRATCH], keys_unsorted, keys,
-                                      vals_unsorted, point_list, L, 32 + bit, s));
+                                      emit_e, sorted_e, L, 32 + bit, s));
         }
         DEBUG_SYNC(s);
     }
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     {
         ProfScope ps_(PK_RANGES, s);
-        HIP_TRY(launch_identify_tile_ranges(L, keys, ranges, T, s));
+        HIP_TRY(launch_finalize(L, keys, sorted_e, emit_gid, point_list, inv, ranges, T, s));
     }
     DEBUG_SYNC(s);
 
@@ -301,10 +305,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     r.ranges = ranges;
     r.point_list = point_list;
     r.W = width; r.H = height; r.grid_x = gx;
-    r.means2D = at<float2>(gb, g.off[GEOM_MEANS2D]);
-    r.features = colors_precomp ? colors_precomp : at<float>(gb, g.off[GEOM_RGB]);
-    r.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
-    r.depths = at<float>(gb, g.off[GEOM_DEPTH]);
+    r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.bg = background;
     r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
@@ -374,19 +375,12 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     r.W = width; r.H = height; r.grid_x = gx;
     r.bg = background;
-    r.means2D = at<float2>(gb, g.off[GEOM_MEANS2D]);
-    r.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
-    r.colors = colors_precomp ? colors_precomp : at<float>(gb, g.off[GEOM_RGB]);
-    r.depths = at<float>(gb, g.off[GEOM_DEPTH]);
+    r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
-    r.dL_dmean2D = dL_dmean2D;
-    r.dL_dconic2D = dL_dconic;
-    r.dL_dopacity = dL_dopacity;
-    r.dL_dcolors = dL_dcolor;
-    r.dL_dinvdepths = dL_dinvdepth;
+    r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
     if (R > 0) {
         {
             ProfScope ps_(PK_RENDER_BWD, s);
@@ -407,6 +401,10 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.tan_fovx = tan_fovx; p.tan_fovy = tan_fovy;
     p.campos = campos;
     p.antialiasing = antialiasing;
+    p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
+    p.inv = R > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
+    p.point_offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    p.has_invdepth = dL_invdepths != nullptr;
     p.dL_dmean2D = dL_dmean2D; p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
     p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;

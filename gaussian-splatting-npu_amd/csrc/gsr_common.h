@@ -144,6 +144,7 @@ enum GeomArray {
     GEOM_TILES_TOUCHED,   // u32[P]
     GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched
     GEOM_COV3D,           // f32[6P]
+    GEOM_SPLAT,           // f32x12[P] render record: {x, y, ext_x, ext_y} {conic a, b, c, opacity} {r, g, b, 1/depth}
     GEOM_SCAN_SCRATCH,    // u32[scan blocks + 64]
     GEOM_FLAGS,           // u32[64] error flags / misc
     GEOM_COUNT
@@ -157,10 +158,14 @@ enum ImageArray {
 };
 
 enum BinArray {
-    BIN_KEYS_UNSORTED = 0, // u64[L]
-    BIN_KEYS,              // u64[L]
-    BIN_VALS_UNSORTED,     // u32[L]
-    BIN_POINT_LIST,        // u32[L]
+    BIN_KEYS_UNSORTED = 0, // u64[L] tile|depth keys, emission order
+    BIN_KEYS,              // u64[L] sorted keys
+    BIN_EMIT_GID,          // u32[L] Gaussian id of emission slot e
+    BIN_EMIT_E,            // u32[L] e (sort payload, emission order)
+    BIN_SORTED_E,          // u32[L] emission slot of sorted position
+    BIN_POINT_LIST,        // u32[L] Gaussian id of sorted position
+    BIN_INV,               // u32[L] sorted position of emission slot e
+    BIN_GRAD_INST,         // f32x12[L] per-(tile, Gaussian) gradient record (backward scratch)
     BIN_SORT_SCRATCH,      // bytes
     BIN_COUNT
 };
@@ -174,7 +179,7 @@ struct BinLayout { size_t off[BIN_COUNT + 1]; };
 inline GeomLayout geom_layout(int P)
 {
     size_t p = (size_t)(P > 0 ? P : 0);
-    size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p,
+    size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p, 48 * p,
                                 4 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 64), 4 * 64};
     GeomLayout l;
     size_t o = 0;
@@ -200,7 +205,7 @@ size_t sort_scratch_bytes(int L);
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {8 * n, 8 * n, 4 * n, 4 * n, sort_scratch_bytes(L)};
+    size_t sizes[BIN_COUNT] = {8 * n, 8 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 48 * n, sort_scratch_bytes(L)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

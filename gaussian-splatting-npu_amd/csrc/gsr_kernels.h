@@ -31,6 +31,7 @@ struct PreprocessArgs {
     uint8_t* clamped;
     uint32_t* tiles_touched;
     uint32_t* flags;
+    float4* splat;  // 3 x float4 per Gaussian (GEOM_SPLAT)
 };
 
 struct RenderFwdArgs {
@@ -38,10 +39,7 @@ struct RenderFwdArgs {
     const uint32_t* point_list;
     int W, H;
     uint32_t grid_x;
-    const float2* means2D;
-    const float* features;
-    const float4* conic_opacity;
-    const float* depths;
+    const float4* splat;  // GEOM_SPLAT records (xy+extent, conic+opacity, rgb+1/depth)
     const float* bg;
     float* final_T;
     uint32_t* n_contrib;
@@ -55,20 +53,20 @@ struct RenderBwdArgs {
     int W, H;
     uint32_t grid_x;
     const float* bg;
-    const float2* means2D;
-    const float4* conic_opacity;
-    const float* colors;
-    const float* depths;
+    const float4* splat;
     const float* final_Ts;
     const uint32_t* n_contrib;
     const float* dL_dpixels;
-    const float* dL_invdepths;
-    float* dL_dmean2D;   // (P,3)
-    float* dL_dconic2D;  // (P,4)
-    float* dL_dopacity;  // (P)
-    float* dL_dcolors;   // (P,3)
-    float* dL_dinvdepths;  // (P) or null
+    const float* dL_invdepths;  // (1,H,W) or null
+    float* grad_inst;           // f32x12[L]: one gradient record per sorted (tile, Gaussian) entry
 };
+
+// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).
+enum GradField {
+    GF_MEAN2D_X = 0, GF_MEAN2D_Y, GF_CONIC_A, GF_CONIC_B, GF_CONIC_C, GF_OPACITY, GF_COLOR_R, GF_COLOR_G,
+    GF_COLOR_B, GF_INVDEPTH, GF_NUM
+};
+constexpr int GRAD_REC = 12;
 
 struct PreprocessBwdArgs {
     int P, D, M;
@@ -86,11 +84,17 @@ struct PreprocessBwdArgs {
     float focal_x, focal_y, tan_fovx, tan_fovy;
     const float* campos;
     int antialiasing;
-    const float* dL_dmean2D;
-    const float* dL_dconic;
-    const float* dL_dinvdepth;
-    float* dL_dopacity;
-    float* dL_dcolor;
+    // per-instance gradient records and the gather map
+    const float* grad_inst;         // f32x12[L] sorted order
+    const uint32_t* inv;            // sorted position of emission slot e
+    const uint32_t* point_offsets;  // inclusive scan of tiles_touched (emission slots of Gaussian i)
+    int has_invdepth;
+    // reduced per-Gaussian render gradients (fully written; outputs of the reference glue)
+    float* dL_dmean2D;   // (P,3)
+    float* dL_dconic;    // (P,4)
+    float* dL_dinvdepth; // (P) or null
+    float* dL_dopacity;  // (P)
+    float* dL_dcolor;    // (P,3)
     float* dL_dmean3D;
     float* dL_dcov3D;
     float* dL_dsh;
@@ -104,10 +108,11 @@ hipError_t launch_inclusive_scan(const uint32_t* in, uint32_t* out, int n, uint3
 
 hipError_t launch_duplicate_with_keys(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
                                       const int* radii, uint32_t gx, uint32_t gy, uint64_t* keys,
-                                      uint32_t* vals, hipStream_t s);
+                                      uint32_t* emit_gid, uint32_t* emit_e, hipStream_t s);
 hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
                              const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit, hipStream_t s);
-hipError_t launch_identify_tile_ranges(int L, const uint64_t* keys, uint2* ranges, int T, hipStream_t s);
+hipError_t launch_finalize(int L, const uint64_t* keys, const uint32_t* sorted_e, const uint32_t* emit_gid,
+                           uint32_t* point_list, uint32_t* inv, uint2* ranges, int T, hipStream_t s);
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);

@@ -159,21 +159,38 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
     getRect(pix_x, pix_y, (int)my_radius, a.grid_x, a.grid_y, rminx, rminy, rmaxx, rmaxy);
     if ((rmaxx - rminx) * (rmaxy - rminy) == 0) return;
 
+    f3 rgb;
     if (!a.colors_precomp) {
         uint8_t cl;
-        const f3 rgb = computeColorFromSH(p_orig, a.D, a.shs + (size_t)idx * a.M * 3, a.campos, cl);
+        rgb = computeColorFromSH(p_orig, a.D, a.shs + (size_t)idx * a.M * 3, a.campos, cl);
         a.rgb[3 * (size_t)idx + 0] = rgb.x;
         a.rgb[3 * (size_t)idx + 1] = rgb.y;
         a.rgb[3 * (size_t)idx + 2] = rgb.z;
         a.clamped[idx] = cl;
+    } else {
+        const float* c = a.colors_precomp + 3 * (size_t)idx;
+        rgb = {c[0], c[1], c[2]};
     }
     a.depths[idx] = p_view.z;
     a.radii[idx] = (int)my_radius;
     reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
-    const float opacity = a.opacities[idx];
-    reinterpret_cast<float4*>(a.conic_opacity)[idx] =
-        make_float4(conic_x, conic_y, conic_z, opacity * h_convolution_scaling);
+    const float opacity = a.opacities[idx] * h_convolution_scaling;
+    reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
+
+    // Render record.  cullK bounds the ellipse d^T Q d <= K = 2 ln(255 opacity) outside which
+    // alpha = opacity * exp(power) < 1/255 (Q = the fp32 conic the render kernels evaluate),
+    // widened by a margin far above the fp32 rounding of `power`.  The render kernels use it
+    // only to skip (Gaussian, 8x8-quadrant) pairs in which no pixel can pass the reference's
+    // alpha >= 1/255 test (forward.cu:364, backward.cu:570), so results are unchanged.
+    // Opacity below 1/255 can never pass: cullK < 0 culls everywhere.
+    float cullK = -1.0f;
+    if (opacity >= 1.0f / 255.0f) cullK = (float)(2.0 * log(255.0 * (double)opacity) * 1.002 + 0.02);
+    if (!(conic_x > 0.f && conic_z > 0.f && conic_x * conic_z - conic_y * conic_y > 0.f)) cullK = 3.0e38f;
+    float4* sp = a.splat + 3 * (size_t)idx;
+    sp[0] = make_float4(pix_x, pix_y, cullK, 0.0f);
+    sp[1] = make_float4(conic_x, conic_y, conic_z, opacity);
+    sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
 }
 
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,

@@ -23,6 +23,12 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     float* dsh = a.dL_dsh ? a.dL_dsh + i * a.M * 3 : nullptr;
 
     if (!(a.radii[idx] > 0)) {
+        a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
+        a.dL_dconic[4 * i] = 0.f; a.dL_dconic[4 * i + 1] = 0.f; a.dL_dconic[4 * i + 2] = 0.f;
+        a.dL_dconic[4 * i + 3] = 0.f;
+        a.dL_dopacity[i] = 0.f;
+        a.dL_dcolor[3 * i] = 0.f; a.dL_dcolor[3 * i + 1] = 0.f; a.dL_dcolor[3 * i + 2] = 0.f;
+        if (a.dL_dinvdepth) a.dL_dinvdepth[i] = 0.f;
         dmean[0] = 0.f; dmean[1] = 0.f; dmean[2] = 0.f;
 #pragma unroll
         for (int k = 0; k < 6; k++) dcov[k] = 0.f;
@@ -33,10 +39,32 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         return;
     }
 
+    // ------- gather this Gaussian's per-tile gradient records (deterministic order) -------
+    float g[GF_NUM];
+#pragma unroll
+    for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
+    {
+        const uint32_t e0 = idx == 0 ? 0u : a.point_offsets[idx - 1];
+        const uint32_t e1 = a.point_offsets[idx];
+        for (uint32_t e = e0; e < e1; e++) {
+            const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)a.inv[e] * GRAD_REC);
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+            g[0] += r0.x; g[1] += r0.y; g[2] += r0.z; g[3] += r0.w;
+            g[4] += r1.x; g[5] += r1.y; g[6] += r1.z; g[7] += r1.w;
+            g[8] += r2.x; g[9] += r2.y;
+        }
+    }
+    // render-pass gradients of the reference glue (rasterize_points.cu:164-172), fully written
+    a.dL_dmean2D[3 * i] = g[GF_MEAN2D_X]; a.dL_dmean2D[3 * i + 1] = g[GF_MEAN2D_Y]; a.dL_dmean2D[3 * i + 2] = 0.f;
+    a.dL_dconic[4 * i] = g[GF_CONIC_A]; a.dL_dconic[4 * i + 1] = g[GF_CONIC_B]; a.dL_dconic[4 * i + 2] = 0.f;
+    a.dL_dconic[4 * i + 3] = g[GF_CONIC_C];
+    a.dL_dcolor[3 * i] = g[GF_COLOR_R]; a.dL_dcolor[3 * i + 1] = g[GF_COLOR_G]; a.dL_dcolor[3 * i + 2] = g[GF_COLOR_B];
+    if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
+
     // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
     const float* cov3D = a.cov3Ds + 6 * i;
     const f3 mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
-    const f3 dL_dconic = {a.dL_dconic[4 * i], a.dL_dconic[4 * i + 1], a.dL_dconic[4 * i + 3]};
+    const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
     const float* view = a.view;
     f3 t = transformPoint4x3(mean, view);
     const float limx = 1.3f * a.tan_fovx;
@@ -66,7 +94,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         c_yy += h_var;
         const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
         const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
-        const float dL_dopacity_v = a.dL_dopacity[idx];
+        const float dL_dopacity_v = g[GF_OPACITY];
         const float d_h_convolution_scaling = dL_dopacity_v * a.opacities[idx];
         a.dL_dopacity[idx] = dL_dopacity_v * h_convolution_scaling;
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
@@ -74,6 +102,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     } else {
         c_xx += h_var;
         c_yy += h_var;
+        a.dL_dopacity[idx] = g[GF_OPACITY];
     }
     float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
     if (a.antialiasing) {
@@ -131,7 +160,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
     float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
                    (2 * h_y * t.y) * tz3 * dL_dJ12;
-    if (a.dL_dinvdepth) dL_dtz -= a.dL_dinvdepth[idx] / (t.z * t.z);
+    if (a.has_invdepth) dL_dtz -= g[GF_INVDEPTH] / (t.z * t.z);
     const f3 dm_cov = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, view);
     float dmx = dm_cov.x, dmy = dm_cov.y, dmz = dm_cov.z;
 
@@ -143,7 +172,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         const float m_w = 1.0f / (m_hom.w + 0.0000001f);
         const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
         const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        const float g2x = a.dL_dmean2D[3 * i], g2y = a.dL_dmean2D[3 * i + 1];
+        const float g2x = g[GF_MEAN2D_X], g2y = g[GF_MEAN2D_Y];
         dmx += (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
         dmy += (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
         dmz += (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
@@ -160,7 +189,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         float dRGB[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-            dRGB[c] = a.dL_dcolor[3 * i + c];
+            dRGB[c] = g[GF_COLOR_R + c];
             dRGB[c] *= (cl >> c) & 1 ? 0 : 1;
         }
         float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
@@ -268,15 +297,15 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         ds[2] = Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2];
 #pragma unroll
         for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
-        const float(*g)[3] = G.m;
+        const float(*gm)[3] = G.m;
         float4 dq;
-        dq.x = 2 * z * (g[0][1] - g[1][0]) + 2 * y * (g[2][0] - g[0][2]) + 2 * x * (g[1][2] - g[2][1]);
-        dq.y = 2 * y * (g[1][0] + g[0][1]) + 2 * z * (g[2][0] + g[0][2]) + 2 * r * (g[1][2] - g[2][1]) -
-               4 * x * (g[2][2] + g[1][1]);
-        dq.z = 2 * x * (g[1][0] + g[0][1]) + 2 * r * (g[2][0] - g[0][2]) + 2 * z * (g[1][2] + g[2][1]) -
-               4 * y * (g[2][2] + g[0][0]);
-        dq.w = 2 * r * (g[0][1] - g[1][0]) + 2 * x * (g[2][0] + g[0][2]) + 2 * y * (g[1][2] + g[2][1]) -
-               4 * z * (g[1][1] + g[0][0]);
+        dq.x = 2 * z * (gm[0][1] - gm[1][0]) + 2 * y * (gm[2][0] - gm[0][2]) + 2 * x * (gm[1][2] - gm[2][1]);
+        dq.y = 2 * y * (gm[1][0] + gm[0][1]) + 2 * z * (gm[2][0] + gm[0][2]) + 2 * r * (gm[1][2] - gm[2][1]) -
+               4 * x * (gm[2][2] + gm[1][1]);
+        dq.z = 2 * x * (gm[1][0] + gm[0][1]) + 2 * r * (gm[2][0] - gm[0][2]) + 2 * z * (gm[1][2] + gm[2][1]) -
+               4 * y * (gm[2][2] + gm[0][0]);
+        dq.w = 2 * r * (gm[0][1] - gm[1][0]) + 2 * x * (gm[2][0] + gm[0][2]) + 2 * y * (gm[1][2] + gm[2][1]) -
+               4 * z * (gm[1][1] + gm[0][0]);
         float* dr = a.dL_drot + 4 * i;
         dr[0] = dq.x; dr[1] = dq.y; dr[2] = dq.z; dr[3] = dq.w;
     } else {

@@ -132,8 +132,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
     M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
-    # Render-pass accumulators (zeroed, one allocation): mean2D 3 | colors 3 | conic 4 | opacity 1 | invdepth 1
-    acc = torch.zeros((P * 12,), dtype=torch.float32, device=dev)
+    # Render-pass gradients (one allocation): mean2D 3 | colors 3 | conic 4 | opacity 1 | invdepth 1.
+    # The HIP backward writes every element (no atomics, no pre-zeroing needed).
+    acc = torch.empty((P * 12,), dtype=torch.float32, device=dev)
     dL_dmeans2D = acc[0:3 * P].view(P, 3)
     dL_dcolors = acc[3 * P:6 * P].view(P, 3)
     dL_dconic = acc[6 * P:10 * P].view(P, 2, 2)

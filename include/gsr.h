@@ -112,10 +112,12 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
 
 /* Replaces Rasterizer::backward (rasterizer.h:57-90; rasterizer_impl.cu:345-450).
  * dL_dinvdepths / dL_dinvdepth may both be NULL (rasterize_points.cu:174-182).
- * Accumulated outputs (dL_dmean2D (P,3), dL_dconic (P,2,2), dL_dopacity (P),
- * dL_dcolor (P,3), dL_dinvdepth (P)) must be zero on entry, as the reference's
- * glue guarantees (rasterize_points.cu:163-172).  dL_dmean3D, dL_dcov3D,
- * dL_dsh, dL_dscale, dL_drot are fully written (zeros for culled Gaussians). */
+ * Every output is fully written (zeros for culled Gaussians), so unlike the
+ * reference glue (rasterize_points.cu:163-182) the caller need not zero them.
+ * The render-pass gradients (dL_dmean2D (P,3), dL_dconic (P,2,2),
+ * dL_dopacity (P), dL_dcolor (P,3), dL_dinvdepth (P)) are reduced on chip and
+ * gathered per Gaussian in a fixed order: results are bitwise reproducible
+ * run to run (the reference sums with float atomics). */
 int gsr_backward(int P, int D, int M, int R,
                  const float* background,
                  int width, int height,

@@ -57,7 +57,7 @@ def run_hip(case, mode="sh_scales", antialiasing=False):
     loss = (color * case["grad_color"].to(DEV)).sum() + (invdepth * case["grad_invdepth"].to(DEV)).sum()
     loss.backward()
     torch.cuda.synchronize()
-    g = {k: v.grad.detach().cpu().numpy() for k, v in t.items()}
+    g = {k: v.grad.detach().cpu().numpy() for k, v in t.items() if v.grad is not None}
     g["means2D"] = means2D.grad.detach().cpu().numpy()
     return color.detach().cpu().numpy(), radii.cpu().numpy(), invdepth.detach().cpu().numpy(), g
 
