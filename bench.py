@@ -50,11 +50,12 @@ def algorithmic_bytes(P, M, L, N, T, P_vis):
     """Compulsory HBM bytes per launch of each kernel (split per kernel)."""
     params = 4 * (11 + 3 * M)  # means 12 + scales 12 + rot 16 + opacity 4 + SH 12M
     return {
-        "preprocess_fwd": P * params + P_vis * 44 + P * 4,     # params in; 44 B splat record + tile count out
-        "scan": P * 8,
-        "duplicate_with_keys": P * 16 + L * 12,                # rect inputs + 12 B key/value per instance
-        "sort_pairs": L * 24,                                  # one read + one write of (key, value)
-        "finalize_ranges": L * 24 + T * 8,                     # sorted key + id out + inverse map + ranges
+        "preprocess_fwd": P * params + P_vis * 44 + P * 8,     # params in; 44 B splat record + count + key out
+        "depth_sort": P * 8,                                   # depth key in, sorted id out
+        "scan": P * 12,                                        # sorted id + gathered count in, offset out
+        "emit_instances": P * 24 + L * 8,                      # per-Gaussian rect inputs; (tile, id) per instance
+        "tile_sort": L * 20,                                   # (tile, id) in; id + tile + inverse slot out
+        "tile_ranges": L * 4 + T * 8,
         "render_fwd": L * 44 + N * 24 + T * 8,                 # id + 40 B record per instance; 24 B/pixel out
         "render_bwd": L * 44 + N * 24 + T * 8,                 # id + record per instance; 24 B/pixel in
         "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in

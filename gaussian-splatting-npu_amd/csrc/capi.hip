@@ -64,11 +64,12 @@ int pinned(uint32_t** out)
 // launch when on.
 // ---------------------------------------------------------------------------
 enum ProfKernel {
-    PK_PREPROCESS = 0, PK_SCAN, PK_DUPLICATE, PK_SORT, PK_RANGES, PK_RENDER_FWD, PK_RENDER_BWD, PK_PREPROCESS_BWD,
+    PK_PREPROCESS = 0, PK_DEPTH_SORT, PK_SCAN, PK_EMIT, PK_TILE_SORT, PK_RANGES, PK_RENDER_FWD, PK_RENDER_BWD,
+    PK_PREPROCESS_BWD,
     PK_COUNT
 };
-const char* kProfNames[PK_COUNT] = {"preprocess_fwd", "scan", "duplicate_with_keys", "sort_pairs",
-                                    "finalize_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
+const char* kProfNames[PK_COUNT] = {"preprocess_fwd", "depth_sort", "scan", "emit_instances", "tile_sort",
+                                    "tile_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
 struct Prof {
     bool on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool[PK_COUNT];
@@ -180,6 +181,7 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return GSR_OK;
 }
 
+
 int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
                          const float* means3D, const float* shs, const float* colors_precomp,
                          const float* opacities, const float* scales, float scale_modifier,
@@ -204,6 +206,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* flags = at<uint32_t>(gb, g.off[GEOM_FLAGS]);
     HIP_TRY(hipMemsetAsync(flags, 0, 256, s));
 
+    // 1. preprocess (forward.cu:154-272)
     PreprocessArgs a;
     a.P = P; a.D = D; a.M = M; a.W = width; a.H = height;
     a.means3D = means3D; a.scales = scales; a.scale_modifier = scale_modifier; a.rotations = rotations;
@@ -225,27 +228,47 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     a.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     a.flags = flags;
     a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
+    a.dkey = at<uint32_t>(gb, g.off[GEOM_DKEY]);
     {
         ProfScope ps_(PK_PREPROCESS, s);
         HIP_TRY(launch_preprocess(a, s));
     }
     DEBUG_SYNC(s);
 
-    uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    // 2. stable depth sort of the Gaussians (first half of the reference's tile|depth key sort)
+    uint32_t* sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
     {
-        ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(a.tiles_touched, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]), s));
+        char* tmp = gb + g.off[GEOM_DSORT_TMP];
+        const size_t p = (size_t)P;
+        uint32_t* k0 = reinterpret_cast<uint32_t*>(tmp);
+        uint2* v0 = reinterpret_cast<uint2*>(tmp + align_up(4 * p, 256));
+        uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + align_up(4 * p, 256) + align_up(8 * p, 256));
+        uint2* v1 = reinterpret_cast<uint2*>(tmp + 2 * align_up(4 * p, 256) + align_up(8 * p, 256));
+        ProfScope ps_(PK_DEPTH_SORT, s);
+        HIP_TRY(radix_sort(P, DEPTH_PASSES, a.dkey, nullptr, k0, v0, k1, v1, nullptr, nullptr, sorted_ids, nullptr,
+                           nullptr, gb + g.off[GEOM_RADIX_SCRATCH], flags + 1, s));
     }
     DEBUG_SYNC(s);
 
+    // 3. instance offsets in depth order (cub::DeviceScan::InclusiveSum, rasterizer_impl.cu:280)
+    uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    {
+        ProfScope ps_(PK_SCAN, s);
+        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]),
+                                      s));
+    }
+    DEBUG_SYNC(s);
+
+    // 4. the one D2H of the forward: num_rendered (rasterizer_impl.cu:283-284), plus error flags
     uint32_t* h;
     int rc = pinned(&h);
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(h, offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h + 1, flags, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h + 1, flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     if (h[1] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (h[2]) return fail(GSR_ERR_HIP, "radix sort look-back did not complete");
     if (h[0] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
     *num_rendered = (int)h[0];
     return GSR_OK;
@@ -255,6 +278,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
                        const float* background, int width, int height, const float* colors_precomp,
                        float* out_color, float* depth, int* radii, bool debug, gsr_stream_t stream)
 {
+    (void)colors_precomp;  // folded into the render record by preprocess
     hipStream_t s = (hipStream_t)stream;
     if (P <= 0) return GSR_OK;
     const int L = num_rendered;
@@ -269,35 +293,42 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     const int T = (int)(gx * gy);
     const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
-
-    uint64_t* keys_unsorted = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS_UNSORTED]) : nullptr;
-    uint64_t* keys = L > 0 ? at<uint64_t>(bb, b.off[BIN_KEYS]) : nullptr;
-    uint32_t* emit_gid = L > 0 ? at<uint32_t>(bb, b.off[BIN_EMIT_GID]) : nullptr;
-    uint32_t* emit_e = L > 0 ? at<uint32_t>(bb, b.off[BIN_EMIT_E]) : nullptr;
-    uint32_t* sorted_e = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_E]) : nullptr;
+    uint32_t* flags = at<uint32_t>(gb, g.off[GEOM_FLAGS]);
     uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
+    uint32_t* sorted_tiles = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr;
     uint32_t* inv = L > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
+    uint32_t* emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     if (L > 0) {
+        // emission arrays and sort ping-pong live in the (not yet used) gradient-record region
+        const size_t n = (size_t)L;
+        char* w = bb + b.off[BIN_GRAD_INST];
+        uint32_t* tile_keys = reinterpret_cast<uint32_t*>(w);
+        uint32_t* gids = reinterpret_cast<uint32_t*>(w + align_up(4 * n, 256));
+        uint32_t* k0 = reinterpret_cast<uint32_t*>(w + 2 * align_up(4 * n, 256));
+        uint2* v0 = reinterpret_cast<uint2*>(w + 3 * align_up(4 * n, 256));
+        uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * align_up(4 * n, 256) + align_up(8 * n, 256));
+        uint2* v1 = reinterpret_cast<uint2*>(w + 4 * align_up(4 * n, 256) + align_up(8 * n, 256));
         {
-            ProfScope ps_(PK_DUPLICATE, s);
-            HIP_TRY(launch_duplicate_with_keys(P, at<float2>(gb, g.off[GEOM_MEANS2D]), at<float>(gb, g.off[GEOM_DEPTH]),
-                                               at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), rad, gx, gy, keys_unsorted,
-                                               emit_gid, emit_e, s));
+            ProfScope ps_(PK_EMIT, s);
+            HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
+                                          at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), at<float2>(gb, g.off[GEOM_MEANS2D]),
+                                          rad, gx, gy, tile_keys, gids, emit_start, s));
         }
         DEBUG_SYNC(s);
+        // stable sort by tile id over bits [0, bit) (rasterizer_impl.cu:303-311 sorts [0, 32+bit))
         const int bit = (int)higher_msb(gx * gy);
+        const int npass = bit <= 8 ? 1 : (bit + 7) / 8;
         {
-            ProfScope ps_(PK_SORT, s);
-            HIP_TRY(launch_sort_pairs(at<void>(bb, b.off[BIN_SORT_SCRATCH]),
-                                      b.off[BIN_SORT_SCRATCH + 1] - b.off[BIN_SORT_SCRATCH], keys_unsorted, keys,
-                                      emit_e, sorted_e, L, 32 + bit, s));
+            ProfScope ps_(PK_TILE_SORT, s);
+            HIP_TRY(radix_sort(L, npass, tile_keys, gids, k0, v0, k1, v1, nullptr, nullptr, point_list, inv,
+                               sorted_tiles, bb + b.off[BIN_RADIX_SCRATCH], flags + 1, s));
         }
         DEBUG_SYNC(s);
     }
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     {
         ProfScope ps_(PK_RANGES, s);
-        HIP_TRY(launch_finalize(L, keys, sorted_e, emit_gid, point_list, inv, ranges, T, s));
+        HIP_TRY(launch_tile_ranges(L, sorted_tiles, ranges, T, s));
     }
     DEBUG_SYNC(s);
 
@@ -316,6 +347,14 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
         HIP_TRY(launch_render_fwd(r, T, s));
     }
     DEBUG_SYNC(s);
+    if (debug) {
+        uint32_t* h;
+        int rc = pinned(&h);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpyAsync(h, flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h[0]) return fail(GSR_ERR_HIP, "radix sort look-back did not complete");
+    }
     return GSR_OK;
 }
 
@@ -355,6 +394,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
                  float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
                  float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
 {
+    (void)colors_precomp;
     hipStream_t s = (hipStream_t)stream;
     if (P <= 0) return GSR_OK;
     const GeomLayout g = geom_layout(P);
@@ -363,13 +403,15 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     char* gb = geom_buffer;
     char* ib = image_buffer;
     char* bb = binning_buffer;
+    if (R > 0 && !bb) return fail(GSR_ERR_ALLOC, "null binning buffer");
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     const int T = (int)(gx * gy);
     const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
-    if ((dL_invdepths == nullptr) != (dL_dinvdepth == nullptr))
-        return fail(GSR_ERR_INVALID, "dL_invdepths and dL_dinvdepth must both be given or both NULL");
+    if ((dL_invdepths == nullptr) != (dL_dinvdepth == nullptr) && dL_dinvdepth == nullptr)
+        return fail(GSR_ERR_INVALID, "dL_dinvdepth must be given with dL_invdepths");
 
+    // BACKWARD::render (rasterizer_impl.cu:399-418): per-(tile, Gaussian) gradient records
     RenderBwdArgs r;
     r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
@@ -389,6 +431,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         DEBUG_SYNC(s);
     }
 
+    // BACKWARD::preprocess (rasterizer_impl.cu:423-449), with the per-Gaussian gather of the records
     PreprocessBwdArgs p;
     p.P = P; p.D = D; p.M = M;
     p.means3D = means3D; p.radii = rad; p.shs = shs;
@@ -403,7 +446,8 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.antialiasing = antialiasing;
     p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
     p.inv = R > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
-    p.point_offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+    p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     p.has_invdepth = dL_invdepths != nullptr;
     p.dL_dmean2D = dL_dmean2D; p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
@@ -422,18 +466,18 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
                           uint32_t* ranges_out, gsr_stream_t stream)
 {
     hipStream_t s = (hipStream_t)stream;
-    (void)geometry_buffer; (void)P;
+    const GeomLayout g = geom_layout(P);
     const BinLayout b = bin_layout(num_rendered);
     const ImageLayout im = image_layout(width, height);
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     if (num_rendered > 0) {
+        const uint32_t* point_list = at<uint32_t>(binning_buffer, b.off[BIN_POINT_LIST]);
         if (keys_out)
-            HIP_TRY(hipMemcpyAsync(keys_out, binning_buffer + b.off[BIN_KEYS], 8 * (size_t)num_rendered,
-                                   hipMemcpyDeviceToDevice, s));
+            HIP_TRY(launch_debug_keys(num_rendered, at<uint32_t>(binning_buffer, b.off[BIN_SORTED_TILES]), point_list,
+                                      at<float>(geometry_buffer, g.off[GEOM_DEPTH]), keys_out, s));
         if (vals_out)
-            HIP_TRY(hipMemcpyAsync(vals_out, binning_buffer + b.off[BIN_POINT_LIST], 4 * (size_t)num_rendered,
-                                   hipMemcpyDeviceToDevice, s));
+            HIP_TRY(hipMemcpyAsync(vals_out, point_list, 4 * (size_t)num_rendered, hipMemcpyDeviceToDevice, s));
     }
     if (ranges_out)
         HIP_TRY(hipMemcpyAsync(ranges_out, image_buffer + im.off[IMG_RANGES], 8 * (size_t)gx * gy,

@@ -142,9 +142,14 @@ enum GeomArray {
     GEOM_CONIC_OPACITY,   // f32x4[P]
     GEOM_RGB,             // f32[3P]
     GEOM_TILES_TOUCHED,   // u32[P]
-    GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched
+    GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched in depth order
     GEOM_COV3D,           // f32[6P]
-    GEOM_SPLAT,           // f32x12[P] render record: {x, y, ext_x, ext_y} {conic a, b, c, opacity} {r, g, b, 1/depth}
+    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {conic a, b, c, opacity} {r, g, b, 1/depth}
+    GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
+    GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
+    GEOM_EMIT_START,      // u32[P] first emission slot of each Gaussian
+    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, u32x2[P] v0, u32[P] k1, u32x2[P] v1
+    GEOM_RADIX_SCRATCH,   // look-back status + histograms of the depth sort
     GEOM_SCAN_SCRATCH,    // u32[scan blocks + 64]
     GEOM_FLAGS,           // u32[64] error flags / misc
     GEOM_COUNT
@@ -158,28 +163,30 @@ enum ImageArray {
 };
 
 enum BinArray {
-    BIN_KEYS_UNSORTED = 0, // u64[L] tile|depth keys, emission order
-    BIN_KEYS,              // u64[L] sorted keys
-    BIN_EMIT_GID,          // u32[L] Gaussian id of emission slot e
-    BIN_EMIT_E,            // u32[L] e (sort payload, emission order)
-    BIN_SORTED_E,          // u32[L] emission slot of sorted position
-    BIN_POINT_LIST,        // u32[L] Gaussian id of sorted position
-    BIN_INV,               // u32[L] sorted position of emission slot e
-    BIN_GRAD_INST,         // f32x12[L] per-(tile, Gaussian) gradient record (backward scratch)
-    BIN_SORT_SCRATCH,      // bytes
+    BIN_POINT_LIST = 0,   // u32[L] Gaussian id of sorted position
+    BIN_SORTED_TILES,     // u32[L] tile id of sorted position
+    BIN_INV,              // u32[L] sorted position of emission slot e
+    BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
+                          // it hosts the emission arrays and sort ping-pong buffers (32 B/instance)
+    BIN_RADIX_SCRATCH,    // look-back status + histograms of the tile sort
     BIN_COUNT
 };
 
 constexpr int SCAN_ITEMS = 4096;  // items per scan block (256 threads x 16)
+constexpr int DEPTH_PASSES = 4;   // 32-bit depth keys
+constexpr int MAX_TILE_PASSES = 4;
 
 struct GeomLayout { size_t off[GEOM_COUNT + 1]; };
 struct ImageLayout { size_t off[IMG_COUNT + 1]; };
 struct BinLayout { size_t off[BIN_COUNT + 1]; };
 
+size_t radix_status_bytes(int n, int npass);
+
 inline GeomLayout geom_layout(int P)
 {
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p, 48 * p,
+                                4 * p, 4 * p, 4 * p, 24 * p + 1024, radix_status_bytes(P, DEPTH_PASSES),
                                 4 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 64), 4 * 64};
     GeomLayout l;
     size_t o = 0;
@@ -200,12 +207,10 @@ inline ImageLayout image_layout(int W, int H)
     return l;
 }
 
-size_t sort_scratch_bytes(int L);
-
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {8 * n, 8 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 48 * n, sort_scratch_bytes(L)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, MAX_TILE_PASSES)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -32,6 +32,7 @@ struct PreprocessArgs {
     uint32_t* tiles_touched;
     uint32_t* flags;
     float4* splat;  // 3 x float4 per Gaussian (GEOM_SPLAT)
+    uint32_t* dkey; // depth-sort key per Gaussian
 };
 
 struct RenderFwdArgs {
@@ -87,7 +88,8 @@ struct PreprocessBwdArgs {
     // per-instance gradient records and the gather map
     const float* grad_inst;         // f32x12[L] sorted order
     const uint32_t* inv;            // sorted position of emission slot e
-    const uint32_t* point_offsets;  // inclusive scan of tiles_touched (emission slots of Gaussian i)
+    const uint32_t* emit_start;     // first emission slot of Gaussian i
+    const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
     int has_invdepth;
     // reduced per-Gaussian render gradients (fully written; outputs of the reference glue)
     float* dL_dmean2D;   // (P,3)
@@ -104,15 +106,19 @@ struct PreprocessBwdArgs {
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
-hipError_t launch_inclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* scratch, hipStream_t s);
+// inclusive scan of in[gather[i]] (gather may be null)
+hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
+                                 hipStream_t s);
 
-hipError_t launch_duplicate_with_keys(int P, const float2* means2D, const float* depths, const uint32_t* offsets,
-                                      const int* radii, uint32_t gx, uint32_t gy, uint64_t* keys,
-                                      uint32_t* emit_gid, uint32_t* emit_e, hipStream_t s);
-hipError_t launch_sort_pairs(void* scratch, size_t scratch_bytes, const uint64_t* keys_in, uint64_t* keys_out,
-                             const uint32_t* vals_in, uint32_t* vals_out, int n, int end_bit, hipStream_t s);
-hipError_t launch_finalize(int L, const uint64_t* keys, const uint32_t* sorted_e, const uint32_t* emit_gid,
-                           uint32_t* point_list, uint32_t* inv, uint2* ranges, int T, hipStream_t s);
+hipError_t radix_sort(int n, int npass, const uint32_t* keys_in, const uint32_t* vals32_in, uint32_t* k0, uint2* v0,
+                      uint32_t* k1, uint2* v1, uint32_t* keys_final, uint2* vals_final, uint32_t* point_list,
+                      uint32_t* inv, uint32_t* sorted_keys, char* scratch, uint32_t* error, hipStream_t s);
+hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
+                                 const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
+                                 uint32_t* emit_start, hipStream_t s);
+hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
+hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
+                             uint64_t* keys, hipStream_t s);
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);

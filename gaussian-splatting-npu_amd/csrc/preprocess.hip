@@ -111,6 +111,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
 
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
+    a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
 
     const f3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
     // in_frustum (auxiliary.h:151-176)
@@ -172,6 +173,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
         rgb = {c[0], c[1], c[2]};
     }
     a.depths[idx] = p_view.z;
+    a.dkey[idx] = __float_as_uint(p_view.z);  // z > 0.2: float bits are monotone in z
     a.radii[idx] = (int)my_radius;
     reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
     const float opacity = a.opacities[idx] * h_convolution_scaling;
@@ -236,7 +238,13 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds
     return wprefix + inc - v;
 }
 
-__global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, int n, uint32_t* block_sums)
+__device__ __forceinline__ uint32_t scan_in(const uint32_t* in, const uint32_t* gather, size_t i)
+{
+    return gather ? in[gather[i]] : in[i];
+}
+
+__global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, const uint32_t* gather, int n,
+                                                          uint32_t* block_sums)
 {
     __shared__ uint32_t lds4[4];
     const size_t base = (size_t)blockIdx.x * SCAN_ITEMS;
@@ -244,7 +252,7 @@ __global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, in
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS / 256; k++) {
         size_t i = base + k * 256 + threadIdx.x;
-        if (i < (size_t)n) s += in[i];
+        if (i < (size_t)n) s += scan_in(in, gather, i);
     }
     uint32_t total;
     block_excl_scan256(s, lds4, total);
@@ -266,7 +274,8 @@ __global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sum
     }
 }
 
-__global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, int n, const uint32_t* block_offsets,
+__global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, const uint32_t* gather, int n,
+                                                         const uint32_t* block_offsets,
                                                          uint32_t* out)
 {
     __shared__ uint32_t lds4[4];
@@ -277,7 +286,7 @@ __global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, int
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         size_t i = base + k;
-        v[k] = i < (size_t)n ? in[i] : 0;
+        v[k] = i < (size_t)n ? scan_in(in, gather, i) : 0;
         s += v[k];
     }
     uint32_t total;
@@ -304,13 +313,14 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
     return hipGetLastError();
 }
 
-hipError_t launch_inclusive_scan(const uint32_t* in, uint32_t* out, int n, uint32_t* scratch, hipStream_t s)
+hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
+                                 hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(256), 0, s, in, n, scratch);
+    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch);
     hipLaunchKernelGGL(scan_blocksums_kernel, dim3(1), dim3(256), 0, s, scratch, nb);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, n, scratch, out);
+    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch, out);
     return hipGetLastError();
 }
 

@@ -44,8 +44,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
     {
-        const uint32_t e0 = idx == 0 ? 0u : a.point_offsets[idx - 1];
-        const uint32_t e1 = a.point_offsets[idx];
+        const uint32_t e0 = a.emit_start[idx];
+        const uint32_t e1 = e0 + a.tiles_touched[idx];
         for (uint32_t e = e0; e < e1; e++) {
             const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)a.inv[e] * GRAD_REC);
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];

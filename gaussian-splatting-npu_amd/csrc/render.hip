@@ -243,171 +243,179 @@ __device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64], int lan
 
 constexpr int GROUP = 6;  // Gaussians per transposed reduction (6 x 10 gradient terms <= 64 lanes)
 
-__global__ void __launch_bounds__(256, 2) render_bwd_kernel(RenderBwdArgs a)
+
+// Per-pixel state of the backward replay (backward.cu:498-528).
+struct BwdPix {
+    float T, T_final, dp0, dp1, dp2, dinv, bg_dot;
+    float acc0, acc1, acc2, acc_inv, last_alpha, last_c0, last_c1, last_c2, last_inv;
+    float pfx, pfy;
+    uint32_t last_contributor;
+    bool inside;
+};
+
+// One pixel x one Gaussian of backward.cu:552-636; adds the ten gradient terms into o[].
+__device__ __forceinline__ void bwd_pixel(BwdPix& s, uint32_t pos, const float4 xy, const float4 co, const float4 col,
+                                          bool has_inv, float ddelx_dx, float ddely_dy, float* o)
+{
+    const float dx = xy.x - s.pfx, dy = xy.y - s.pfy;
+    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+    const float G = __expf(power);
+    const float alpha = fminf(0.99f, co.w * G);
+    const bool contrib = s.inside && pos < s.last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+    if (contrib) {
+        const float one_m = 1.f - alpha;
+        // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
+        const float r_om = __builtin_amdgcn_rcpf(one_m);
+        s.T = s.T * r_om;
+        const float dchannel_dcolor = alpha * s.T;
+        float dL_dalpha = 0.0f;
+        s.acc0 = s.last_alpha * s.last_c0 + (1.f - s.last_alpha) * s.acc0;
+        s.acc1 = s.last_alpha * s.last_c1 + (1.f - s.last_alpha) * s.acc1;
+        s.acc2 = s.last_alpha * s.last_c2 + (1.f - s.last_alpha) * s.acc2;
+        s.last_c0 = col.x; s.last_c1 = col.y; s.last_c2 = col.z;
+        dL_dalpha += (col.x - s.acc0) * s.dp0;
+        dL_dalpha += (col.y - s.acc1) * s.dp1;
+        dL_dalpha += (col.z - s.acc2) * s.dp2;
+        o[GF_COLOR_R] += dchannel_dcolor * s.dp0;
+        o[GF_COLOR_G] += dchannel_dcolor * s.dp1;
+        o[GF_COLOR_B] += dchannel_dcolor * s.dp2;
+        if (has_inv) {
+            const float invd = col.w;
+            s.acc_inv = s.last_alpha * s.last_inv + (1.f - s.last_alpha) * s.acc_inv;
+            s.last_inv = invd;
+            dL_dalpha += (invd - s.acc_inv) * s.dinv;
+            o[GF_INVDEPTH] += dchannel_dcolor * s.dinv;
+        }
+        dL_dalpha *= s.T;
+        s.last_alpha = alpha;
+        dL_dalpha += (-s.T_final * r_om) * s.bg_dot;
+        const float dL_dG = co.w * dL_dalpha;
+        const float gdx = G * dx;
+        const float gdy = G * dy;
+        const float dG_ddelx = -gdx * co.x - gdy * co.y;
+        const float dG_ddely = -gdy * co.z - gdx * co.y;
+        o[GF_MEAN2D_X] += dL_dG * dG_ddelx * ddelx_dx;
+        o[GF_MEAN2D_Y] += dL_dG * dG_ddely * ddely_dy;
+        o[GF_CONIC_A] += -0.5f * gdx * dx * dL_dG;
+        o[GF_CONIC_B] += -0.5f * gdx * dy * dL_dG;
+        o[GF_CONIC_C] += -0.5f * gdy * dy * dL_dG;
+        o[GF_OPACITY] += G * dL_dalpha;
+    }
+}
+
+// Backward: ONE wave per 16x16 tile, each lane replaying 4 pixels (one per 8x8 quadrant),
+// so there are no workgroup barriers in the main loop and no cross-wave combine.  Per batch
+// of 64 list entries (back to front from the tile's largest n_contrib) each lane stages one
+// record in LDS and computes its quadrant mask (exact ellipse test + per-quadrant max
+// n_contrib); the wave compacts the surviving entries and, per group of 6, every lane
+// accumulates its (up to) 4 pixels' ten gradient terms, the transposed reduction sums the
+// 64 lanes, and lanes 0..59 store the 6 records (10 contiguous floats each).  Entries that
+// survive no quadrant get a zero record.  No atomics: per-(tile, Gaussian) sums are
+// bitwise reproducible.
+__global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 {
 #pragma clang fp contract(fast)
     const uint32_t tile = blockIdx.x;
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, wid = tid >> 6;
-    uint32_t px, py;
-    quad_pixel(tx, ty, tid, px, py);
-    const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-    const float pfx = (float)px, pfy = (float)py;
+    const int lane = threadIdx.x;
     const uint2 range = a.ranges[tile];
     const int todo = (int)(range.y - range.x);
-    const uint32_t pix_id = (uint32_t)a.W * py + px;
     const size_t HW = (size_t)a.H * a.W;
-
-    __shared__ float4 s_rec[BATCH * 3];
-    __shared__ uint8_t s_mask[BATCH];
-    __shared__ uint8_t s_list[4][BATCH];
-    __shared__ float s_part[4][BATCH * GF_NUM];
-    __shared__ uint32_t s_wmax[4];
-
-    const float T_final = inside ? a.final_Ts[pix_id] : 0.f;
-    float T = T_final;
-    const uint32_t last_contributor = inside ? a.n_contrib[pix_id] : 0;
-    float dpix0 = 0.f, dpix1 = 0.f, dpix2 = 0.f, dinv = 0.f;
-    if (inside) {
-        dpix0 = a.dL_dpixels[0 * HW + pix_id];
-        dpix1 = a.dL_dpixels[1 * HW + pix_id];
-        dpix2 = a.dL_dpixels[2 * HW + pix_id];
-        if (a.dL_invdepths) dinv = a.dL_invdepths[pix_id];
-    }
     const bool has_inv = a.dL_invdepths != nullptr;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc_inv = 0.f;
-    float last_alpha = 0.f, last_c0 = 0.f, last_c1 = 0.f, last_c2 = 0.f, last_inv = 0.f;
     const float ddelx_dx = 0.5 * a.W;
     const float ddely_dy = 0.5 * a.H;
-    const float bg_dot_dpixel = a.bg[0] * dpix0 + a.bg[1] * dpix1 + a.bg[2] * dpix2;
 
-    // Entries at or behind the largest n_contrib of a wave (tile) contribute nothing to it.
-    const uint32_t wmax = wave_max_u32(last_contributor);
-    if (lane == 0) s_wmax[wid] = wmax;
-    __syncthreads();
-    const uint32_t tmax = max(max(s_wmax[0], s_wmax[1]), max(s_wmax[2], s_wmax[3]));
-    const uint32_t wm0 = s_wmax[0], wm1 = s_wmax[1], wm2 = s_wmax[2], wm3 = s_wmax[3];
-    const int skip = todo - (int)tmax;
-    // zero records for the skipped tail (list positions tmax..todo-1)
+    BwdPix st[4];
+    uint32_t qmax[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        BwdPix& s = st[q];
+        const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * (q & 1);
+        const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * (q >> 1);
+        s.inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
+        s.pfx = (float)px;
+        s.pfy = (float)py;
+        const uint32_t pix_id = (uint32_t)a.W * py + px;
+        s.T_final = s.inside ? a.final_Ts[pix_id] : 0.f;
+        s.T = s.T_final;
+        s.last_contributor = s.inside ? a.n_contrib[pix_id] : 0u;
+        s.dp0 = s.inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
+        s.dp1 = s.inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
+        s.dp2 = s.inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
+        s.dinv = (s.inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
+        s.bg_dot = a.bg[0] * s.dp0 + a.bg[1] * s.dp1 + a.bg[2] * s.dp2;
+        s.acc0 = s.acc1 = s.acc2 = s.acc_inv = 0.f;
+        s.last_alpha = s.last_c0 = s.last_c1 = s.last_c2 = s.last_inv = 0.f;
+        qmax[q] = __builtin_amdgcn_readfirstlane(wave_max_u32(s.last_contributor));
+    }
+    const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
+
+    __shared__ float4 s_rec[3][64];
+    __shared__ uint8_t s_mask[64];
+    __shared__ uint8_t s_list[64];
+
+    // entries at list positions >= tmax contribute to no pixel: zero records
     {
         float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)(range.x + tmax) * GRAD_REC);
-        for (int k = tid; k < skip * (GRAD_REC / 4); k += 256) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = lane; k < (todo - (int)tmax) * (GRAD_REC / 4); k += 64) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
-    for (int base = skip; base < todo; base += BATCH) {
-        __syncthreads();
-        const int k = base + tid;
+    for (int p_hi = (int)tmax; p_hi > 0; p_hi -= 64) {
+        const int p_lo = max(0, p_hi - 64);
+        const int pos_l = p_hi - 1 - lane;  // this lane's entry; lane order = back-to-front
         uint32_t m = 0;
-        if (k < todo) {
-            const uint32_t id = a.point_list[range.y - k - 1];
+        if (pos_l >= p_lo) {
+            const uint32_t id = a.point_list[range.x + pos_l];
             const float4* r = a.splat + 3 * (size_t)id;
-            const float4 r0 = r[0];
-            s_rec[tid] = r0;
-            const float4 r1 = r[1];
-            s_rec[BATCH + tid] = r1;
-            s_rec[2 * BATCH + tid] = r[2];
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            s_rec[0][lane] = r0;
+            s_rec[1][lane] = r1;
+            s_rec[2][lane] = r2;
             m = quad_mask(r0, r1, tx, ty);
-            const uint32_t pos = (uint32_t)(todo - 1 - k);
-            m &= (uint32_t)(pos < wm0) | ((uint32_t)(pos < wm1) << 1) | ((uint32_t)(pos < wm2) << 2) |
-                 ((uint32_t)(pos < wm3) << 3);
+            m &= (uint32_t)((uint32_t)pos_l < qmax[0]) | ((uint32_t)((uint32_t)pos_l < qmax[1]) << 1) |
+                 ((uint32_t)((uint32_t)pos_l < qmax[2]) << 2) | ((uint32_t)((uint32_t)pos_l < qmax[3]) << 3);
+            if (m == 0) {
+                float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)(range.x + pos_l) * GRAD_REC);
+                z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+                z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                z[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
         }
-        s_mask[tid] = (uint8_t)m;
-        {
-            float4* zp = reinterpret_cast<float4*>(s_part[wid]);
-            for (int q = lane; q < BATCH * GF_NUM / 4; q += 64) zp[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-        __syncthreads();
-        const int n = min(BATCH, todo - base);
-        const int cnt = compact_batch(s_mask, n, wid, lane, s_list[wid]);
+        s_mask[lane] = (uint8_t)m;
+        const uint64_t b = __ballot(m != 0);
+        const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
+        if (m != 0) s_list[before] = (uint8_t)lane;
+        const int cnt = __popcll(b);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
         for (int g0 = 0; g0 < cnt; g0 += GROUP) {
             float v[64];
-            bool anyc = false;
+#pragma unroll
+            for (int q = 0; q < 64; q++) v[q] = 0.f;
 #pragma unroll
             for (int jj = 0; jj < GROUP; jj++) {
-                float* o = v + jj * GF_NUM;
+                if (g0 + jj < cnt) {
+                    const int j = __builtin_amdgcn_readfirstlane(s_list[g0 + jj]);
+                    const uint32_t mj = __builtin_amdgcn_readfirstlane(s_mask[j]);
+                    const uint32_t pos = (uint32_t)(p_hi - 1 - j);
+                    const float4 xy = s_rec[0][j], co = s_rec[1][j], col = s_rec[2][j];
+                    float* o = v + jj * GF_NUM;
 #pragma unroll
-                for (int q = 0; q < GF_NUM; q++) o[q] = 0.f;
-                if (g0 + jj < cnt) {  // wave-uniform
-                    const int j = s_list[wid][g0 + jj];
-                    const uint32_t pos = (uint32_t)(todo - 1 - (base + j));
-                    const float4 xy = s_rec[j];
-                    const float4 co = s_rec[BATCH + j];
-                    const float dx = xy.x - pfx, dy = xy.y - pfy;
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    const float G = __expf(power);
-                    const float alpha = fminf(0.99f, co.w * G);
-                    const bool contrib =
-                        inside && pos < last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                    if (contrib) {
-                        anyc = true;
-                        const float4 col = s_rec[2 * BATCH + j];
-                        const float one_m = 1.f - alpha;
-                        // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
-                        const float r_om = __builtin_amdgcn_rcpf(one_m);
-                        T = T * r_om;
-                        const float dchannel_dcolor = alpha * T;
-                        float dL_dalpha = 0.0f;
-                        acc0 = last_alpha * last_c0 + (1.f - last_alpha) * acc0;
-                        acc1 = last_alpha * last_c1 + (1.f - last_alpha) * acc1;
-                        acc2 = last_alpha * last_c2 + (1.f - last_alpha) * acc2;
-                        last_c0 = col.x; last_c1 = col.y; last_c2 = col.z;
-                        dL_dalpha += (col.x - acc0) * dpix0;
-                        dL_dalpha += (col.y - acc1) * dpix1;
-                        dL_dalpha += (col.z - acc2) * dpix2;
-                        o[GF_COLOR_R] = dchannel_dcolor * dpix0;
-                        o[GF_COLOR_G] = dchannel_dcolor * dpix1;
-                        o[GF_COLOR_B] = dchannel_dcolor * dpix2;
-                        if (has_inv) {
-                            const float invd = col.w;
-                            acc_inv = last_alpha * last_inv + (1.f - last_alpha) * acc_inv;
-                            last_inv = invd;
-                            dL_dalpha += (invd - acc_inv) * dinv;
-                            o[GF_INVDEPTH] = dchannel_dcolor * dinv;
-                        }
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        dL_dalpha += (-T_final * r_om) * bg_dot_dpixel;
-                        const float dL_dG = co.w * dL_dalpha;
-                        const float gdx = G * dx;
-                        const float gdy = G * dy;
-                        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                        const float dG_ddely = -gdy * co.z - gdx * co.y;
-                        o[GF_MEAN2D_X] = dL_dG * dG_ddelx * ddelx_dx;
-                        o[GF_MEAN2D_Y] = dL_dG * dG_ddely * ddely_dy;
-                        o[GF_CONIC_A] = -0.5f * gdx * dx * dL_dG;
-                        o[GF_CONIC_B] = -0.5f * gdx * dy * dL_dG;
-                        o[GF_CONIC_C] = -0.5f * gdy * dy * dL_dG;
-                        o[GF_OPACITY] = G * dL_dalpha;
-                    }
+                    for (int q = 0; q < 4; q++)
+                        if (mj & (1u << q)) bwd_pixel(st[q], pos, xy, co, col, has_inv, ddelx_dx, ddely_dy, o);
                 }
             }
-#pragma unroll
-            for (int q = GROUP * GF_NUM; q < 64; q++) v[q] = 0.f;
-            if (__any(anyc)) {
-                const float r = wave_transpose_reduce64(v, lane);
-                const int jj = lane / GF_NUM;
-                if (lane < GROUP * GF_NUM && g0 + jj < cnt)
-                    s_part[wid][s_list[wid][g0 + jj] * GF_NUM + (lane - jj * GF_NUM)] = r;
+            const float r = wave_transpose_reduce64(v, lane);
+            const int jj = lane / GF_NUM;
+            if (lane < GROUP * GF_NUM && g0 + jj < cnt) {
+                const int j = s_list[g0 + jj];
+                const size_t gpos = (size_t)range.x + (size_t)(p_hi - 1 - j);
+                a.grad_inst[gpos * GRAD_REC + (lane - jj * GF_NUM)] = r;
             }
         }
-        __syncthreads();
-        if (tid < n) {
-            float rec[GRAD_REC];
-#pragma unroll
-            for (int q = 0; q < GF_NUM; q++)
-                rec[q] = ((s_part[0][tid * GF_NUM + q] + s_part[1][tid * GF_NUM + q]) + s_part[2][tid * GF_NUM + q]) +
-                         s_part[3][tid * GF_NUM + q];
-            rec[10] = 0.f;
-            rec[11] = 0.f;
-            float4* dst = reinterpret_cast<float4*>(a.grad_inst + (size_t)(range.y - (base + tid) - 1) * GRAD_REC);
-            dst[0] = make_float4(rec[0], rec[1], rec[2], rec[3]);
-            dst[1] = make_float4(rec[4], rec[5], rec[6], rec[7]);
-            dst[2] = make_float4(rec[8], rec[9], rec[10], rec[11]);
-        }
+        __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
     }
 }
 
@@ -421,7 +429,7 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(T), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(T), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

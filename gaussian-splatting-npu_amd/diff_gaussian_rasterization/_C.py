@@ -187,7 +187,7 @@ def mark_visible(means3D, viewmatrix, projmatrix):
 
 
 # ---- parity/debug introspection (tests only) -------------------------------------------------
-def _layout(fn, *args, n=16):
+def _layout(fn, *args, n=64):
     offs = (_sz * n)()
     cnt = fn(*args, offs, n)
     return [offs[i] for i in range(cnt + 1)]

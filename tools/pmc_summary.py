@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc CSVs (tools/profile_pmc.sh) per kernel: mean counter value per
+dispatch.  Also derives per-launch memory-side traffic:
+    traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
+FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B read requests as 64 B).
+Writes <dir>/pmc_traffic.json (kernel -> bytes per launch) next to the printed summary."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_reduce_kernel": "scan", "scan_apply_kernel": "scan",
+         "scan_blocksums_kernel": "scan", "duplicate_with_keys_kernel": "duplicate_with_keys",
+         "finalize_kernel": "finalize_ranges", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
+         "preprocess_bwd_kernel": "preprocess_bwd", "depth_sort": "sort_pairs", "onesweep": "sort_pairs",
+         "radix": "sort_pairs", "emit_": "duplicate_with_keys", "tile_sort": "sort_pairs"}
+
+
+def short_name(k):
+    for key, v in SHORT.items():
+        if key in k:
+            return v
+    return None
+
+
+def main(d):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                k = row.get("Kernel_Name", "")
+                c = row.get("Counter_Name", "")
+                try:
+                    v = float(row.get("Counter_Value", "nan"))
+                except ValueError:
+                    continue
+                acc[k][c].append((row.get("Dispatch_Id", ""), v))
+    out = {}
+    for k, cs in acc.items():
+        if "gsr" not in k and "rocprim" not in k and "hipcub" not in k:
+            continue
+        ent = {}
+        for c, vals in cs.items():
+            per = collections.defaultdict(float)
+            for did, v in vals:
+                per[did] += v
+            ent[c] = sum(per.values()) / max(1, len(per))
+            ent["dispatches"] = len(per)
+        out[k[:120]] = ent
+    traffic = collections.defaultdict(float)
+    counts = collections.defaultdict(int)
+    for k, ent in out.items():
+        s = short_name(k)
+        if s and "FETCH_SIZE" in ent and "WRITE_SIZE" in ent:
+            traffic[s] += (2 * ent["FETCH_SIZE"] + ent["WRITE_SIZE"]) * 1024.0
+            counts[s] += 1
+    json.dump({k: round(v) for k, v in traffic.items()}, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
+    print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
+                     indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
