@@ -13,14 +13,13 @@ namespace gsr {
 
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a)
+// One Gaussian.  `sh` / `dsh` point at this Gaussian's SH coefficients and SH gradient,
+// either in global memory or in the workgroup's LDS staging slot (the same slot for both).
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const float* sh, float* dsh)
 {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
     const size_t i = (size_t)idx;
     float* dmean = a.dL_dmean3D + 3 * i;
     float* dcov = a.dL_dcov3D + 6 * i;
-    float* dsh = a.dL_dsh ? a.dL_dsh + i * a.M * 3 : nullptr;
 
     if (!(a.radii[idx] > 0)) {
         a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
@@ -181,7 +180,6 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     // ---------------- computeColorFromSH backward (backward.cu:23-142) ----------------
     if (a.shs) {
         const int deg = a.D;
-        const float* sh = a.shs + i * a.M * 3;
         const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
         const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
         const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
@@ -193,9 +191,15 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             dRGB[c] *= (cl >> c) & 1 ? 0 : 1;
         }
         float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
-        for (int k = 0; k < a.M * 3; k++) dsh[k] = 0.f;
-#define SETSH(k, coef)                                             \
-    _Pragma("unroll") for (int c = 0; c < 3; c++) dsh[(k) * 3 + c] = (coef) * dRGB[c]
+        // dRGB/dsh_k coefficients; dL_dsh is written after every read of sh (sh and dsh may
+        // share an LDS slot), coefficient k * dRGB exactly as backward.cu:51-100.
+        float coef[16];
+        int ncoef = 0;
+#define SETSH(k, cf)      \
+    do {                  \
+        coef[k] = (cf);   \
+        ncoef = (k) + 1;  \
+    } while (0)
         const float dRGBdsh0 = SH_C0;
         SETSH(0, dRGBdsh0);
         if (deg > 0) {
@@ -255,6 +259,17 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             }
         }
 #undef SETSH
+        {
+            const int kmax = a.M < 16 ? a.M : 16;
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (k < kmax) {
+#pragma unroll
+                    for (int c = 0; c < 3; c++) dsh[k * 3 + c] = k < ncoef ? coef[k] * dRGB[c] : 0.f;
+                }
+            }
+            for (int k = 48; k < a.M * 3; k++) dsh[k] = 0.f;
+        }
         const f3 dL_ddir = {ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2],
                             ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2],
                             ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2]};
@@ -314,10 +329,58 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     }
 }
 
+// SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's
+// traffic.  STAGED: the workgroup's 256 x 3M floats are read with coalesced 16-byte loads
+// into LDS (row stride padded to an odd number of 16-byte slots: conflict-free b128 rows),
+// each thread works on its row in place, and the SH gradients leave the same way -- instead
+// of every lane striding 192 B through global memory.
+template <bool STAGED>
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a, int lds_stride)
+{
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const int base = blockIdx.x * 256;
+    const int idx = base + (int)threadIdx.x;
+    if (!STAGED) {
+        if (idx < a.P) {
+            const size_t w3 = (size_t)a.M * 3;
+            preprocess_bwd_one(a, idx, a.shs ? a.shs + idx * w3 : nullptr, a.dL_dsh ? a.dL_dsh + idx * w3 : nullptr);
+        }
+        return;
+    }
+    const int W3 = a.M * 3;  // multiple of 4 on this path
+    const int n = min(256, a.P - base);
+    const int nv4 = n * (W3 / 4);
+    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
+    for (int f = threadIdx.x; f < nv4; f += 256) {
+        const int g = (f * 4) / W3, w = (f * 4) - g * W3;
+        *reinterpret_cast<float4*>(&s_sh[g * lds_stride + w]) = src[f];
+    }
+    __syncthreads();
+    if (idx < a.P) {
+        float* row = s_sh + threadIdx.x * lds_stride;
+        preprocess_bwd_one(a, idx, row, row);
+    }
+    __syncthreads();
+    float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * W3);
+    for (int f = threadIdx.x; f < nv4; f += 256) {
+        const int g = (f * 4) / W3, w = (f * 4) - g * W3;
+        dst[f] = *reinterpret_cast<const float4*>(&s_sh[g * lds_stride + w]);
+    }
+}
+
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
 {
     if (a.P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(preprocess_bwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    const int W3 = a.M * 3;
+    const bool staged = a.shs && a.dL_dsh && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
+                        ((uintptr_t)a.shs % 16) == 0 && ((uintptr_t)a.dL_dsh % 16) == 0;
+    if (staged) {
+        const int stride = ((W3 / 4) % 2) ? W3 : W3 + 4;  // odd number of 16-B slots per row
+        hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
+                           256 * stride * sizeof(float), s, a, stride);
+    } else {
+        hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, 0);
+    }
     return hipGetLastError();
 }
 
