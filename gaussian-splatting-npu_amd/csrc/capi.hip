@@ -449,6 +449,8 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     p.has_invdepth = dL_invdepths != nullptr;
+    p.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
+    p.W = width; p.H = height;
     p.dL_dmean2D = dL_dmean2D; p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
     p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;

@@ -62,7 +62,9 @@ struct RenderBwdArgs {
     float* grad_inst;           // f32x12[L]: one gradient record per sorted (tile, Gaussian) entry
 };
 
-// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).
+// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  The mean2D and conic
+// fields are pixel sums WITHOUT the per-Gaussian factors -opacity*W/2, -opacity*H/2 and
+// -opacity/2 (backward.cu:619-636); preprocess_bwd applies them once per Gaussian.
 enum GradField {
     GF_MEAN2D_X = 0, GF_MEAN2D_Y, GF_CONIC_A, GF_CONIC_B, GF_CONIC_C, GF_OPACITY, GF_COLOR_R, GF_COLOR_G,
     GF_COLOR_B, GF_INVDEPTH, GF_NUM
@@ -91,6 +93,8 @@ struct PreprocessBwdArgs {
     const uint32_t* emit_start;     // first emission slot of Gaussian i
     const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
     int has_invdepth;
+    const float4* conic_opacity;    // GEOM_CONIC_OPACITY (the rendered, AA-scaled opacity in .w)
+    int W, H;
     // reduced per-Gaussian render gradients (fully written; outputs of the reference glue)
     float* dL_dmean2D;   // (P,3)
     float* dL_dconic;    // (P,4)

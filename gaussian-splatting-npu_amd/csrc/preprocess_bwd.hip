@@ -53,6 +53,15 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
             g[8] += r2.x; g[9] += r2.y;
         }
     }
+    {
+        // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
+        const float op = a.conic_opacity[idx].w;
+        g[GF_MEAN2D_X] *= -op * (0.5f * a.W);
+        g[GF_MEAN2D_Y] *= -op * (0.5f * a.H);
+        g[GF_CONIC_A] *= -0.5f * op;
+        g[GF_CONIC_B] *= -0.5f * op;
+        g[GF_CONIC_C] *= -0.5f * op;
+    }
     // render-pass gradients of the reference glue (rasterize_points.cu:164-172), fully written
     a.dL_dmean2D[3 * i] = g[GF_MEAN2D_X]; a.dL_dmean2D[3 * i + 1] = g[GF_MEAN2D_Y]; a.dL_dmean2D[3 * i + 2] = 0.f;
     a.dL_dconic[4 * i] = g[GF_CONIC_A]; a.dL_dconic[4 * i + 1] = g[GF_CONIC_B]; a.dL_dconic[4 * i + 2] = 0.f;

@@ -241,65 +241,60 @@ __device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64], int lan
     return keep + dpp<DPP_QUAD_1032>(send);
 }
 
-constexpr int GROUP = 6;  // Gaussians per transposed reduction (6 x 10 gradient terms <= 64 lanes)
 
 
-// Per-pixel state of the backward replay (backward.cu:498-528).
+// Per-pixel state of the backward replay (backward.cu:498-528).  Pixels outside the image
+// carry last_contributor = 0, so no list entry contributes to them.  acc* is the reference's
+// accum_rec already folded with the previous contributor (backward.cu:577-583 evaluated
+// eagerly, same operands and order), so last_color / last_alpha need no registers.
 struct BwdPix {
-    float T, T_final, dp0, dp1, dp2, dinv, bg_dot;
-    float acc0, acc1, acc2, acc_inv, last_alpha, last_c0, last_c1, last_c2, last_inv;
-    float pfx, pfy;
+    float T, tb, dp0, dp1, dp2, dinv;  // tb = -T_final * (bg . dL/dpixel), backward.cu:612-615
+    float acc0, acc1, acc2, acc_inv;
     uint32_t last_contributor;
-    bool inside;
 };
 
-// One pixel x one Gaussian of backward.cu:552-636; adds the ten gradient terms into o[].
-__device__ __forceinline__ void bwd_pixel(BwdPix& s, uint32_t pos, const float4 xy, const float4 co, const float4 col,
-                                          bool has_inv, float ddelx_dx, float ddely_dy, float* o)
+// One pixel x one Gaussian of backward.cu:552-636; adds the ten per-record sums into o[].
+// Per-Gaussian constant factors are left to preprocess_bwd (see GradField): with
+// u = G * dL/dalpha the record holds sum u (opacity), sum u*(dx*a + dy*b) and
+// sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and sum u*dx*dx,
+// u*dx*dy, u*dy*dy (conic, times -opacity/2).
+__device__ __forceinline__ void bwd_pixel(BwdPix& s, float pfx, float pfy, uint32_t pos, const float4 xy,
+                                          const float4 co, const float4 col, bool has_inv, float* o)
 {
-    const float dx = xy.x - s.pfx, dy = xy.y - s.pfy;
+    const float dx = xy.x - pfx, dy = xy.y - pfy;
     const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
     const float G = __expf(power);
     const float alpha = fminf(0.99f, co.w * G);
-    const bool contrib = s.inside && pos < s.last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+    const bool contrib = pos < s.last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
     if (contrib) {
         const float one_m = 1.f - alpha;
         // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
         const float r_om = __builtin_amdgcn_rcpf(one_m);
         s.T = s.T * r_om;
         const float dchannel_dcolor = alpha * s.T;
-        float dL_dalpha = 0.0f;
-        s.acc0 = s.last_alpha * s.last_c0 + (1.f - s.last_alpha) * s.acc0;
-        s.acc1 = s.last_alpha * s.last_c1 + (1.f - s.last_alpha) * s.acc1;
-        s.acc2 = s.last_alpha * s.last_c2 + (1.f - s.last_alpha) * s.acc2;
-        s.last_c0 = col.x; s.last_c1 = col.y; s.last_c2 = col.z;
-        dL_dalpha += (col.x - s.acc0) * s.dp0;
+        float dL_dalpha = (col.x - s.acc0) * s.dp0;
         dL_dalpha += (col.y - s.acc1) * s.dp1;
         dL_dalpha += (col.z - s.acc2) * s.dp2;
+        s.acc0 = alpha * col.x + one_m * s.acc0;
+        s.acc1 = alpha * col.y + one_m * s.acc1;
+        s.acc2 = alpha * col.z + one_m * s.acc2;
         o[GF_COLOR_R] += dchannel_dcolor * s.dp0;
         o[GF_COLOR_G] += dchannel_dcolor * s.dp1;
         o[GF_COLOR_B] += dchannel_dcolor * s.dp2;
         if (has_inv) {
-            const float invd = col.w;
-            s.acc_inv = s.last_alpha * s.last_inv + (1.f - s.last_alpha) * s.acc_inv;
-            s.last_inv = invd;
-            dL_dalpha += (invd - s.acc_inv) * s.dinv;
+            dL_dalpha += (col.w - s.acc_inv) * s.dinv;
+            s.acc_inv = alpha * col.w + one_m * s.acc_inv;
             o[GF_INVDEPTH] += dchannel_dcolor * s.dinv;
         }
-        dL_dalpha *= s.T;
-        s.last_alpha = alpha;
-        dL_dalpha += (-s.T_final * r_om) * s.bg_dot;
-        const float dL_dG = co.w * dL_dalpha;
-        const float gdx = G * dx;
-        const float gdy = G * dy;
-        const float dG_ddelx = -gdx * co.x - gdy * co.y;
-        const float dG_ddely = -gdy * co.z - gdx * co.y;
-        o[GF_MEAN2D_X] += dL_dG * dG_ddelx * ddelx_dx;
-        o[GF_MEAN2D_Y] += dL_dG * dG_ddely * ddely_dy;
-        o[GF_CONIC_A] += -0.5f * gdx * dx * dL_dG;
-        o[GF_CONIC_B] += -0.5f * gdx * dy * dL_dG;
-        o[GF_CONIC_C] += -0.5f * gdy * dy * dL_dG;
-        o[GF_OPACITY] += G * dL_dalpha;
+        dL_dalpha = dL_dalpha * s.T + s.tb * r_om;
+        const float u = G * dL_dalpha;
+        const float ux = u * dx, uy = u * dy;
+        o[GF_OPACITY] += u;
+        o[GF_MEAN2D_X] += ux * co.x + uy * co.y;
+        o[GF_MEAN2D_Y] += uy * co.z + ux * co.y;
+        o[GF_CONIC_A] += ux * dx;
+        o[GF_CONIC_B] += ux * dy;
+        o[GF_CONIC_C] += uy * dy;
     }
 }
 
@@ -315,6 +310,7 @@ __device__ __forceinline__ void bwd_pixel(BwdPix& s, uint32_t pos, const float4 
 __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 {
 #pragma clang fp contract(fast)
+    constexpr int G = 6;  // Gaussians per transposed reduction (6 x 10 gradient terms <= 64 lanes)
     const uint32_t tile = blockIdx.x;
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int lane = threadIdx.x;
@@ -322,8 +318,8 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     const int todo = (int)(range.y - range.x);
     const size_t HW = (size_t)a.H * a.W;
     const bool has_inv = a.dL_invdepths != nullptr;
-    const float ddelx_dx = 0.5 * a.W;
-    const float ddely_dy = 0.5 * a.H;
+    const float pfx0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
+    const float pfy0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
 
     BwdPix st[4];
     uint32_t qmax[4];
@@ -332,20 +328,17 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
         BwdPix& s = st[q];
         const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * (q & 1);
         const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * (q >> 1);
-        s.inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-        s.pfx = (float)px;
-        s.pfy = (float)py;
+        const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
         const uint32_t pix_id = (uint32_t)a.W * py + px;
-        s.T_final = s.inside ? a.final_Ts[pix_id] : 0.f;
-        s.T = s.T_final;
-        s.last_contributor = s.inside ? a.n_contrib[pix_id] : 0u;
-        s.dp0 = s.inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
-        s.dp1 = s.inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
-        s.dp2 = s.inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
-        s.dinv = (s.inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
-        s.bg_dot = a.bg[0] * s.dp0 + a.bg[1] * s.dp1 + a.bg[2] * s.dp2;
+        const float T_final = inside ? a.final_Ts[pix_id] : 0.f;
+        s.T = T_final;
+        s.last_contributor = inside ? a.n_contrib[pix_id] : 0u;
+        s.dp0 = inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
+        s.dp1 = inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
+        s.dp2 = inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
+        s.dinv = (inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
+        s.tb = -T_final * (a.bg[0] * s.dp0 + a.bg[1] * s.dp1 + a.bg[2] * s.dp2);
         s.acc0 = s.acc1 = s.acc2 = s.acc_inv = 0.f;
-        s.last_alpha = s.last_c0 = s.last_c1 = s.last_c2 = s.last_inv = 0.f;
         qmax[q] = __builtin_amdgcn_readfirstlane(wave_max_u32(s.last_contributor));
     }
     const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
@@ -390,12 +383,12 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        for (int g0 = 0; g0 < cnt; g0 += GROUP) {
+        for (int g0 = 0; g0 < cnt; g0 += G) {
             float v[64];
 #pragma unroll
             for (int q = 0; q < 64; q++) v[q] = 0.f;
 #pragma unroll
-            for (int jj = 0; jj < GROUP; jj++) {
+            for (int jj = 0; jj < G; jj++) {
                 if (g0 + jj < cnt) {
                     const int j = __builtin_amdgcn_readfirstlane(s_list[g0 + jj]);
                     const uint32_t mj = __builtin_amdgcn_readfirstlane(s_mask[j]);
@@ -404,12 +397,13 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                     float* o = v + jj * GF_NUM;
 #pragma unroll
                     for (int q = 0; q < 4; q++)
-                        if (mj & (1u << q)) bwd_pixel(st[q], pos, xy, co, col, has_inv, ddelx_dx, ddely_dy, o);
+                        if (mj & (1u << q))
+                            bwd_pixel(st[q], pfx0 + 8.f * (q & 1), pfy0 + 8.f * (q >> 1), pos, xy, co, col, has_inv, o);
                 }
             }
             const float r = wave_transpose_reduce64(v, lane);
             const int jj = lane / GF_NUM;
-            if (lane < GROUP * GF_NUM && g0 + jj < cnt) {
+            if (lane < G * GF_NUM && g0 + jj < cnt) {
                 const int j = s_list[g0 + jj];
                 const size_t gpos = (size_t)range.x + (size_t)(p_hi - 1 - j);
                 a.grad_inst[gpos * GRAD_REC + (lane - jj * GF_NUM)] = r;
