@@ -75,6 +75,7 @@ def main():
     torch.cuda.set_device(dev)
 
     import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import multiview
     lib = dgr._C.lib
     lib.gsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     lib.gsr_profile_kernel_name.restype = ctypes.c_char_p
@@ -83,7 +84,7 @@ def main():
     scene = synthetic.make_scene(P, seed=0)
     params = {k: v.to(dev).requires_grad_(True) for k, v in scene.items()}
     M = params["shs"].shape[1]
-    views = [(rank + i * world) % 8 for i in range(args.views_per_rank)]
+    views = multiview.views_for_rank(rank, world, args.views_per_rank)
     cams, grads = [], []
     for v in views:
         cam = synthetic.Camera(W, H, view=v)
@@ -95,7 +96,6 @@ def main():
         cams.append(s)
         gc, gi = synthetic.make_grads(H, W, seed=1 + v)
         grads.append((gc.to(dev), gi.to(dev)))
-    order = ["means3D", "shs", "opacities", "scales", "rotations"]
 
     def step():
         for p in params.values():
@@ -107,14 +107,7 @@ def main():
                                      opacities=params["opacities"], scales=params["scales"],
                                      rotations=params["rotations"])
             torch.autograd.backward([color, inv], [gc, gi])
-        if world > 1:
-            flat = torch.cat([params[k].grad.reshape(-1) for k in order])
-            dist.all_reduce(flat)
-            off = 0
-            for k in order:
-                n = params[k].numel()
-                params[k].grad.copy_(flat[off:off + n].view_as(params[k]))
-                off += n
+        multiview.allreduce_grads(params)
 
     for _ in range(args.warmup):
         step()
@@ -133,10 +126,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = multiview.max_over_ranks(t1 - t0, dev)
 
     # per-kernel HIP-event timings over the timed region
     kern = {}

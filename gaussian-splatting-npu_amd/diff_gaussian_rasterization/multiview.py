@@ -1,0 +1,53 @@
+"""Multi-view data parallelism over the rasterizer.
+
+One process per GPU; the Gaussian parameters are replicated, camera views are dealt out
+round-robin (view v goes to rank v mod world), every rank runs forward+backward of its own
+views and accumulates the parameter gradients locally, and ONE all_reduce(SUM) of a flat
+fp32 bucket holding every parameter gradient (236 B per Gaussian at SH degree 3) makes the
+replicas agree.  The reference trains on one view per step on one GPU (train.py:97-111);
+this is the multi-view form of that step, the only exchange the path has.
+
+Backend-agnostic: "nccl" (RCCL over xGMI) on the GPU box, "gloo" in the CPU tests.
+"""
+import torch
+import torch.distributed as dist
+
+# parameter order of the bucket (xyz, features, opacity, scaling, rotation)
+PARAM_ORDER = ("means3D", "shs", "opacities", "scales", "rotations")
+
+
+def views_for_rank(rank, world, views_per_rank=1, n_views=8):
+    """Views this rank renders: rank, rank + world, ... (mod n_views)."""
+    if not (0 <= rank < world):
+        raise ValueError(f"rank {rank} outside world {world}")
+    return [(rank + i * world) % n_views for i in range(views_per_rank)]
+
+
+def grad_bucket(params, order=PARAM_ORDER):
+    """Flat fp32 view of every parameter gradient (a fresh contiguous buffer)."""
+    return torch.cat([params[k].grad.reshape(-1) for k in order])
+
+
+def allreduce_grads(params, order=PARAM_ORDER, group=None):
+    """SUM every parameter gradient across ranks with one collective on a flat bucket, and
+    write the result back into .grad.  Returns the number of bytes reduced per rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return 0
+    flat = grad_bucket(params, order)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    off = 0
+    for k in order:
+        g = params[k].grad
+        n = g.numel()
+        g.copy_(flat[off:off + n].view_as(g))
+        off += n
+    return flat.numel() * flat.element_size()
+
+
+def max_over_ranks(seconds, device=None, group=None):
+    """The slowest rank's wall time (the bench's timed region)."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return float(seconds)
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return float(t.item())

@@ -1,0 +1,108 @@
+"""Multi-view data-parallel step logic on CPU with gloo, world_size 2.
+
+The GPU bench runs the same functions over RCCL; here each rank fabricates the gradients a
+forward+backward of its views would leave in .grad and checks that the single bucketed
+all_reduce(SUM) produces the sum over all views on every rank, and that the view deal-out
+covers each of the 8 ring views exactly once at every supported GPU count.
+"""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gaussian-splatting-npu_amd"))
+
+from diff_gaussian_rasterization import multiview  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fake_params(P, M, view):
+    """Parameters plus the per-view gradient a fwd+bwd of `view` would accumulate."""
+    g = torch.Generator().manual_seed(100 + view)
+    shapes = {"means3D": (P, 3), "shs": (P, M, 3), "opacities": (P, 1), "scales": (P, 3), "rotations": (P, 4)}
+    out = {}
+    for k, shp in shapes.items():
+        t = torch.zeros(shp, requires_grad=True)
+        t.grad = torch.randn(shp, generator=g)
+        out[k] = t
+    return out
+
+
+def _worker(rank, world, port, P, M, views_per_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        views = multiview.views_for_rank(rank, world, views_per_rank)
+        params = None
+        for v in views:  # local accumulation over this rank's views
+            p = _fake_params(P, M, v)
+            if params is None:
+                params = p
+            else:
+                for k in params:
+                    params[k].grad += p[k].grad
+        nbytes = multiview.allreduce_grads(params)
+        t = multiview.max_over_ranks(0.5 + rank)
+        q.put((rank, views, {k: v.grad.numpy().copy() for k, v in params.items()}, nbytes, t))  # by value
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("views_per_rank", [1, 4])
+def test_allreduce_sums_all_views_world2(views_per_rank):
+    world, P, M = 2, 257, 16
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, M, views_per_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort(key=lambda r: r[0])
+    all_views = sorted(v for r in res for v in r[1])
+    assert all_views == sorted(set(all_views)) and len(all_views) == world * views_per_rank
+    expect = None
+    for v in all_views:
+        p = _fake_params(P, M, v)
+        expect = {k: t.grad.clone() for k, t in p.items()} if expect is None else \
+            {k: expect[k] + p[k].grad for k in expect}
+    for rank, _, grads, nbytes, t in res:
+        assert nbytes == 4 * P * (3 + 3 * M + 1 + 3 + 4)  # 236 B/Gaussian at M=16
+        assert t == 0.5 + (world - 1)  # max over ranks
+        for k in expect:
+            torch.testing.assert_close(torch.from_numpy(grads[k]), expect[k], rtol=1e-6, atol=1e-6)
+    # both replicas hold bit-identical gradients after the reduction
+    for k in expect:
+        assert (res[0][2][k] == res[1][2][k]).all()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_views_cover_the_ring(world):
+    views = [v for r in range(world) for v in multiview.views_for_rank(r, world, 8 // world)]
+    assert sorted(views) == list(range(8))
+
+
+def test_single_process_is_a_noop():
+    params = _fake_params(4, 16, 0)
+    before = {k: v.grad.clone() for k, v in params.items()}
+    assert multiview.allreduce_grads(params) == 0
+    for k in params:
+        assert torch.equal(params[k].grad, before[k])
+    with pytest.raises(ValueError):
+        multiview.views_for_rank(2, 2)
