@@ -20,12 +20,13 @@
 // stops fetching once all four are (the reference's __syncthreads_count,
 // forward.cu:329-331).
 //
-// Backward: traversal is back-to-front from each pixel's n_contrib; entries behind a
-// wave's largest n_contrib are culled for that wave, batches behind the tile's largest
-// are not loaded.  The ten per-(pixel, Gaussian) gradient terms are reduced over the
-// tile's 256 pixels on chip (transposed cross-lane reduction, then LDS in a fixed order)
-// and stored once per (tile, Gaussian) entry -- no global atomics, bitwise-reproducible
-// sums (the reference issues up to ten float atomics per contributing pixel,
+// Backward: one wave64 per tile, 4 pixels per lane (one per quadrant); traversal is
+// back-to-front from each pixel's n_contrib; entries behind a quadrant's largest
+// n_contrib are culled for that quadrant, batches behind the tile's largest are not
+// loaded.  The ten per-(pixel, Gaussian) gradient terms are reduced over the tile's 256
+// pixels on chip (in-lane over the 4 pixels, then a transposed cross-lane reduction) and
+// stored once per (tile, Gaussian) entry -- no global atomics, bitwise-reproducible sums
+// (the reference issues up to ten float atomics per contributing pixel,
 // backward.cu:593-635).
 #include "gsr_common.h"
 #include "gsr_kernels.h"
@@ -101,6 +102,38 @@ __device__ __forceinline__ int compact_batch(const uint8_t* s_mask, int n, int w
     return cnt;
 }
 
+// ---- packed-f32 pixel pairs -----------------------------------------------------------------
+// gfx950 issues v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 at the cost of one scalar f32 op, so
+// the backward evaluates its pixels two at a time: each lane owns two horizontally paired
+// pixels (x, x + 8) of the upper and of the lower half of the tile.
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+
+// Gaussian falloff exponent in the log2 domain, shared by forward and backward so that both
+// make identical alpha decisions: with (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic,
+// p2 = (ka dx + kb dy) dx + kc dy^2 = log2(e) * power (forward.cu:353-354), G = 2^p2.
+struct Falloff {
+    float ka, kb, kc;
+};
+constexpr float LOG2E = 1.4426950408889634f;
+__device__ __forceinline__ Falloff falloff(const float4 co)
+{
+    return {-0.5f * LOG2E * co.x, -LOG2E * co.y, -0.5f * LOG2E * co.z};
+}
+__device__ __forceinline__ float falloff_p2(const Falloff f, float dx, float dy)
+{
+    const float bq = f.kb * dy;
+    const float cq = (f.kc * dy) * dy;
+    return __builtin_fmaf(__builtin_fmaf(f.ka, dx, bq), dx, cq);
+}
+__device__ __forceinline__ v2f falloff_p2(const Falloff f, v2f dx, float dy)
+{
+    const float bq = f.kb * dy;
+    const float cq = (f.kc * dy) * dy;
+    return fma2(fma2((v2f)(f.ka), dx, (v2f)(bq)), dx, (v2f)(cq));
+}
+
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 {
 #pragma clang fp contract(fast)
@@ -150,10 +183,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
             const int j = s_list[wid][c];
             const float4 xy = s_rec[j];
             const float4 co = s_rec[BATCH + j];
-            const float dx = xy.x - pfx, dy = xy.y - pfy;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            const float alpha = fminf(0.99f, co.w * __expf(power));
-            bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
+            const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
+            bool contrib = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
             const float test_T = T * (1 - alpha);
             if (contrib && test_T < 0.0001f) {
                 done = true;
@@ -243,70 +275,76 @@ __device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64], int lan
 
 
 
-// Per-pixel state of the backward replay (backward.cu:498-528).  Pixels outside the image
+// State of two pixels of the backward replay (backward.cu:498-528).  Pixels outside the image
 // carry last_contributor = 0, so no list entry contributes to them.  acc* is the reference's
 // accum_rec already folded with the previous contributor (backward.cu:577-583 evaluated
-// eagerly, same operands and order), so last_color / last_alpha need no registers.
-struct BwdPix {
-    float T, tb, dp0, dp1, dp2, dinv;  // tb = -T_final * (bg . dL/dpixel), backward.cu:612-615
-    float acc0, acc1, acc2, acc_inv;
-    uint32_t last_contributor;
+// eagerly), so last_color / last_alpha need no registers.
+struct BwdPair {
+    v2f T, tb, dp0, dp1, dp2, dinv;  // tb = -T_final * (bg . dL/dpixel), backward.cu:612-615
+    v2f acc0, acc1, acc2, acc_inv;
+    uint32_t lc0, lc1;               // last_contributor
 };
 
-// One pixel x one Gaussian of backward.cu:552-636; adds the ten per-record sums into o[].
-// Per-Gaussian constant factors are left to preprocess_bwd (see GradField): with
-// u = G * dL/dalpha the record holds sum u (opacity), sum u*(dx*a + dy*b) and
-// sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and sum u*dx*dx,
-// u*dx*dy, u*dy*dy (conic, times -opacity/2).
-__device__ __forceinline__ void bwd_pixel(BwdPix& s, float pfx, float pfy, uint32_t pos, const float4 xy,
-                                          const float4 co, const float4 col, bool has_inv, float* o)
+// Two pixels x one Gaussian of backward.cu:552-636, branch-free: a pixel the Gaussian does not
+// contribute to gets alpha = G = 0, which leaves its state bitwise unchanged (T * rcp(1) = T,
+// acc + 0 * d = acc) and adds exact zeros.  Per-Gaussian constant factors are left to
+// preprocess_bwd (see GradField): with u = G * dL/dalpha the record holds sum u (opacity),
+// sum u*(dx*a + dy*b) and sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and
+// sum u*dx*dx, u*dx*dy, u*dy*dy (conic, times -opacity/2).
+template <bool HAS_INV>
+__device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_t pos, const float4 xy,
+                                         const Falloff f, const float4 co, const float4 col, v2f* o)
 {
-    const float dx = xy.x - pfx, dy = xy.y - pfy;
-    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-    const float G = __expf(power);
-    const float alpha = fminf(0.99f, co.w * G);
-    const bool contrib = pos < s.last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-    if (contrib) {
-        const float one_m = 1.f - alpha;
-        // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
-        const float r_om = __builtin_amdgcn_rcpf(one_m);
-        s.T = s.T * r_om;
-        const float dchannel_dcolor = alpha * s.T;
-        float dL_dalpha = (col.x - s.acc0) * s.dp0;
-        dL_dalpha += (col.y - s.acc1) * s.dp1;
-        dL_dalpha += (col.z - s.acc2) * s.dp2;
-        s.acc0 = alpha * col.x + one_m * s.acc0;
-        s.acc1 = alpha * col.y + one_m * s.acc1;
-        s.acc2 = alpha * col.z + one_m * s.acc2;
-        o[GF_COLOR_R] += dchannel_dcolor * s.dp0;
-        o[GF_COLOR_G] += dchannel_dcolor * s.dp1;
-        o[GF_COLOR_B] += dchannel_dcolor * s.dp2;
-        if (has_inv) {
-            dL_dalpha += (col.w - s.acc_inv) * s.dinv;
-            s.acc_inv = alpha * col.w + one_m * s.acc_inv;
-            o[GF_INVDEPTH] += dchannel_dcolor * s.dinv;
-        }
-        dL_dalpha = dL_dalpha * s.T + s.tb * r_om;
-        const float u = G * dL_dalpha;
-        const float ux = u * dx, uy = u * dy;
-        o[GF_OPACITY] += u;
-        o[GF_MEAN2D_X] += ux * co.x + uy * co.y;
-        o[GF_MEAN2D_Y] += uy * co.z + ux * co.y;
-        o[GF_CONIC_A] += ux * dx;
-        o[GF_CONIC_B] += ux * dy;
-        o[GF_CONIC_C] += uy * dy;
+    const v2f dx = (v2f)(xy.x) - pfx;
+    const float dy = xy.y - pfy;
+    const v2f p2 = falloff_p2(f, dx, dy);
+    const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
+    const v2f al = G * co.w;
+    const float alx = fminf(0.99f, al.x), aly = fminf(0.99f, al.y);
+    const bool c0 = pos < s.lc0 && !(p2.x > 0.0f) && !(alx < 1.0f / 255.0f);
+    const bool c1 = pos < s.lc1 && !(p2.y > 0.0f) && !(aly < 1.0f / 255.0f);
+    const v2f alpha = {c0 ? alx : 0.f, c1 ? aly : 0.f};
+    const v2f Gc = {c0 ? G.x : 0.f, c1 ? G.y : 0.f};
+    const v2f one_m = 1.f - alpha;
+    // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
+    const v2f r_om = {__builtin_amdgcn_rcpf(one_m.x), __builtin_amdgcn_rcpf(one_m.y)};
+    s.T = s.T * r_om;
+    const v2f dch = alpha * s.T;
+    const v2f d0 = (v2f)(col.x) - s.acc0, d1 = (v2f)(col.y) - s.acc1, d2 = (v2f)(col.z) - s.acc2;
+    v2f dL = fma2(d2, s.dp2, fma2(d1, s.dp1, d0 * s.dp0));
+    s.acc0 = fma2(alpha, d0, s.acc0);
+    s.acc1 = fma2(alpha, d1, s.acc1);
+    s.acc2 = fma2(alpha, d2, s.acc2);
+    o[GF_COLOR_R] = fma2(dch, s.dp0, o[GF_COLOR_R]);
+    o[GF_COLOR_G] = fma2(dch, s.dp1, o[GF_COLOR_G]);
+    o[GF_COLOR_B] = fma2(dch, s.dp2, o[GF_COLOR_B]);
+    if constexpr (HAS_INV) {
+        const v2f di = (v2f)(col.w) - s.acc_inv;
+        dL = fma2(di, s.dinv, dL);
+        s.acc_inv = fma2(alpha, di, s.acc_inv);
+        o[GF_INVDEPTH] = fma2(dch, s.dinv, o[GF_INVDEPTH]);
     }
+    dL = fma2(dL, s.T, s.tb * r_om);
+    const v2f u = Gc * dL;
+    const v2f ux = u * dx, uy = u * dy;
+    o[GF_OPACITY] += u;
+    o[GF_MEAN2D_X] = fma2(ux, (v2f)(co.x), fma2(uy, (v2f)(co.y), o[GF_MEAN2D_X]));
+    o[GF_MEAN2D_Y] = fma2(uy, (v2f)(co.z), fma2(ux, (v2f)(co.y), o[GF_MEAN2D_Y]));
+    o[GF_CONIC_A] = fma2(ux, dx, o[GF_CONIC_A]);
+    o[GF_CONIC_B] = fma2(ux, (v2f)(dy), o[GF_CONIC_B]);
+    o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
 }
 
-// Backward: ONE wave per 16x16 tile, each lane replaying 4 pixels (one per 8x8 quadrant),
-// so there are no workgroup barriers in the main loop and no cross-wave combine.  Per batch
-// of 64 list entries (back to front from the tile's largest n_contrib) each lane stages one
-// record in LDS and computes its quadrant mask (exact ellipse test + per-quadrant max
-// n_contrib); the wave compacts the surviving entries and, per group of 6, every lane
-// accumulates its (up to) 4 pixels' ten gradient terms, the transposed reduction sums the
-// 64 lanes, and lanes 0..59 store the 6 records (10 contiguous floats each).  Entries that
-// survive no quadrant get a zero record.  No atomics: per-(tile, Gaussian) sums are
-// bitwise reproducible.
+// Backward: ONE wave per 16x16 tile, each lane replaying 4 pixels as two packed pairs (upper
+// half: quadrants 0|1, lower half: 2|3), so there are no workgroup barriers in the main loop
+// and no cross-wave combine.  Per batch of 64 list entries (back to front from the tile's
+// largest n_contrib) each lane stages one record in LDS and computes its quadrant mask (exact
+// ellipse test + per-quadrant max n_contrib); the wave compacts the surviving entries and,
+// per group of 6, every lane accumulates its pixels' ten gradient terms, the transposed
+// reduction sums the 64 lanes, and lanes 0..59 store the 6 records (10 contiguous floats
+// each).  Entries that survive no quadrant get a zero record.  No atomics: per-(tile,
+// Gaussian) sums are bitwise reproducible.
+template <bool HAS_INV>
 __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 {
 #pragma clang fp contract(fast)
@@ -317,29 +355,42 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     const uint2 range = a.ranges[tile];
     const int todo = (int)(range.y - range.x);
     const size_t HW = (size_t)a.H * a.W;
-    const bool has_inv = a.dL_invdepths != nullptr;
-    const float pfx0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
-    const float pfy0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
+    const bool has_inv = HAS_INV;
+    const float px0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
+    const float py0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
+    const v2f pfx = {px0, px0 + 8.f};
 
-    BwdPix st[4];
+    BwdPair st[2];
     uint32_t qmax[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        BwdPix& s = st[q];
-        const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * (q & 1);
-        const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * (q >> 1);
-        const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-        const uint32_t pix_id = (uint32_t)a.W * py + px;
-        const float T_final = inside ? a.final_Ts[pix_id] : 0.f;
-        s.T = T_final;
-        s.last_contributor = inside ? a.n_contrib[pix_id] : 0u;
-        s.dp0 = inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
-        s.dp1 = inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
-        s.dp2 = inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
-        s.dinv = (inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
-        s.tb = -T_final * (a.bg[0] * s.dp0 + a.bg[1] * s.dp1 + a.bg[2] * s.dp2);
-        s.acc0 = s.acc1 = s.acc2 = s.acc_inv = 0.f;
-        qmax[q] = __builtin_amdgcn_readfirstlane(wave_max_u32(s.last_contributor));
+    for (int h = 0; h < 2; h++) {
+        float Tf[2], dp0[2], dp1[2], dp2[2], dinv[2], tb[2];
+        uint32_t lc[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * e;
+            const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * h;
+            const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
+            const uint32_t pix_id = (uint32_t)a.W * py + px;
+            Tf[e] = inside ? a.final_Ts[pix_id] : 0.f;
+            lc[e] = inside ? a.n_contrib[pix_id] : 0u;
+            dp0[e] = inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
+            dp1[e] = inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
+            dp2[e] = inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
+            dinv[e] = (inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
+            tb[e] = -Tf[e] * (a.bg[0] * dp0[e] + a.bg[1] * dp1[e] + a.bg[2] * dp2[e]);
+            qmax[2 * h + e] = __builtin_amdgcn_readfirstlane(wave_max_u32(lc[e]));
+        }
+        BwdPair& s = st[h];
+        s.T = {Tf[0], Tf[1]};
+        s.tb = {tb[0], tb[1]};
+        s.dp0 = {dp0[0], dp0[1]};
+        s.dp1 = {dp1[0], dp1[1]};
+        s.dp2 = {dp2[0], dp2[1]};
+        s.dinv = {dinv[0], dinv[1]};
+        s.acc0 = s.acc1 = s.acc2 = s.acc_inv = (v2f)(0.f);
+        s.lc0 = lc[0];
+        s.lc1 = lc[1];
     }
     const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
 
@@ -394,11 +445,14 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                     const uint32_t mj = __builtin_amdgcn_readfirstlane(s_mask[j]);
                     const uint32_t pos = (uint32_t)(p_hi - 1 - j);
                     const float4 xy = s_rec[0][j], co = s_rec[1][j], col = s_rec[2][j];
-                    float* o = v + jj * GF_NUM;
+                    const Falloff f = falloff(co);
+                    v2f o[GF_NUM];
 #pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if (mj & (1u << q))
-                            bwd_pixel(st[q], pfx0 + 8.f * (q & 1), pfy0 + 8.f * (q >> 1), pos, xy, co, col, has_inv, o);
+                    for (int q = 0; q < GF_NUM; q++) o[q] = (v2f)(0.f);
+                    if (mj & 3u) bwd_pair<HAS_INV>(st[0], pfx, py0, pos, xy, f, co, col, o);
+                    if (mj & 12u) bwd_pair<HAS_INV>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
+#pragma unroll
+                    for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
                 }
             }
             const float r = wave_transpose_reduce64(v, lane);
@@ -423,7 +477,10 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(T), dim3(64), 0, s, a);
+    if (a.dL_invdepths)
+        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(64), 0, s, a);
+    else
+        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(64), 0, s, a);
     return hipGetLastError();
 }
 

@@ -264,3 +264,49 @@ def test_hip_matches_golden_fixture(path):
             assert ok_, f"{path}: grad {k} rel err {rel:.3e}"
     ok_, rel = common.allclose_rel(means2D.grad.detach().cpu().numpy(), z["dL_dmean2D"])
     assert ok_, f"{path}: grad means2D rel err {rel:.3e}"
+
+
+def test_callback_forward_matches_split_forward():
+    """gsr_forward (the Rasterizer::forward form with resize callbacks, rasterizer.h:31-55 and
+    rasterize_points.cu:27-33; the binding INTEGRATION.md shows) gives the same image, radii and
+    L as the two-phase entry points the Python package uses."""
+    import ctypes
+    dgr = _dgr()
+    lib = dgr._C.lib
+    case = common.make_case()
+    s = _settings(case)
+    sc = {k: v.to(DEV).contiguous() for k, v in case["scene"].items()}
+    P, H, W = sc["means3D"].shape[0], case["H"], case["W"]
+    RESIZE = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+    V, I, F, B = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_bool
+    lib.gsr_forward.argtypes = [RESIZE, V, RESIZE, V, RESIZE, V, I, I, I, V, I, I, V, V, V, V, V, F, V, V, V, V, V,
+                                F, F, B, V, V, B, V, B, V, ctypes.POINTER(I)]
+    bufs = [torch.empty(0, dtype=torch.uint8, device=DEV) for _ in range(3)]
+
+    def resizer(k):
+        def f(_ctx, n):
+            bufs[k].resize_(n)
+            return bufs[k].data_ptr()
+        return RESIZE(f)
+
+    rg, rb, ri = resizer(0), resizer(1), resizer(2)
+    view, proj = s.viewmatrix.contiguous(), s.projmatrix.contiguous()  # the settings hold transposed views
+    color = torch.zeros((3, H, W), device=DEV)
+    inv = torch.zeros((1, H, W), device=DEV)
+    radii = torch.zeros((P,), dtype=torch.int32, device=DEV)
+    L = ctypes.c_int(0)
+    rc = lib.gsr_forward(rg, None, rb, None, ri, None, P, 3, 16, s.bg.data_ptr(), W, H, sc["means3D"].data_ptr(),
+                         sc["shs"].data_ptr(), None, sc["opacities"].data_ptr(), sc["scales"].data_ptr(), 1.0,
+                         sc["rotations"].data_ptr(), None, view.data_ptr(), proj.data_ptr(),
+                         s.campos.data_ptr(), s.tanfovx, s.tanfovy, False, color.data_ptr(), inv.data_ptr(), False,
+                         radii.data_ptr(), False, torch.cuda.current_stream(DEV).cuda_stream, ctypes.byref(L))
+    assert rc == 0, lib.gsr_last_error()
+    L2, color2, radii2, _, _, _, inv2 = dgr._C.rasterize_gaussians(
+        s.bg, sc["means3D"], torch.Tensor([]), sc["opacities"], sc["scales"], sc["rotations"], 1.0,
+        torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, H, W, sc["shs"], 3, s.campos, False,
+        False, False)
+    torch.cuda.synchronize()
+    assert L.value == L2 > 0
+    assert bufs[1].numel() >= lib.gsr_binning_buffer_size(L2)
+    assert torch.equal(radii, radii2)
+    assert torch.equal(color, color2) and torch.equal(inv, inv2)

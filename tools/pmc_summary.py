@@ -12,10 +12,12 @@ import os
 import sys
 
 SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_reduce_kernel": "scan", "scan_apply_kernel": "scan",
-         "scan_blocksums_kernel": "scan", "duplicate_with_keys_kernel": "duplicate_with_keys",
-         "finalize_kernel": "finalize_ranges", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
-         "preprocess_bwd_kernel": "preprocess_bwd", "depth_sort": "sort_pairs", "onesweep": "sort_pairs",
-         "radix": "sort_pairs", "emit_": "duplicate_with_keys", "tile_sort": "sort_pairs"}
+         "scan_blocksums_kernel": "scan", "emit_instances_kernel": "emit_instances",
+         "tile_ranges_kernel": "tile_ranges", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
+         "preprocess_bwd_kernel": "preprocess_bwd",
+         # the depth sort and the tile sort share these kernels: reported together, per step
+         "radix_histogram_kernel": "radix_sorts", "radix_digit_scan_kernel": "radix_sorts",
+         "onesweep_kernel": "radix_sorts"}
 
 
 def short_name(k):
