@@ -239,14 +239,14 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
     {
         char* tmp = gb + g.off[GEOM_DSORT_TMP];
-        const size_t p = (size_t)P;
+        const size_t q = align_up(4 * (size_t)P, 256);
         uint32_t* k0 = reinterpret_cast<uint32_t*>(tmp);
-        uint2* v0 = reinterpret_cast<uint2*>(tmp + align_up(4 * p, 256));
-        uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + align_up(4 * p, 256) + align_up(8 * p, 256));
-        uint2* v1 = reinterpret_cast<uint2*>(tmp + 2 * align_up(4 * p, 256) + align_up(8 * p, 256));
+        uint32_t* v0 = reinterpret_cast<uint32_t*>(tmp + q);
+        uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + 2 * q);
+        uint32_t* v1 = reinterpret_cast<uint32_t*>(tmp + 3 * q);
         ProfScope ps_(PK_DEPTH_SORT, s);
-        HIP_TRY(radix_sort(P, DEPTH_PASSES, a.dkey, nullptr, k0, v0, k1, v1, nullptr, nullptr, sorted_ids, nullptr,
-                           nullptr, gb + g.off[GEOM_RADIX_SCRATCH], flags + 1, s));
+        HIP_TRY(radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
+                           gb + g.off[GEOM_RADIX_SCRATCH], s));
     }
     DEBUG_SYNC(s);
 
@@ -268,7 +268,6 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     HIP_TRY(hipStreamSynchronize(s));
     if (h[1] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (h[2]) return fail(GSR_ERR_HIP, "radix sort look-back did not complete");
     if (h[0] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
     *num_rendered = (int)h[0];
     return GSR_OK;
@@ -293,21 +292,21 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     const int T = (int)(gx * gy);
     const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
-    uint32_t* flags = at<uint32_t>(gb, g.off[GEOM_FLAGS]);
     uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     uint32_t* sorted_tiles = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr;
-    uint32_t* inv = L > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
+    uint32_t* slot = L > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     uint32_t* emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     if (L > 0) {
         // emission arrays and sort ping-pong live in the (not yet used) gradient-record region
         const size_t n = (size_t)L;
         char* w = bb + b.off[BIN_GRAD_INST];
+        const size_t q = align_up(4 * n, 256);
         uint32_t* tile_keys = reinterpret_cast<uint32_t*>(w);
-        uint32_t* gids = reinterpret_cast<uint32_t*>(w + align_up(4 * n, 256));
-        uint32_t* k0 = reinterpret_cast<uint32_t*>(w + 2 * align_up(4 * n, 256));
-        uint2* v0 = reinterpret_cast<uint2*>(w + 3 * align_up(4 * n, 256));
-        uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * align_up(4 * n, 256) + align_up(8 * n, 256));
-        uint2* v1 = reinterpret_cast<uint2*>(w + 4 * align_up(4 * n, 256) + align_up(8 * n, 256));
+        uint32_t* gids = reinterpret_cast<uint32_t*>(w + q);
+        uint32_t* k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
+        uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
+        uint32_t* v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
+        uint32_t* v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
         {
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
@@ -317,11 +316,10 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
         DEBUG_SYNC(s);
         // stable sort by tile id over bits [0, bit) (rasterizer_impl.cu:303-311 sorts [0, 32+bit))
         const int bit = (int)higher_msb(gx * gy);
-        const int npass = bit <= 8 ? 1 : (bit + 7) / 8;
         {
             ProfScope ps_(PK_TILE_SORT, s);
-            HIP_TRY(radix_sort(L, npass, tile_keys, gids, k0, v0, k1, v1, nullptr, nullptr, point_list, inv,
-                               sorted_tiles, bb + b.off[BIN_RADIX_SCRATCH], flags + 1, s));
+            HIP_TRY(radix_sort(L, bit, tile_keys, gids, k0, v0, k1, v1, slot, point_list, sorted_tiles,
+                               bb + b.off[BIN_RADIX_SCRATCH], s));
         }
         DEBUG_SYNC(s);
     }
@@ -340,6 +338,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     r.bg = background;
     r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.out_color = out_color;
     r.invdepth = depth;
     {
@@ -347,14 +346,6 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
         HIP_TRY(launch_render_fwd(r, T, s));
     }
     DEBUG_SYNC(s);
-    if (debug) {
-        uint32_t* h;
-        int rc = pinned(&h);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpyAsync(h, flags + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        if (h[0]) return fail(GSR_ERR_HIP, "radix sort look-back did not complete");
-    }
     return GSR_OK;
 }
 
@@ -420,9 +411,11 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
+    r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     if (R > 0) {
         {
             ProfScope ps_(PK_RENDER_BWD, s);
@@ -445,7 +438,6 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.campos = campos;
     p.antialiasing = antialiasing;
     p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
-    p.inv = R > 0 ? at<uint32_t>(bb, b.off[BIN_INV]) : nullptr;
     p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     p.has_invdepth = dL_invdepths != nullptr;

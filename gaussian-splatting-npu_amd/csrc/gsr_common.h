@@ -148,8 +148,8 @@ enum GeomArray {
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
     GEOM_EMIT_START,      // u32[P] first emission slot of each Gaussian
-    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, u32x2[P] v0, u32[P] k1, u32x2[P] v1
-    GEOM_RADIX_SCRATCH,   // look-back status + histograms of the depth sort
+    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
+    GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
     GEOM_SCAN_SCRATCH,    // u32[scan blocks + 64]
     GEOM_FLAGS,           // u32[64] error flags / misc
     GEOM_COUNT
@@ -159,22 +159,22 @@ enum ImageArray {
     IMG_RANGES = 0,       // u32x2[T]
     IMG_FINAL_T,          // f32[N]
     IMG_N_CONTRIB,        // u32[N]
+    IMG_ACCUM,            // f32x4[N] blended colour before the background + blended inverse depth
     IMG_COUNT
 };
 
 enum BinArray {
     BIN_POINT_LIST = 0,   // u32[L] Gaussian id of sorted position
     BIN_SORTED_TILES,     // u32[L] tile id of sorted position
-    BIN_INV,              // u32[L] sorted position of emission slot e
+    BIN_SLOT,             // u32[L] emission slot of sorted position
     BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
                           // it hosts the emission arrays and sort ping-pong buffers (32 B/instance)
-    BIN_RADIX_SCRATCH,    // look-back status + histograms of the tile sort
+    BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
     BIN_COUNT
 };
 
 constexpr int SCAN_ITEMS = 4096;  // items per scan block (256 threads x 16)
-constexpr int DEPTH_PASSES = 4;   // 32-bit depth keys
-constexpr int MAX_TILE_PASSES = 4;
+constexpr int DEPTH_BITS = 32;  // depth keys are full float bit patterns
 
 struct GeomLayout { size_t off[GEOM_COUNT + 1]; };
 struct ImageLayout { size_t off[IMG_COUNT + 1]; };
@@ -186,7 +186,7 @@ inline GeomLayout geom_layout(int P)
 {
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p, 48 * p,
-                                4 * p, 4 * p, 4 * p, 24 * p + 1024, radix_status_bytes(P, DEPTH_PASSES),
+                                4 * p, 4 * p, 4 * p, 16 * p + 1024, radix_status_bytes(P, 4),
                                 4 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 64), 4 * 64};
     GeomLayout l;
     size_t o = 0;
@@ -199,7 +199,7 @@ inline ImageLayout image_layout(int W, int H)
 {
     size_t n = (size_t)W * H;
     size_t t = (size_t)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X) * ((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
-    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n};
+    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n, 16 * n};
     ImageLayout l;
     size_t o = 0;
     for (int i = 0; i < IMG_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
@@ -210,7 +210,7 @@ inline ImageLayout image_layout(int W, int H)
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, MAX_TILE_PASSES)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, 4)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -46,6 +46,7 @@ struct RenderFwdArgs {
     uint32_t* n_contrib;
     float* out_color;
     float* invdepth;
+    float4* accum;  // IMG_ACCUM: {C_r, C_g, C_b, invdepth} before the background
 };
 
 struct RenderBwdArgs {
@@ -57,9 +58,11 @@ struct RenderBwdArgs {
     const float4* splat;
     const float* final_Ts;
     const uint32_t* n_contrib;
+    const float4* accum;  // IMG_ACCUM written by the forward
     const float* dL_dpixels;
     const float* dL_invdepths;  // (1,H,W) or null
-    float* grad_inst;           // f32x12[L]: one gradient record per sorted (tile, Gaussian) entry
+    const uint32_t* slot;       // emission slot of each sorted position
+    float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
 };
 
 // Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  The mean2D and conic
@@ -88,8 +91,8 @@ struct PreprocessBwdArgs {
     const float* campos;
     int antialiasing;
     // per-instance gradient records and the gather map
-    const float* grad_inst;         // f32x12[L] sorted order
-    const uint32_t* inv;            // sorted position of emission slot e
+    const float* grad_inst;         // f32x12[L], emission order
+    // (records are stored at emission slots: Gaussian i's are [emit_start[i], +tiles_touched[i]))
     const uint32_t* emit_start;     // first emission slot of Gaussian i
     const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
     int has_invdepth;
@@ -114,9 +117,9 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
                                  hipStream_t s);
 
-hipError_t radix_sort(int n, int npass, const uint32_t* keys_in, const uint32_t* vals32_in, uint32_t* k0, uint2* v0,
-                      uint32_t* k1, uint2* v1, uint32_t* keys_final, uint2* vals_final, uint32_t* point_list,
-                      uint32_t* inv, uint32_t* sorted_keys, char* scratch, uint32_t* error, hipStream_t s);
+hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
+                      uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
+                      char* scratch, hipStream_t s);
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
                                  const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
                                  uint32_t* emit_start, hipStream_t s);

@@ -1,4 +1,4 @@
-// radix.hip -- stable LSD onesweep radix sort for gfx950 (replaces the reference's
+// radix.hip -- stable LSD radix sort for gfx950 (replaces the reference's
 // cub::DeviceRadixSort::SortPairs, rasterizer_impl.cu:303-311), and the depth-first
 // binning built on it.
 //
@@ -7,115 +7,131 @@
 //      culled Gaussians carry key 0xFFFFFFFF and land last);
 //   2. emit (tile, Gaussian) instances in that depth order (y-major, then x, inside each
 //      Gaussian's rect, exactly like duplicateWithKeys, rasterizer_impl.cu:98-109);
-//   3. stable-sort the instances by tile id alone: ceil(bit/8) passes of 8 bits (2 at 1080p)
-//      instead of the reference's ceil((32+bit)/8) passes over 12-byte pairs.
+//   3. stable-sort the instances by tile id alone: ceil(bit/8) passes over bit = msb(T) bits
+//      (2 at 1080p) instead of the reference's ceil((32+bit)/8) passes over 12-byte pairs.
 // Because both sorts are stable, every tile's list comes out ordered by (depth bits,
 // Gaussian index) -- the reference's order -- and the sorted key array
 // (tile << 32 | depth bits) is bit-identical to the reference's.
 //
-// One pass = one kernel: each 256-thread workgroup takes the next 4096-element chunk
-// (atomic ticket, so chunk c-1 is always already running), ranks its elements stably per
-// 8-bit digit (wave-level ballot match + per-wave running counters in LDS), publishes its
-// per-digit counts and resolves its global offsets by decoupled look-back over the
-// previous chunks' status words (64-bit {flag, count} granules, relaxed agent-scope
-// atomics: the data is the flag), then scatters through LDS so that global writes are
-// contiguous runs per digit.
+// One pass = three kernels, no inter-workgroup waiting: (1) every 4096-element chunk counts
+// its digits (digit-major count matrix); (2) one workgroup per digit scans that digit's row
+// over the chunks; (3) every chunk ranks its elements stably per digit (wave-level ballot
+// match + per-wave running counters in LDS), adds the digit's offset (exclusive scan of the
+// 2^bits digit totals, redone in LDS by each chunk) and its row prefix, and scatters through
+// LDS so that global writes are contiguous runs per digit.  Digit widths are balanced over
+// the passes (the tile sort at 1080p: 13 bits = 7 + 6).  The payload is one u32 (the
+// element's input index in pass 1).
 #include "gsr_common.h"
 #include "gsr_kernels.h"
+
+#include <type_traits>
 
 namespace gsr {
 
 constexpr int RS_THREADS = 256;
 constexpr int RS_ITEMS = 16;
 constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 elements per chunk
-constexpr int RS_BINS = 256;
-constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_MASK = 3ull << 62;
-constexpr uint32_t SPIN_LIMIT = 1u << 22;
+constexpr int RS_MAXBINS = 256;
 
-__device__ __forceinline__ uint64_t ld_status(const uint64_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_status(uint64_t* p, uint64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
-// Histograms of every 8-bit digit pass at once: hist[p * 256 + d].
-__global__ void __launch_bounds__(RS_THREADS) radix_histogram_kernel(const uint32_t* keys, int n, int npass,
-                                                                    uint32_t* hist)
+// (1) counts[d * nchunks + c] = number of elements of chunk c with digit d.
+__global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t* keys, int n, int shift, int nbits,
+                                                                int nchunks, uint32_t* counts)
 {
-    __shared__ uint32_t h[4][RS_BINS];
-    for (int p = 0; p < 4; p++) h[p][threadIdx.x] = 0;
+    __shared__ uint32_t h[4][RS_MAXBINS];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const uint32_t nb = 1u << nbits, mask = nb - 1u;
+    for (int q = 0; q < 4; q++) h[q][tid] = 0;
     __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * RS_THREADS + threadIdx.x; i < (size_t)n; i += (size_t)gridDim.x * RS_THREADS) {
-        const uint32_t k = keys[i];
-        for (int p = 0; p < npass; p++) atomicAdd(&h[p][(k >> (8 * p)) & 255u], 1u);
+    const size_t base = (size_t)blockIdx.x * RS_TILE;
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; i++) {
+        const size_t gi = base + (size_t)i * RS_THREADS + tid;
+        if (gi < (size_t)n) atomicAdd(&h[w][digit_of(keys[gi], shift, mask)], 1u);
     }
     __syncthreads();
-    for (int p = 0; p < npass; p++) {
-        const uint32_t c = h[p][threadIdx.x];
-        if (c) atomicAdd(&hist[p * RS_BINS + threadIdx.x], c);
-    }
+    if ((uint32_t)tid < nb) counts[(size_t)tid * nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-// In-place exclusive scan of each pass's 256-bin histogram (one block, thread = bin).
-__global__ void __launch_bounds__(RS_THREADS) radix_digit_scan_kernel(uint32_t* hist, int npass)
+// (2) one workgroup per digit: exclusive scan of counts[d, 0..nchunks) in place; the row total
+// goes to totals[d].
+__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(uint32_t* counts, int nchunks, uint32_t* totals)
 {
-    __shared__ uint32_t s[RS_BINS];
-    for (int p = 0; p < npass; p++) {
-        const uint32_t v = hist[p * RS_BINS + threadIdx.x];
-        s[threadIdx.x] = v;
-        __syncthreads();
-        for (int d = 1; d < RS_BINS; d <<= 1) {
-            const uint32_t a = threadIdx.x >= (unsigned)d ? s[threadIdx.x - d] : 0u;
-            __syncthreads();
-            s[threadIdx.x] += a;
-            __syncthreads();
+    __shared__ uint32_t s_wave[4];
+    __shared__ uint32_t s_carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t* row = counts + (size_t)blockIdx.x * nchunks;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (int c0 = 0; c0 < nchunks; c0 += RS_THREADS) {
+        const int c = c0 + tid;
+        const uint32_t v = c < nchunks ? row[c] : 0u;
+        uint32_t x = v;  // inclusive wave scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+            if (lane >= d) x += y;
         }
-        hist[p * RS_BINS + threadIdx.x] = s[threadIdx.x] - v;
+        if (lane == 63) s_wave[w] = x;
+        __syncthreads();
+        uint32_t wpre = s_carry;
+        for (int q = 0; q < w; q++) wpre += s_wave[q];
+        if (c < nchunks) row[c] = wpre + x - v;
+        __syncthreads();
+        if (tid == RS_THREADS - 1) s_carry = wpre + x;
         __syncthreads();
     }
+    if (tid == 0) totals[blockIdx.x] = s_carry;
 }
 
-struct OnesweepArgs {
-    int n;
-    int shift;
+struct SortPassArgs {
+    int n, shift, nbits, nchunks;
     const uint32_t* keys_in;
-    const uint2* vals_in;       // payload in (null: synthesise {vals32_in[i] or i, i})
-    const uint32_t* vals32_in;  // optional first-pass payload .x
-    uint32_t* keys_out;
-    uint2* vals_out;
-    // final tile-sort mode (vals_out == null): point_list[dst] = v.x, inv[v.y] = dst, tiles[dst] = key
-    uint32_t* point_list;
-    uint32_t* inv;
+    const uint32_t* vals_in;   // payload in; null: .x = input index (and .y = gids[index] when paired)
+    const uint32_t* gids;      // paired sorts: second payload word of the first pass
+    uint32_t* keys_out;        // intermediate pass: keys_out[dst], vals_out[dst] (u32 or u32x2)
+    uint32_t* vals_out;
+    // final pass (keys_out == null): out_x[dst] = v.x, out_y[dst] = v.y, sorted_keys[dst] = key
+    uint32_t* out_x;
+    uint32_t* out_y;
     uint32_t* sorted_keys;
-    const uint32_t* digit_offsets;  // exclusive digit offsets of this pass (256)
-    uint64_t* status;               // nchunks * 256 zeroed granules
-    uint32_t* ticket;               // zeroed chunk counter
-    uint32_t* error;                // set to 1 if a look-back spin gives up
+    const uint32_t* row_prefix;  // (nbins, nchunks) exclusive row scans
+    const uint32_t* totals;      // (nbins) digit totals
 };
 
-__global__ void __launch_bounds__(RS_THREADS) onesweep_kernel(OnesweepArgs a)
+// (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
+template <bool PAIR>
+__global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs a)
 {
-    __shared__ uint32_t s_cnt[4][RS_BINS];  // per-wave running digit counts, then per-wave prefixes
-    __shared__ uint32_t s_blk[RS_BINS];     // block-local start of each digit
-    __shared__ uint32_t s_base[RS_BINS];    // global start of each digit for this chunk
+    using Val = typename std::conditional<PAIR, uint2, uint32_t>::type;
+    __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
+    __shared__ uint32_t s_blk[RS_MAXBINS];     // block-local start of each digit
+    __shared__ uint32_t s_base[RS_MAXBINS];    // global start of each digit for this chunk
     __shared__ uint32_t s_keys[RS_TILE];
-    __shared__ uint2 s_vals[RS_TILE];
-    __shared__ uint32_t s_chunk;
+    __shared__ Val s_vals[RS_TILE];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_chunk = atomicAdd(a.ticket, 1u);
+    const uint32_t nb = 1u << a.nbits, mask = nb - 1u;
+    const uint32_t chunk = blockIdx.x;
     for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
+    // digit offsets: exclusive scan of the totals (in s_base), plus this chunk's row prefix
+    const uint32_t tot = (uint32_t)tid < nb ? a.totals[tid] : 0u;
+    const uint32_t rowp = (uint32_t)tid < nb ? a.row_prefix[(size_t)tid * a.nchunks + chunk] : 0u;
+    s_base[tid] = tot;
     __syncthreads();
-    const uint32_t chunk = s_chunk;
+    for (int d = 1; d < RS_MAXBINS; d <<= 1) {
+        const uint32_t v = tid >= d ? s_base[tid - d] : 0u;
+        __syncthreads();
+        s_base[tid] += v;
+        __syncthreads();
+    }
+    const uint32_t gbase = s_base[tid] - tot + rowp;
+
     const size_t base = (size_t)chunk * RS_TILE;
     const int nvalid = (int)min((size_t)RS_TILE, (size_t)a.n - base);
-
-    uint32_t key[RS_ITEMS];
-    uint2 val[RS_ITEMS];
-    uint32_t rank[RS_ITEMS];
+    uint32_t key[RS_ITEMS], rank[RS_ITEMS];
+    Val val[RS_ITEMS];
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int i = 0; i < RS_ITEMS; i++) {
@@ -123,12 +139,15 @@ __global__ void __launch_bounds__(RS_THREADS) onesweep_kernel(OnesweepArgs a)
         const bool valid = li < nvalid;
         const size_t gi = base + li;
         key[i] = valid ? a.keys_in[gi] : 0u;
-        if (a.vals_in) val[i] = valid ? a.vals_in[gi] : make_uint2(0u, 0u);
-        else val[i] = make_uint2(valid ? (a.vals32_in ? a.vals32_in[gi] : (uint32_t)gi) : 0u, (uint32_t)gi);
-        const uint32_t d = (key[i] >> a.shift) & 255u;
+        if constexpr (PAIR) {
+            if (a.vals_in) val[i] = valid ? reinterpret_cast<const uint2*>(a.vals_in)[gi] : make_uint2(0u, 0u);
+            else val[i] = make_uint2((uint32_t)gi, valid ? a.gids[gi] : 0u);
+        } else {
+            val[i] = valid ? (a.vals_in ? a.vals_in[gi] : (uint32_t)gi) : 0u;
+        }
+        const uint32_t d = digit_of(key[i], a.shift, mask);
         uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = 0; b < a.nbits; b++) {
             const uint64_t bal = __ballot((d >> b) & 1u);
             peers &= ((d >> b) & 1u) ? bal : ~bal;
         }
@@ -147,52 +166,25 @@ __global__ void __launch_bounds__(RS_THREADS) onesweep_kernel(OnesweepArgs a)
     s_cnt[1][tid] = c0;
     s_cnt[2][tid] = c0 + c1;
     s_cnt[3][tid] = c0 + c1 + c2;
-    // publish this chunk's aggregate for digit tid as early as possible
-    uint64_t* st = a.status + (size_t)chunk * RS_BINS + tid;
-    if (chunk == 0) st_status(st, ST_INC | total);
-    else st_status(st, ST_AGG | total);
-    // block-local exclusive scan of totals over digits
     s_blk[tid] = total;
     __syncthreads();
-    for (int d = 1; d < RS_BINS; d <<= 1) {
+    for (int d = 1; d < RS_MAXBINS; d <<= 1) {
         const uint32_t v = tid >= d ? s_blk[tid - d] : 0u;
         __syncthreads();
         s_blk[tid] += v;
         __syncthreads();
     }
     const uint32_t blk_start = s_blk[tid] - total;
-    // decoupled look-back for digit tid
-    uint32_t prefix = 0;
-    if (chunk > 0) {
-        int j = (int)chunk - 1;
-        while (j >= 0) {
-            const uint64_t* sp = a.status + (size_t)j * RS_BINS + tid;
-            uint64_t s = ld_status(sp);
-            uint32_t spins = 0;
-            while ((s & ST_MASK) == 0ull && ++spins < SPIN_LIMIT) {
-                __builtin_amdgcn_s_sleep(1);
-                s = ld_status(sp);
-            }
-            if ((s & ST_MASK) == 0ull) {
-                atomicOr(a.error, 1u);
-                break;
-            }
-            prefix += (uint32_t)s;
-            if ((s & ST_MASK) == ST_INC) break;
-            j--;
-        }
-        st_status(st, ST_INC | (prefix + total));
-    }
     __syncthreads();
     s_blk[tid] = blk_start;
-    s_base[tid] = a.digit_offsets[tid] + prefix;
+    s_base[tid] = gbase;
     __syncthreads();
 
     // scatter into LDS in block-local sorted (stable) order
 #pragma unroll
     for (int i = 0; i < RS_ITEMS; i++) {
         if (rank[i] != 0xFFFFFFFFu) {
-            const uint32_t d = (key[i] >> a.shift) & 255u;
+            const uint32_t d = digit_of(key[i], a.shift, mask);
             const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
             s_keys[lpos] = key[i];
             s_vals[lpos] = val[i];
@@ -205,15 +197,19 @@ __global__ void __launch_bounds__(RS_THREADS) onesweep_kernel(OnesweepArgs a)
         const int lpos = i * RS_THREADS + tid;
         if (lpos < nvalid) {
             const uint32_t k = s_keys[lpos];
-            const uint32_t d = (k >> a.shift) & 255u;
+            const uint32_t d = digit_of(k, a.shift, mask);
             const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
-            const uint2 v = s_vals[lpos];
-            if (a.vals_out) {
+            const Val v = s_vals[lpos];
+            if (a.keys_out) {
                 a.keys_out[dst] = k;
-                a.vals_out[dst] = v;
+                reinterpret_cast<Val*>(a.vals_out)[dst] = v;
             } else {
-                if (a.point_list) a.point_list[dst] = v.x;
-                if (a.inv) a.inv[v.y] = dst;
+                if constexpr (PAIR) {
+                    if (a.out_x) a.out_x[dst] = v.x;
+                    if (a.out_y) a.out_y[dst] = v.y;
+                } else {
+                    if (a.out_x) a.out_x[dst] = v;
+                }
                 if (a.sorted_keys) a.sorted_keys[dst] = k;
             }
         }
@@ -270,57 +266,58 @@ __global__ void __launch_bounds__(256) debug_keys_kernel(int L, const uint32_t* 
     keys[idx] = ((uint64_t)sorted_tiles[idx] << 32) | __float_as_uint(depths[point_list[idx]]);
 }
 
+static inline size_t rs_chunks(int n) { return ((size_t)(n > 0 ? n : 0) + RS_TILE - 1) / RS_TILE; }
+
+// Scratch of one sort: the (bins x chunks) count matrix and the bin totals (reused by every pass).
 size_t radix_status_bytes(int n, int npass)
 {
-    const size_t chunks = ((size_t)(n > 0 ? n : 0) + RS_TILE - 1) / RS_TILE;
-    return align_up((size_t)npass * (chunks * RS_BINS * 8 + 256) + (size_t)npass * RS_BINS * 4 + 256, 256);
+    (void)npass;
+    return align_up(rs_chunks(n) * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
 }
 
-// Full LSD sort of n (key, payload) pairs over `npass` 8-bit digits starting at bit 0.
-// scratch: radix_status_bytes(n, npass) bytes.  Ping-pongs between (k0,v0) and (k1,v1);
-// the last pass either writes (keys_final, vals_final) or the final tile outputs.
-hipError_t radix_sort(int n, int npass, const uint32_t* keys_in, const uint32_t* vals32_in, uint32_t* k0, uint2* v0,
-                      uint32_t* k1, uint2* v1, uint32_t* keys_final, uint2* vals_final, uint32_t* point_list,
-                      uint32_t* inv, uint32_t* sorted_keys, char* scratch, uint32_t* error, hipStream_t s)
+// Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, and
+// with `gids` also gids[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
+// gids); the last pass writes out_x[dst] = i, out_y[dst] = gids[i] and sorted_keys[dst] = key
+// (any of them may be null).  All writes are contiguous runs: no gathers, no scattered stores.
+hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
+                      uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
+                      char* scratch, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
-    const size_t chunks = ((size_t)n + RS_TILE - 1) / RS_TILE;
-    const size_t per_pass = chunks * RS_BINS * 8 + 256;
-    uint32_t* hist = reinterpret_cast<uint32_t*>(scratch + (size_t)npass * per_pass);
-    hipError_t e = hipMemsetAsync(scratch, 0, radix_status_bytes(n, npass), s);
-    if (e != hipSuccess) return e;
-    const int hgrid = (int)min((size_t)1024, (size_t)(n + RS_THREADS - 1) / RS_THREADS);
-    hipLaunchKernelGGL(radix_histogram_kernel, dim3(hgrid), dim3(RS_THREADS), 0, s, keys_in, n, npass, hist);
-    hipLaunchKernelGGL(radix_digit_scan_kernel, dim3(1), dim3(RS_THREADS), 0, s, hist, npass);
+    const int nchunks = (int)rs_chunks(n);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
+    uint32_t* totals = reinterpret_cast<uint32_t*>(scratch + align_up((size_t)nchunks * RS_MAXBINS * 4 + 256, 256));
+    if (nbits < 1) nbits = 1;
+    const int npass = (nbits + 7) / 8;
     const uint32_t* kin = keys_in;
-    const uint2* vin = nullptr;
+    const uint32_t* vin = nullptr;
+    int shift = 0;
     for (int p = 0; p < npass; p++) {
+        const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
         const bool last = p == npass - 1;
-        OnesweepArgs a;
+        hipLaunchKernelGGL(radix_count_kernel, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, kin, n, shift, w,
+                           nchunks, counts);
+        hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks, totals);
+        SortPassArgs a;
         a.n = n;
-        a.shift = 8 * p;
+        a.shift = shift;
+        a.nbits = w;
+        a.nchunks = nchunks;
         a.keys_in = kin;
         a.vals_in = vin;
-        a.vals32_in = p == 0 ? vals32_in : nullptr;
-        uint32_t* ko = (p & 1) ? k1 : k0;
-        uint2* vo = (p & 1) ? v1 : v0;
-        if (last) {
-            ko = keys_final;
-            vo = vals_final;
-        }
-        a.keys_out = ko;
-        a.vals_out = vo;
-        a.point_list = point_list;
-        a.inv = inv;
+        a.gids = gids;
+        a.keys_out = last ? nullptr : ((p & 1) ? k1 : k0);
+        a.vals_out = last ? nullptr : ((p & 1) ? v1 : v0);
+        a.out_x = out_x;
+        a.out_y = out_y;
         a.sorted_keys = sorted_keys;
-        a.digit_offsets = hist + p * RS_BINS;
-        char* pass_base = scratch + (size_t)p * per_pass;
-        a.status = reinterpret_cast<uint64_t*>(pass_base + 256);
-        a.ticket = reinterpret_cast<uint32_t*>(pass_base);
-        a.error = error;
-        hipLaunchKernelGGL(onesweep_kernel, dim3((unsigned)chunks), dim3(RS_THREADS), 0, s, a);
-        kin = ko;
-        vin = vo;
+        a.row_prefix = counts;
+        a.totals = totals;
+        if (gids) hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, a);
+        else hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, a);
+        kin = a.keys_out;
+        vin = a.vals_out;
+        shift += w;
     }
     return hipGetLastError();
 }

@@ -212,6 +212,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
         a.out_color[1 * HW + pix_id] = C1 + T * a.bg[1];
         a.out_color[2 * HW + pix_id] = C2 + T * a.bg[2];
         if (a.invdepth) a.invdepth[pix_id] = ID;
+        a.accum[pix_id] = make_float4(C0, C1, C2, ID);
     }
 }
 
@@ -275,22 +276,29 @@ __device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64], int lan
 
 
 
-// State of two pixels of the backward replay (backward.cu:498-528).  Pixels outside the image
-// carry last_contributor = 0, so no list entry contributes to them.  acc* is the reference's
-// accum_rec already folded with the previous contributor (backward.cu:577-583 evaluated
-// eagerly), so last_color / last_alpha need no registers.
+// State of two pixels of the backward pass (backward.cu:498-528, restated front to back).
+// Pixels outside the image carry last_contributor = 0, so no list entry contributes to them.
+//
+// The reference replays each pixel's list back to front, rebuilding T by division and the
+// colour behind entry j (accum_rec) incrementally.  The same gradient in forward order:
+// with T_j the transmittance in front of j, cd_j = c_j . dL/dpixel (+ invdepth_j . dL/dinvdepth),
+// Fd_j = sum_{k <= j} alpha_k T_k cd_k and R = out_color . dL/dpixel (+ invdepth . dL/dinvdepth)
+// (out_color includes the background term T_final * bg),
+//     dL/dalpha_j = T_j cd_j - (R - Fd_j) / (1 - alpha_j)            (backward.cu:577-615)
+// because R - Fd_j = (colour behind j) . dL + T_final * (bg . dL).  T_j is then the forward's
+// own running product (bit-identical to forward.cu:372-383), no division by (1 - alpha) is
+// needed to rebuild it, and the per-pixel state shrinks to T, Fd, R and dL/dpixel.
 struct BwdPair {
-    v2f T, tb, dp0, dp1, dp2, dinv;  // tb = -T_final * (bg . dL/dpixel), backward.cu:612-615
-    v2f acc0, acc1, acc2, acc_inv;
-    uint32_t lc0, lc1;               // last_contributor
+    v2f T, R, Fd, dp0, dp1, dp2, dinv;
+    uint32_t lc0, lc1;  // last_contributor
 };
 
-// Two pixels x one Gaussian of backward.cu:552-636, branch-free: a pixel the Gaussian does not
-// contribute to gets alpha = G = 0, which leaves its state bitwise unchanged (T * rcp(1) = T,
-// acc + 0 * d = acc) and adds exact zeros.  Per-Gaussian constant factors are left to
-// preprocess_bwd (see GradField): with u = G * dL/dalpha the record holds sum u (opacity),
-// sum u*(dx*a + dy*b) and sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and
-// sum u*dx*dx, u*dx*dy, u*dy*dy (conic, times -opacity/2).
+// Two pixels x one Gaussian, branch-free: a pixel the Gaussian does not contribute to gets
+// alpha = G = 0, which leaves its state bitwise unchanged (T * (1 - 0) = T, Fd + 0 * cd = Fd)
+// and adds exact zeros.  Per-Gaussian constant factors are left to preprocess_bwd (see
+// GradField): with u = G * dL/dalpha the record holds sum u (opacity), sum u*(dx*a + dy*b) and
+// sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy,
+// u*dy*dy (conic, times -opacity/2).
 template <bool HAS_INV>
 __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_t pos, const float4 xy,
                                          const Falloff f, const float4 co, const float4 col, v2f* o)
@@ -306,25 +314,18 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
     const v2f alpha = {c0 ? alx : 0.f, c1 ? aly : 0.f};
     const v2f Gc = {c0 ? G.x : 0.f, c1 ? G.y : 0.f};
     const v2f one_m = 1.f - alpha;
-    // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:573,615
+    // v_rcp_f32 (1 ulp) in place of the IEEE division of backward.cu:615
     const v2f r_om = {__builtin_amdgcn_rcpf(one_m.x), __builtin_amdgcn_rcpf(one_m.y)};
-    s.T = s.T * r_om;
-    const v2f dch = alpha * s.T;
-    const v2f d0 = (v2f)(col.x) - s.acc0, d1 = (v2f)(col.y) - s.acc1, d2 = (v2f)(col.z) - s.acc2;
-    v2f dL = fma2(d2, s.dp2, fma2(d1, s.dp1, d0 * s.dp0));
-    s.acc0 = fma2(alpha, d0, s.acc0);
-    s.acc1 = fma2(alpha, d1, s.acc1);
-    s.acc2 = fma2(alpha, d2, s.acc2);
-    o[GF_COLOR_R] = fma2(dch, s.dp0, o[GF_COLOR_R]);
-    o[GF_COLOR_G] = fma2(dch, s.dp1, o[GF_COLOR_G]);
-    o[GF_COLOR_B] = fma2(dch, s.dp2, o[GF_COLOR_B]);
-    if constexpr (HAS_INV) {
-        const v2f di = (v2f)(col.w) - s.acc_inv;
-        dL = fma2(di, s.dinv, dL);
-        s.acc_inv = fma2(alpha, di, s.acc_inv);
-        o[GF_INVDEPTH] = fma2(dch, s.dinv, o[GF_INVDEPTH]);
-    }
-    dL = fma2(dL, s.T, s.tb * r_om);
+    v2f cd = fma2((v2f)(col.z), s.dp2, fma2((v2f)(col.y), s.dp1, (v2f)(col.x) * s.dp0));
+    if constexpr (HAS_INV) cd = fma2((v2f)(col.w), s.dinv, cd);
+    const v2f aT = alpha * s.T;  // dL/dcolour / dL/dpixel (backward.cu:586-590)
+    s.Fd = fma2(aT, cd, s.Fd);
+    const v2f dL = fma2(s.T, cd, -(s.R - s.Fd) * r_om);
+    s.T = s.T * one_m;
+    o[GF_COLOR_R] = fma2(aT, s.dp0, o[GF_COLOR_R]);
+    o[GF_COLOR_G] = fma2(aT, s.dp1, o[GF_COLOR_G]);
+    o[GF_COLOR_B] = fma2(aT, s.dp2, o[GF_COLOR_B]);
+    if constexpr (HAS_INV) o[GF_INVDEPTH] = fma2(aT, s.dinv, o[GF_INVDEPTH]);
     const v2f u = Gc * dL;
     const v2f ux = u * dx, uy = u * dy;
     o[GF_OPACITY] += u;
@@ -335,15 +336,15 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
     o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
 }
 
-// Backward: ONE wave per 16x16 tile, each lane replaying 4 pixels as two packed pairs (upper
-// half: quadrants 0|1, lower half: 2|3), so there are no workgroup barriers in the main loop
-// and no cross-wave combine.  Per batch of 64 list entries (back to front from the tile's
-// largest n_contrib) each lane stages one record in LDS and computes its quadrant mask (exact
-// ellipse test + per-quadrant max n_contrib); the wave compacts the surviving entries and,
-// per group of 6, every lane accumulates its pixels' ten gradient terms, the transposed
-// reduction sums the 64 lanes, and lanes 0..59 store the 6 records (10 contiguous floats
-// each).  Entries that survive no quadrant get a zero record.  No atomics: per-(tile,
-// Gaussian) sums are bitwise reproducible.
+// Backward: ONE wave per 16x16 tile, each lane owning 4 pixels as two packed pairs (upper half:
+// quadrants 0|1, lower half: 2|3), so there are no workgroup barriers in the main loop and no
+// cross-wave combine.  The list is walked front to back in batches of 64 entries up to the
+// tile's largest n_contrib; each lane stages one record in LDS and computes its quadrant mask
+// (exact ellipse test + per-quadrant max n_contrib); the surviving entries are taken from the
+// ballot in list order, six at a time: every lane accumulates its pixels' ten gradient terms,
+// the transposed reduction sums the 64 lanes, and lanes 0..59 store the 6 records (10
+// contiguous floats each).  Entries that survive no quadrant get a zero record.  No atomics:
+// per-(tile, Gaussian) sums are bitwise reproducible.
 template <bool HAS_INV>
 __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 {
@@ -355,7 +356,6 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     const uint2 range = a.ranges[tile];
     const int todo = (int)(range.y - range.x);
     const size_t HW = (size_t)a.H * a.W;
-    const bool has_inv = HAS_INV;
     const float px0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
     const float py0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
     const v2f pfx = {px0, px0 + 8.f};
@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     uint32_t qmax[4];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        float Tf[2], dp0[2], dp1[2], dp2[2], dinv[2], tb[2];
+        float dp0[2], dp1[2], dp2[2], dinv[2], R[2];
         uint32_t lc[2];
 #pragma unroll
         for (int e = 0; e < 2; e++) {
@@ -372,44 +372,47 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
             const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * h;
             const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
             const uint32_t pix_id = (uint32_t)a.W * py + px;
-            Tf[e] = inside ? a.final_Ts[pix_id] : 0.f;
+            const float Tf = inside ? a.final_Ts[pix_id] : 0.f;
+            const float4 acc = inside ? a.accum[pix_id] : make_float4(0.f, 0.f, 0.f, 0.f);
             lc[e] = inside ? a.n_contrib[pix_id] : 0u;
             dp0[e] = inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
             dp1[e] = inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
             dp2[e] = inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
-            dinv[e] = (inside && has_inv) ? a.dL_invdepths[pix_id] : 0.f;
-            tb[e] = -Tf[e] * (a.bg[0] * dp0[e] + a.bg[1] * dp1[e] + a.bg[2] * dp2[e]);
+            dinv[e] = (inside && HAS_INV) ? a.dL_invdepths[pix_id] : 0.f;
+            R[e] = (acc.x + Tf * a.bg[0]) * dp0[e] + (acc.y + Tf * a.bg[1]) * dp1[e] +
+                   (acc.z + Tf * a.bg[2]) * dp2[e] + acc.w * dinv[e];
             qmax[2 * h + e] = __builtin_amdgcn_readfirstlane(wave_max_u32(lc[e]));
         }
         BwdPair& s = st[h];
-        s.T = {Tf[0], Tf[1]};
-        s.tb = {tb[0], tb[1]};
+        s.T = (v2f)(1.f);
+        s.R = {R[0], R[1]};
+        s.Fd = (v2f)(0.f);
         s.dp0 = {dp0[0], dp0[1]};
         s.dp1 = {dp1[0], dp1[1]};
         s.dp2 = {dp2[0], dp2[1]};
         s.dinv = {dinv[0], dinv[1]};
-        s.acc0 = s.acc1 = s.acc2 = s.acc_inv = (v2f)(0.f);
         s.lc0 = lc[0];
         s.lc1 = lc[1];
     }
     const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
 
     __shared__ float4 s_rec[3][64];
-    __shared__ uint8_t s_mask[64];
     __shared__ uint8_t s_list[64];
 
     // entries at list positions >= tmax contribute to no pixel: zero records
-    {
-        float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)(range.x + tmax) * GRAD_REC);
-        for (int k = lane; k < (todo - (int)tmax) * (GRAD_REC / 4); k += 64) z[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int pos = (int)tmax + lane; pos < todo; pos += 64) {
+        float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)a.slot[range.x + pos] * GRAD_REC);
+        z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        z[2] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
-    for (int p_hi = (int)tmax; p_hi > 0; p_hi -= 64) {
-        const int p_lo = max(0, p_hi - 64);
-        const int pos_l = p_hi - 1 - lane;  // this lane's entry; lane order = back-to-front
-        uint32_t m = 0;
-        if (pos_l >= p_lo) {
+    for (int p0 = 0; p0 < (int)tmax; p0 += 64) {
+        const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
+        uint32_t m = 0, myslot = 0;
+        if (pos_l < (int)tmax) {
             const uint32_t id = a.point_list[range.x + pos_l];
+            myslot = a.slot[range.x + pos_l];
             const float4* r = a.splat + 3 * (size_t)id;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
             s_rec[0][lane] = r0;
@@ -419,13 +422,12 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
             m &= (uint32_t)((uint32_t)pos_l < qmax[0]) | ((uint32_t)((uint32_t)pos_l < qmax[1]) << 1) |
                  ((uint32_t)((uint32_t)pos_l < qmax[2]) << 2) | ((uint32_t)((uint32_t)pos_l < qmax[3]) << 3);
             if (m == 0) {
-                float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)(range.x + pos_l) * GRAD_REC);
+                float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)myslot * GRAD_REC);
                 z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
                 z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
                 z[2] = make_float4(0.f, 0.f, 0.f, 0.f);
             }
         }
-        s_mask[lane] = (uint8_t)m;
         const uint64_t b = __ballot(m != 0);
         const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
         if (m != 0) s_list[before] = (uint8_t)lane;
@@ -434,17 +436,31 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
+        // Surviving entries in list order straight from the ballot (scalar bit scan); each
+        // record is read from LDS one entry ahead of its use.
+        uint64_t rem = b;
         for (int g0 = 0; g0 < cnt; g0 += G) {
-            float v[64];
-#pragma unroll
-            for (int q = 0; q < 64; q++) v[q] = 0.f;
+            int js[G];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                if (g0 + jj < cnt) {
-                    const int j = __builtin_amdgcn_readfirstlane(s_list[g0 + jj]);
-                    const uint32_t mj = __builtin_amdgcn_readfirstlane(s_mask[j]);
-                    const uint32_t pos = (uint32_t)(p_hi - 1 - j);
-                    const float4 xy = s_rec[0][j], co = s_rec[1][j], col = s_rec[2][j];
+                js[jj] = rem ? (int)__builtin_ctzll(rem) : -1;
+                rem &= rem - 1;
+            }
+            float v[64];
+            float4 xy = s_rec[0][js[0]], co = s_rec[1][js[0]], col = s_rec[2][js[0]];
+#pragma unroll
+            for (int jj = 0; jj < G; jj++) {
+                if (js[jj] >= 0) {
+                    const int j = js[jj];
+                    float4 nxy, nco, ncol;
+                    if (jj + 1 < G) {
+                        const int nj = js[jj + 1] >= 0 ? js[jj + 1] : j;
+                        nxy = s_rec[0][nj];
+                        nco = s_rec[1][nj];
+                        ncol = s_rec[2][nj];
+                    }
+                    const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)m, j);
+                    const uint32_t pos = (uint32_t)(p0 + j);
                     const Falloff f = falloff(co);
                     v2f o[GF_NUM];
 #pragma unroll
@@ -453,15 +469,23 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                     if (mj & 12u) bwd_pair<HAS_INV>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
+                    if (jj + 1 < G) {
+                        xy = nxy;
+                        co = nco;
+                        col = ncol;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = 0.f;
                 }
             }
+#pragma unroll
+            for (int q = G * GF_NUM; q < 64; q++) v[q] = 0.f;
             const float r = wave_transpose_reduce64(v, lane);
             const int jj = lane / GF_NUM;
-            if (lane < G * GF_NUM && g0 + jj < cnt) {
-                const int j = s_list[g0 + jj];
-                const size_t gpos = (size_t)range.x + (size_t)(p_hi - 1 - j);
-                a.grad_inst[gpos * GRAD_REC + (lane - jj * GF_NUM)] = r;
-            }
+            const int jl = s_list[min(g0 + jj, 63)];
+            const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // emission slot of entry jl
+            if (lane < G * GF_NUM && g0 + jj < cnt) a.grad_inst[(size_t)dst * GRAD_REC + (lane - jj * GF_NUM)] = r;
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
     }
