@@ -416,9 +416,11 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
     r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
+    r.valid = R > 0 ? at<uint8_t>(bb, b.off[BIN_VALID]) : nullptr;
     if (R > 0) {
         {
             ProfScope ps_(PK_RENDER_BWD, s);
+            HIP_TRY(hipMemsetAsync(r.valid, 0, (size_t)R, s));
             HIP_TRY(launch_render_bwd(r, T, s));
         }
         DEBUG_SYNC(s);
@@ -438,6 +440,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.campos = campos;
     p.antialiasing = antialiasing;
     p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
+    p.valid = R > 0 ? at<uint8_t>(bb, b.off[BIN_VALID]) : nullptr;
     p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     p.has_invdepth = dL_invdepths != nullptr;

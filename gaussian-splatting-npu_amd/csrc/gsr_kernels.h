@@ -62,6 +62,7 @@ struct RenderBwdArgs {
     const float* dL_dpixels;
     const float* dL_invdepths;  // (1,H,W) or null
     const uint32_t* slot;       // emission slot of each sorted position
+    uint8_t* valid;             // valid[slot] = 1 for every record written (zeroed by the caller)
     float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
 };
 
@@ -92,6 +93,7 @@ struct PreprocessBwdArgs {
     int antialiasing;
     // per-instance gradient records and the gather map
     const float* grad_inst;         // f32x12[L], emission order
+    const uint8_t* valid;           // records not flagged were never written (no contribution)
     // (records are stored at emission slots: Gaussian i's are [emit_start[i], +tiles_touched[i]))
     const uint32_t* emit_start;     // first emission slot of Gaussian i
     const uint32_t* tiles_touched;  // number of emission slots of Gaussian i

@@ -46,6 +46,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         const uint32_t e0 = a.emit_start[idx];
         const uint32_t e1 = e0 + a.tiles_touched[idx];
         for (uint32_t e = e0; e < e1; e++) {  // this Gaussian's records are contiguous (emission order)
+            if (!a.valid[e]) continue;        // entry contributed to no pixel: record never written
             const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)e * GRAD_REC);
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
             g[0] += r0.x; g[1] += r0.y; g[2] += r0.z; g[3] += r0.w;

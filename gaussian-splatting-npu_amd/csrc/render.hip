@@ -343,7 +343,8 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 // (exact ellipse test + per-quadrant max n_contrib); the surviving entries are taken from the
 // ballot in list order, six at a time: every lane accumulates its pixels' ten gradient terms,
 // the transposed reduction sums the 64 lanes, and lanes 0..59 store the 6 records (10
-// contiguous floats each).  Entries that survive no quadrant get a zero record.  No atomics:
+// contiguous floats each) at their emission slots and flag them valid; entries that survive
+// no quadrant get no record.  No atomics:
 // per-(tile, Gaussian) sums are bitwise reproducible.
 template <bool HAS_INV>
 __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
@@ -354,7 +355,6 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int lane = threadIdx.x;
     const uint2 range = a.ranges[tile];
-    const int todo = (int)(range.y - range.x);
     const size_t HW = (size_t)a.H * a.W;
     const float px0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
     const float py0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
@@ -399,13 +399,8 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     __shared__ float4 s_rec[3][64];
     __shared__ uint8_t s_list[64];
 
-    // entries at list positions >= tmax contribute to no pixel: zero records
-    for (int pos = (int)tmax + lane; pos < todo; pos += 64) {
-        float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)a.slot[range.x + pos] * GRAD_REC);
-        z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-        z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-        z[2] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    // Entries that contribute to no pixel (list positions >= tmax, or culled for every quadrant)
+    // get no record: valid[slot] stays 0 and preprocess_bwd skips them.
 
     for (int p0 = 0; p0 < (int)tmax; p0 += 64) {
         const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
@@ -421,12 +416,6 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
             m = quad_mask(r0, r1, tx, ty);
             m &= (uint32_t)((uint32_t)pos_l < qmax[0]) | ((uint32_t)((uint32_t)pos_l < qmax[1]) << 1) |
                  ((uint32_t)((uint32_t)pos_l < qmax[2]) << 2) | ((uint32_t)((uint32_t)pos_l < qmax[3]) << 3);
-            if (m == 0) {
-                float4* z = reinterpret_cast<float4*>(a.grad_inst + (size_t)myslot * GRAD_REC);
-                z[0] = make_float4(0.f, 0.f, 0.f, 0.f);
-                z[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-                z[2] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
         }
         const uint64_t b = __ballot(m != 0);
         const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
@@ -485,7 +474,10 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
             const int jj = lane / GF_NUM;
             const int jl = s_list[min(g0 + jj, 63)];
             const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // emission slot of entry jl
-            if (lane < G * GF_NUM && g0 + jj < cnt) a.grad_inst[(size_t)dst * GRAD_REC + (lane - jj * GF_NUM)] = r;
+            if (lane < G * GF_NUM && g0 + jj < cnt) {
+                a.grad_inst[(size_t)dst * GRAD_REC + (lane - jj * GF_NUM)] = r;
+                if (lane == jj * GF_NUM) a.valid[dst] = 1;
+            }
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
     }
