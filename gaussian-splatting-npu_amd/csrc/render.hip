@@ -85,23 +85,6 @@ __device__ __forceinline__ uint32_t quad_mask(const float4 r0, const float4 co, 
     return m;
 }
 
-// Wave-level stream compaction of the batch entries whose mask bit `w` is set, in order.
-// Returns the count; indices land in list[0..count).
-__device__ __forceinline__ int compact_batch(const uint8_t* s_mask, int n, int w, int lane, uint8_t* list)
-{
-    int cnt = 0;
-#pragma unroll
-    for (int r = 0; r < BATCH / 64; r++) {
-        const int j = r * 64 + lane;
-        const bool keep = j < n && ((s_mask[j] >> w) & 1);
-        const uint64_t b = __ballot(keep);
-        const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
-        if (keep) list[cnt + before] = (uint8_t)j;
-        cnt += __popcll(b);
-    }
-    return cnt;
-}
-
 // ---- packed-f32 pixel pairs -----------------------------------------------------------------
 // gfx950 issues v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 at the cost of one scalar f32 op, so
 // the backward evaluates its pixels two at a time: each lane owns two horizontally paired
@@ -150,7 +133,6 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 
     __shared__ float4 s_rec[BATCH * 3];
     __shared__ uint8_t s_mask[BATCH];
-    __shared__ uint8_t s_list[4][BATCH];
 
     bool done = !inside;
     float T = 1.0f;
@@ -174,31 +156,41 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
         s_mask[tid] = (uint8_t)m;
         __syncthreads();
         const int n = min(BATCH, todo - base);
-        const int cnt = compact_batch(s_mask, n, wid, lane, s_list[wid]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int c = 0; c < cnt; c++) {
+        // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
+        // per 64 entries, then a scalar bit scan; each record is read one entry ahead of use.
+        for (int r = 0; r < BATCH / 64; r++) {
             if (__all(done)) break;
-            const int j = s_list[wid][c];
-            const float4 xy = s_rec[j];
-            const float4 co = s_rec[BATCH + j];
-            const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
-            const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
-            bool contrib = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const float test_T = T * (1 - alpha);
-            if (contrib && test_T < 0.0001f) {
-                done = true;
-                contrib = false;
-            }
-            if (contrib) {
-                const float4 col = s_rec[2 * BATCH + j];
-                C0 += col.x * alpha * T;
-                C1 += col.y * alpha * T;
-                C2 += col.z * alpha * T;
-                ID += col.w * alpha * T;
-                T = test_T;
-                last_contributor = (uint32_t)(base + j + 1);
+            const int jr = r * 64 + lane;
+            uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
+            if (rem == 0) continue;
+            int j = r * 64 + (int)__builtin_ctzll(rem);
+            rem &= rem - 1;
+            float4 xy = s_rec[j], co = s_rec[BATCH + j], col = s_rec[2 * BATCH + j];
+            while (true) {
+                const int jn = rem ? r * 64 + (int)__builtin_ctzll(rem) : j;
+                const float4 nxy = s_rec[jn], nco = s_rec[BATCH + jn], ncol = s_rec[2 * BATCH + jn];
+                const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
+                const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
+                bool contrib = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const float test_T = T * (1 - alpha);
+                if (contrib && test_T < 0.0001f) {
+                    done = true;
+                    contrib = false;
+                }
+                if (contrib) {
+                    C0 += col.x * alpha * T;
+                    C1 += col.y * alpha * T;
+                    C2 += col.z * alpha * T;
+                    ID += col.w * alpha * T;
+                    T = test_T;
+                    last_contributor = (uint32_t)(base + j + 1);
+                }
+                if (rem == 0 || __all(done)) break;
+                j = jn;
+                rem &= rem - 1;
+                xy = nxy;
+                co = nco;
+                col = ncol;
             }
         }
     }
