@@ -45,11 +45,12 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t*
     for (int q = 0; q < 4; q++) h[q][tid] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * RS_TILE;
+    uint32_t k[RS_ITEMS];
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) {
-        const size_t gi = base + (size_t)i * RS_THREADS + tid;
-        if (gi < (size_t)n) atomicAdd(&h[w][digit_of(keys[gi], shift, mask)], 1u);
-    }
+    for (int i = 0; i < RS_ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; i++)
+        if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
     __syncthreads();
     if ((uint32_t)tid < nb) counts[(size_t)tid * nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
@@ -133,18 +134,24 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     uint32_t key[RS_ITEMS], rank[RS_ITEMS];
     Val val[RS_ITEMS];
     const uint64_t lt = (1ull << lane) - 1ull;
+    // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
+    auto gidx = [&](int i) { return base + (size_t)min(w * (RS_ITEMS * 64) + i * 64 + lane, nvalid - 1); };
+#pragma unroll
+    for (int i = 0; i < RS_ITEMS; i++) key[i] = a.keys_in[gidx(i)];
+    if (a.vals_in) {
+#pragma unroll
+        for (int i = 0; i < RS_ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
+    } else {
+#pragma unroll
+        for (int i = 0; i < RS_ITEMS; i++) {
+            if constexpr (PAIR) val[i] = make_uint2((uint32_t)gidx(i), a.gids[gidx(i)]);
+            else val[i] = (uint32_t)gidx(i);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < RS_ITEMS; i++) {
-        const int li = w * (RS_ITEMS * 64) + i * 64 + lane;  // chunk-local index; order = (wave, item, lane)
+        const int li = w * (RS_ITEMS * 64) + i * 64 + lane;
         const bool valid = li < nvalid;
-        const size_t gi = base + li;
-        key[i] = valid ? a.keys_in[gi] : 0u;
-        if constexpr (PAIR) {
-            if (a.vals_in) val[i] = valid ? reinterpret_cast<const uint2*>(a.vals_in)[gi] : make_uint2(0u, 0u);
-            else val[i] = make_uint2((uint32_t)gi, valid ? a.gids[gi] : 0u);
-        } else {
-            val[i] = valid ? (a.vals_in ? a.vals_in[gi] : (uint32_t)gi) : 0u;
-        }
         const uint32_t d = digit_of(key[i], a.shift, mask);
         uint64_t peers = __ballot(valid);
         for (int b = 0; b < a.nbits; b++) {
