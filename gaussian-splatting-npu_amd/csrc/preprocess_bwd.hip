@@ -43,15 +43,33 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
     {
+        // This Gaussian's records are contiguous (emission order); entries that contributed to
+        // no pixel were never written (valid = 0) and are skipped.  Four slots per step so that
+        // their loads are in flight together; the sum order stays the slot order.
         const uint32_t e0 = a.emit_start[idx];
         const uint32_t e1 = e0 + a.tiles_touched[idx];
-        for (uint32_t e = e0; e < e1; e++) {  // this Gaussian's records are contiguous (emission order)
-            if (!a.valid[e]) continue;        // entry contributed to no pixel: record never written
-            const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)e * GRAD_REC);
-            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-            g[0] += r0.x; g[1] += r0.y; g[2] += r0.z; g[3] += r0.w;
-            g[4] += r1.x; g[5] += r1.y; g[6] += r1.z; g[7] += r1.w;
-            g[8] += r2.x; g[9] += r2.y;
+        for (uint32_t e = e0; e < e1; e += 4) {
+            bool v[4];
+            float4 r[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = e + k < e1 && a.valid[e + k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (v[k]) {
+                    const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)(e + k) * GRAD_REC);
+                    r[k][0] = rec[0];
+                    r[k][1] = rec[1];
+                    r[k][2] = rec[2];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                if (v[k]) {
+                    g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
+                    g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
+                    g[8] += r[k][2].x; g[9] += r[k][2].y;
+                }
+            }
         }
     }
     {
@@ -341,8 +359,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 
 // SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's
 // traffic.  STAGED: the workgroup's 256 x 3M floats are read with coalesced 16-byte loads
-// into LDS (row stride padded to an odd number of 16-byte slots: conflict-free b128 rows),
-// each thread works on its row in place, and the SH gradients leave the same way -- instead
+// into LDS (row stride padded to an odd number of dwords, so the 64 lanes walking their own
+// rows hit 64 different banks), each thread works on its row in place, and the SH gradients leave the same way -- instead
 // of every lane striding 192 B through global memory.
 template <bool STAGED>
 __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a, int lds_stride)
@@ -363,7 +381,9 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
     for (int f = threadIdx.x; f < nv4; f += 256) {
         const int g = (f * 4) / W3, w = (f * 4) - g * W3;
-        *reinterpret_cast<float4*>(&s_sh[g * lds_stride + w]) = src[f];
+        const float4 v = src[f];
+        float* d = &s_sh[g * lds_stride + w];
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
     __syncthreads();
     if (idx < a.P) {
@@ -374,7 +394,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * W3);
     for (int f = threadIdx.x; f < nv4; f += 256) {
         const int g = (f * 4) / W3, w = (f * 4) - g * W3;
-        dst[f] = *reinterpret_cast<const float4*>(&s_sh[g * lds_stride + w]);
+        const float* q = &s_sh[g * lds_stride + w];
+        dst[f] = make_float4(q[0], q[1], q[2], q[3]);
     }
 }
 
@@ -385,7 +406,7 @@ hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
     const bool staged = a.shs && a.dL_dsh && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
                         ((uintptr_t)a.shs % 16) == 0 && ((uintptr_t)a.dL_dsh % 16) == 0;
     if (staged) {
-        const int stride = ((W3 / 4) % 2) ? W3 : W3 + 4;  // odd number of 16-B slots per row
+        const int stride = W3 | 1;  // odd number of dwords per row: the per-thread row walks are conflict-free
         hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
                            256 * stride * sizeof(float), s, a, stride);
     } else {
