@@ -254,7 +254,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
     {
         ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]),
+        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]), flags + 2,
                                       s));
     }
     DEBUG_SYNC(s);
@@ -263,13 +263,13 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* h;
     int rc = pinned(&h);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(h, offsets + (P - 1), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h + 1, flags, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    // flags[0]: prefiltered violation, flags[2]: total of the tile-count scan (= num_rendered)
+    HIP_TRY(hipMemcpyAsync(h, flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    if (h[1] & 1u)
+    if (h[0] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (h[0] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
-    *num_rendered = (int)h[0];
+    if (h[2] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
+    *num_rendered = (int)h[2];
     return GSR_OK;
 }
 

@@ -117,7 +117,7 @@ hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 // inclusive scan of in[gather[i]] (gather may be null)
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
-                                 hipStream_t s);
+                                 uint32_t* total_out, hipStream_t s);
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,

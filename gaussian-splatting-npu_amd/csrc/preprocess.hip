@@ -260,7 +260,7 @@ __global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, co
 }
 
 // single block: exclusive scan of block sums in place (nb can exceed 256; loop)
-__global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sums, int nb)
+__global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sums, int nb, uint32_t* total_out)
 {
     __shared__ uint32_t lds4[4];
     uint32_t carry = 0;
@@ -272,6 +272,7 @@ __global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sum
         if (i < nb) block_sums[i] = carry + ex;
         carry += total;
     }
+    if (total_out && threadIdx.x == 0) *total_out = carry;
 }
 
 __global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, const uint32_t* gather, int n,
@@ -314,12 +315,12 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 }
 
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
-                                 hipStream_t s)
+                                 uint32_t* total_out, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
     hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch);
-    hipLaunchKernelGGL(scan_blocksums_kernel, dim3(1), dim3(256), 0, s, scratch, nb);
+    hipLaunchKernelGGL(scan_blocksums_kernel, dim3(1), dim3(256), 0, s, scratch, nb, total_out);
     hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch, out);
     return hipGetLastError();
 }

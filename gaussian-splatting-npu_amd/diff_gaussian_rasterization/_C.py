@@ -53,6 +53,27 @@ def _check(rc):
         raise RuntimeError(f"diff_gaussian_rasterization (HIP): {lib.gsr_last_error().decode()} [status {rc}]")
 
 
+_contig_cache = {}  # small non-contiguous inputs (the transposed view matrices) -> contiguous copy
+
+
+def _contiguous(t):
+    """t.contiguous(), memoised for small tensors: the reference's camera matrices are
+    transposed views (scene/cameras.py:86-88) that every call would otherwise copy with a
+    separate kernel launch.  Keyed on storage, layout and the in-place version counter."""
+    if t.is_contiguous():
+        return t
+    if t.numel() > 64:
+        return t.contiguous()
+    key = (t.data_ptr(), t.shape, t.stride(), t._version, t.device)
+    hit = _contig_cache.get(key)
+    if hit is None:
+        if len(_contig_cache) > 256:
+            _contig_cache.clear()
+        # the entry keeps `t` alive, so its storage cannot be recycled under the same key
+        hit = _contig_cache[key] = (t, t.contiguous())
+    return hit[1]
+
+
 def _ptr(t, name, device):
     """Device pointer of a float32 tensor, or None for an absent (empty) input -- the
     reference passes `.data<float>()` of `torch.Tensor([])`, i.e. nullptr."""
@@ -62,7 +83,7 @@ def _ptr(t, name, device):
         raise RuntimeError(f"{name} must be on {device}, got {t.device}")
     if t.dtype != torch.float32:
         raise RuntimeError(f"{name} must be float32, got {t.dtype}")
-    t = t.contiguous()
+    t = _contiguous(t)
     return t.data_ptr(), t
 
 
@@ -85,13 +106,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     _require_gpu(means3D)
     dev = means3D.device
     P, H, W = means3D.size(0), int(image_height), int(image_width)
-    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
-    out_invdepth = torch.zeros((1, H, W), dtype=torch.float32, device=dev)
     empty = lambda: torch.empty((0,), dtype=torch.uint8, device=dev)  # noqa: E731
     if P == 0:
+        radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+        out_invdepth = torch.zeros((1, H, W), dtype=torch.float32, device=dev)
         out_color = torch.zeros((3, H, W), dtype=torch.float32, device=dev)
         return 0, out_color, radii, empty(), empty(), empty(), out_invdepth
 
+    # every element of these is written by the HIP forward (radii by preprocess, pixels by render)
+    radii = torch.empty((P,), dtype=torch.int32, device=dev)
+    out_invdepth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
     M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
     keep = []
