@@ -66,9 +66,11 @@ struct RenderBwdArgs {
     float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
 };
 
-// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  The mean2D and conic
-// fields are pixel sums WITHOUT the per-Gaussian factors -opacity*W/2, -opacity*H/2 and
-// -opacity/2 (backward.cu:619-636); preprocess_bwd applies them once per Gaussian.
+// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  With u = G dL/dalpha
+// per pixel, the mean2D fields hold Sx = sum u dx, Sy = sum u dy and the conic fields
+// sum u dx^2, u dx dy, u dy^2 -- WITHOUT the per-Gaussian factors (backward.cu:619-636):
+// preprocess_bwd forms dL/dmean2D = (a Sx + b Sy, b Sx + c Sy) * (-opacity W/2, -opacity H/2)
+// from the conic (a, b, c) and scales the conic sums by -opacity/2, once per Gaussian.
 enum GradField {
     GF_MEAN2D_X = 0, GF_MEAN2D_Y, GF_CONIC_A, GF_CONIC_B, GF_CONIC_C, GF_OPACITY, GF_COLOR_R, GF_COLOR_G,
     GF_COLOR_B, GF_INVDEPTH, GF_NUM

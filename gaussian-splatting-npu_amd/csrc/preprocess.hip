@@ -104,16 +104,25 @@ __device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const fl
     return {res[0], res[1], res[2]};
 }
 
-__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
+// One Gaussian; `sh` points at its SH coefficients (global memory or its LDS staging row).
+__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const float* sh)
 {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
 
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
     a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
 
+    // Issue every per-Gaussian load up front (one memory round trip instead of one per phase).
     const f3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
+    float scl[3] = {0.f, 0.f, 0.f};
+    if (!a.cov3D_precomp) {
+        const float* rp = a.rotations + 4 * (size_t)idx;
+        rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        const float* sp = a.scales + 3 * (size_t)idx;
+        scl[0] = sp[0]; scl[1] = sp[1]; scl[2] = sp[2];
+    }
+    const float opacity_in = a.opacities[idx];
     // in_frustum (auxiliary.h:151-176)
     const f3 p_view = transformPoint4x3(p_orig, a.view);
     if (p_view.z <= 0.2f) {
@@ -129,9 +138,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
     if (a.cov3D_precomp) {
         cov3D = a.cov3D_precomp + (size_t)idx * 6;
     } else {
-        const float* rp = a.rotations + 4 * (size_t)idx;
-        const float4 rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
-        computeCov3D(a.scales + 3 * (size_t)idx, a.scale_modifier, rot, cov3D_local);
+        computeCov3D(scl, a.scale_modifier, rot, cov3D_local);
 #pragma unroll
         for (int i = 0; i < 6; i++) a.cov3D_out[(size_t)idx * 6 + i] = cov3D_local[i];
         cov3D = cov3D_local;
@@ -163,7 +170,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
     f3 rgb;
     if (!a.colors_precomp) {
         uint8_t cl;
-        rgb = computeColorFromSH(p_orig, a.D, a.shs + (size_t)idx * a.M * 3, a.campos, cl);
+        rgb = computeColorFromSH(p_orig, a.D, sh, a.campos, cl);
         a.rgb[3 * (size_t)idx + 0] = rgb.x;
         a.rgb[3 * (size_t)idx + 1] = rgb.y;
         a.rgb[3 * (size_t)idx + 2] = rgb.z;
@@ -176,7 +183,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
     a.dkey[idx] = __float_as_uint(p_view.z);  // z > 0.2: float bits are monotone in z
     a.radii[idx] = (int)my_radius;
     reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
-    const float opacity = a.opacities[idx] * h_convolution_scaling;
+    const float opacity = opacity_in * h_convolution_scaling;
     reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
 
@@ -193,6 +200,33 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a)
     sp[0] = make_float4(pix_x, pix_y, cullK, 0.0f);
     sp[1] = make_float4(conic_x, conic_y, conic_z, opacity);
     sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
+}
+
+// SH coefficients are 192 of the 236 bytes read per Gaussian at degree 3.  STAGED: the block's
+// 256 x 3M floats arrive through LDS with coalesced 16-byte loads (rows padded to an odd number
+// of dwords, so the per-thread row walks are bank-conflict-free) instead of every lane striding
+// 3M floats through global memory.
+template <bool STAGED>
+__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, int lds_stride)
+{
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const int base = blockIdx.x * 256;
+    const int idx = base + (int)threadIdx.x;
+    if (!STAGED) {
+        if (idx < a.P) preprocess_one(a, idx, a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr);
+        return;
+    }
+    const int W3 = a.M * 3;  // multiple of 4 on this path
+    const int nv4 = min(256, a.P - base) * (W3 / 4);
+    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
+    for (int f = threadIdx.x; f < nv4; f += 256) {
+        const int g = (f * 4) / W3, w = (f * 4) - g * W3;
+        const float4 v = src[f];
+        float* d = &s_sh[g * lds_stride + w];
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    __syncthreads();
+    if (idx < a.P) preprocess_one(a, idx, s_sh + threadIdx.x * lds_stride);
 }
 
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,
@@ -303,7 +337,16 @@ __global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, con
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
 {
     if (a.P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(preprocess_fwd_kernel, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    const int W3 = a.M * 3;
+    const bool staged = a.shs && !a.colors_precomp && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
+                        ((uintptr_t)a.shs % 16) == 0;
+    if (staged) {
+        const int stride = W3 | 1;
+        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
+                           256 * stride * sizeof(float), s, a, stride);
+    } else {
+        hipLaunchKernelGGL(preprocess_fwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, 0);
+    }
     return hipGetLastError();
 }
 

@@ -74,9 +74,11 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     }
     {
         // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
-        const float op = a.conic_opacity[idx].w;
-        g[GF_MEAN2D_X] *= -op * (0.5f * a.W);
-        g[GF_MEAN2D_Y] *= -op * (0.5f * a.H);
+        const float4 co = a.conic_opacity[idx];
+        const float op = co.w;
+        const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
+        g[GF_MEAN2D_X] = (co.x * sx + co.y * sy) * (-op * (0.5f * a.W));
+        g[GF_MEAN2D_Y] = (co.y * sx + co.z * sy) * (-op * (0.5f * a.H));
         g[GF_CONIC_A] *= -0.5f * op;
         g[GF_CONIC_B] *= -0.5f * op;
         g[GF_CONIC_C] *= -0.5f * op;

@@ -225,28 +225,57 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 
 // Emission in depth order: instance slots [off(k-1), off(k)) of depth rank k belong to
 // Gaussian g = sorted_ids[k]; tiles y-major then x inside its rect (rasterizer_impl.cu:98-109).
+// One wave per 64 consecutive ranks: the lanes first publish their rects in LDS, then the wave
+// fills its whole slot range 64 consecutive slots at a time (coalesced stores), each lane
+// finding the owner of its slot by a binary search over the 64 rect starts.
 __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
                                                              const uint32_t* offsets_d, const float2* means2D,
                                                              const int* radii, uint32_t gx, uint32_t gy,
                                                              uint32_t* tile_keys, uint32_t* gids,
                                                              uint32_t* emit_start)
 {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= P) return;
-    const uint32_t g = sorted_ids[k];
-    const int r = radii[g];
-    uint32_t off = k == 0 ? 0u : offsets_d[k - 1];
-    emit_start[g] = off;
-    if (r <= 0) return;
-    const float2 xy = means2D[g];
-    uint32_t rminx, rminy, rmaxx, rmaxy;
-    getRect(xy.x, xy.y, r, gx, gy, rminx, rminy, rmaxx, rmaxy);
-    for (uint32_t y = rminy; y < rmaxy; y++)
-        for (uint32_t x = rminx; x < rmaxx; x++) {
-            tile_keys[off] = y * gx + x;
-            gids[off] = g;
-            off++;
+    __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int k0 = (blockIdx.x * 4 + w) * 64;
+    if (k0 >= P) return;  // whole wave out of range (waves are independent: no block barriers)
+    const int k = k0 + lane;
+    uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1, g = 0;
+    if (k < P) {
+        g = sorted_ids[k];
+        start = k == 0 ? 0u : offsets_d[k - 1];
+        emit_start[g] = start;
+        const int r = radii[g];
+        if (r > 0) {
+            const float2 xy = means2D[g];
+            uint32_t rminx, rminy, rmaxx, rmaxy;
+            getRect(xy.x, xy.y, r, gx, gy, rminx, rminy, rmaxx, rmaxy);
+            x0 = rminx;
+            y0 = rminy;
+            wd = max(rmaxx - rminx, 1u);
         }
+    }
+    s_start[w][lane] = start;
+    s_x0[w][lane] = x0;
+    s_y0[w][lane] = y0;
+    s_w[w][lane] = wd;
+    s_g[w][lane] = g;
+    const uint32_t wbeg = (uint32_t)__shfl((int)start, 0, 64);
+    const uint32_t wend = offsets_d[min(k0 + 63, P - 1)];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t sl = wbeg + lane; sl < wend; sl += 64) {
+        // largest j with start_j <= sl (ranks without instances share their successor's start)
+        int j = 0;
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (s_start[w][j + step] <= sl) j += step;
+        const uint32_t local = sl - s_start[w][j];
+        const uint32_t wj = s_w[w][j];
+        const uint32_t yy = local / wj, xx = local - yy * wj;
+        tile_keys[sl] = (s_y0[w][j] + yy) * gx + (s_x0[w][j] + xx);
+        gids[sl] = s_g[w][j];
+    }
 }
 
 __global__ void __launch_bounds__(256) tile_ranges_kernel(int L, const uint32_t* sorted_tiles, uint2* ranges)

@@ -288,8 +288,8 @@ struct BwdPair {
 // Two pixels x one Gaussian, branch-free: a pixel the Gaussian does not contribute to gets
 // alpha = G = 0, which leaves its state bitwise unchanged (T * (1 - 0) = T, Fd + 0 * cd = Fd)
 // and adds exact zeros.  Per-Gaussian constant factors are left to preprocess_bwd (see
-// GradField): with u = G * dL/dalpha the record holds sum u (opacity), sum u*(dx*a + dy*b) and
-// sum u*(dy*c + dx*b) (mean2D, times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy,
+// GradField): with u = G * dL/dalpha the record holds sum u (opacity), sum u*dx and sum u*dy
+// (mean2D: (a Sx + b Sy, b Sx + c Sy) times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy,
 // u*dy*dy (conic, times -opacity/2).
 template <bool HAS_INV>
 __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_t pos, const float4 xy,
@@ -321,8 +321,8 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
     const v2f u = Gc * dL;
     const v2f ux = u * dx, uy = u * dy;
     o[GF_OPACITY] += u;
-    o[GF_MEAN2D_X] = fma2(ux, (v2f)(co.x), fma2(uy, (v2f)(co.y), o[GF_MEAN2D_X]));
-    o[GF_MEAN2D_Y] = fma2(uy, (v2f)(co.z), fma2(ux, (v2f)(co.y), o[GF_MEAN2D_Y]));
+    o[GF_MEAN2D_X] += ux;  // sum u dx, sum u dy: the conic (a, b, c) is applied per Gaussian
+    o[GF_MEAN2D_Y] += uy;
     o[GF_CONIC_A] = fma2(ux, dx, o[GF_CONIC_A]);
     o[GF_CONIC_B] = fma2(ux, (v2f)(dy), o[GF_CONIC_B]);
     o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
