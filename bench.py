@@ -56,6 +56,7 @@ def algorithmic_bytes(P, M, L, N, T, P_vis):
         "emit_instances": P * 24 + L * 8,                      # per-Gaussian rect inputs; (tile, id) per instance
         "tile_sort": L * 20,                                   # (tile, id) in; id + tile + inverse slot out
         "tile_ranges": L * 4 + T * 8,
+        "tile_order": T * 12,                                  # per-tile work in, launch order out
         "render_fwd": L * 44 + N * 24 + T * 8,                 # id + 40 B record per instance; 24 B/pixel out
         "render_bwd": L * 44 + N * 24 + T * 8,                 # id + record per instance; 24 B/pixel in
         "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in

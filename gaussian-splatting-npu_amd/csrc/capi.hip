@@ -65,11 +65,11 @@ int pinned(uint32_t** out)
 // ---------------------------------------------------------------------------
 enum ProfKernel {
     PK_PREPROCESS = 0, PK_DEPTH_SORT, PK_SCAN, PK_EMIT, PK_TILE_SORT, PK_RANGES, PK_RENDER_FWD, PK_RENDER_BWD,
-    PK_PREPROCESS_BWD,
+    PK_PREPROCESS_BWD, PK_TILE_ORDER,
     PK_COUNT
 };
 const char* kProfNames[PK_COUNT] = {"preprocess_fwd", "depth_sort", "scan", "emit_instances", "tile_sort",
-                                    "tile_ranges", "render_fwd", "render_bwd", "preprocess_bwd"};
+                                    "tile_ranges", "render_fwd", "render_bwd", "preprocess_bwd", "tile_order"};
 struct Prof {
     bool on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool[PK_COUNT];
@@ -330,8 +330,15 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     }
     DEBUG_SYNC(s);
 
+    uint32_t* tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    {
+        ProfScope ps_(PK_TILE_ORDER, s);
+        HIP_TRY(launch_tile_order(ranges, nullptr, T, tile_order, s));
+    }
     RenderFwdArgs r;
     r.ranges = ranges;
+    r.tile_order = tile_order;
+    r.tile_work = at<uint32_t>(ib, im.off[IMG_TILE_WORK]);
     r.point_list = point_list;
     r.W = width; r.H = height; r.grid_x = gx;
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
@@ -405,6 +412,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     // BACKWARD::render (rasterizer_impl.cu:399-418): per-(tile, Gaussian) gradient records
     RenderBwdArgs r;
     r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
     r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     r.W = width; r.H = height; r.grid_x = gx;
     r.bg = background;
@@ -418,6 +426,11 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     r.valid = R > 0 ? at<uint8_t>(bb, b.off[BIN_VALID]) : nullptr;
     if (R > 0) {
+        {
+            ProfScope ps_(PK_TILE_ORDER, s);
+            HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,
+                                      at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
+        }
         {
             ProfScope ps_(PK_RENDER_BWD, s);
             HIP_TRY(hipMemsetAsync(r.valid, 0, (size_t)R, s));

@@ -37,6 +37,8 @@ struct PreprocessArgs {
 
 struct RenderFwdArgs {
     const uint2* ranges;
+    const uint32_t* tile_order;  // IMG_TILE_ORDER: block b renders tile tile_order[b]
+    uint32_t* tile_work;         // IMG_TILE_WORK: largest n_contrib of the tile (out)
     const uint32_t* point_list;
     int W, H;
     uint32_t grid_x;
@@ -51,6 +53,7 @@ struct RenderFwdArgs {
 
 struct RenderBwdArgs {
     const uint2* ranges;
+    const uint32_t* tile_order;  // IMG_TILE_ORDER (re-ordered from IMG_TILE_WORK for the backward)
     const uint32_t* point_list;
     int W, H;
     uint32_t grid_x;
@@ -131,6 +134,9 @@ hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
                              uint64_t* keys, hipStream_t s);
 
+// Longest-first launch order of the T tiles: order[] = tiles by decreasing work, work = range length
+// (ranges != null, the forward) or work[] (the backward's per-tile largest n_contrib).
+hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s);
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);

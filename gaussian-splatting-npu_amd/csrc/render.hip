@@ -117,10 +117,95 @@ __device__ __forceinline__ v2f falloff_p2(const Falloff f, v2f dx, float dy)
     return fma2(fma2((v2f)(f.ka), dx, (v2f)(bq)), dx, (v2f)(cq));
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
+// ---- longest-first tile order ---------------------------------------------------------------
+// One 1024-thread workgroup buckets the T tiles by work into NB classes, heaviest first, and
+// writes the launch order.  Workgroups start roughly in blockIdx order, so the long tiles are
+// dispatched first and the tail of the launch is made of short ones (list scheduling, LPT).
+// The order inside a class is whatever the LDS atomics give: tiles are independent, so the
+// launch order changes timing only, never a result.
+constexpr int ORDER_BUCKETS = 1024;
+
+constexpr int ORDER_CACHE = 16384;  // tiles whose work stays in LDS (4K UHD: 32,400 tiles reload)
+
+__global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, const uint32_t* work, int T,
+                                                          uint32_t* order)
+{
+    __shared__ uint32_t s_cnt[ORDER_BUCKETS];
+    __shared__ uint32_t s_work[ORDER_CACHE];
+    __shared__ uint32_t s_wsum[16];
+    __shared__ uint32_t s_max, s_zero;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    auto load_work = [&](int t) -> uint32_t { return ranges ? ranges[t].y - ranges[t].x : work[t]; };
+    auto work_of = [&](int t) -> uint32_t { return t < ORDER_CACHE ? s_work[t] : load_work(t); };
+    s_cnt[tid] = 0;
+    if (tid == 0) { s_max = 0; s_zero = 0; }
+    uint32_t mx = 0;
+    for (int t = tid; t < T; t += 1024) {
+        const uint32_t w = load_work(t);
+        if (t < ORDER_CACHE) s_work[t] = w;
+        mx = max(mx, w);
+    }
+    mx = wave_max_u32(mx);
+    __syncthreads();
+    if (lane == 0) atomicMax(&s_max, mx);
+    __syncthreads();
+    const uint64_t wmax = max(s_max, 1u);
+    // tiles with no work go last, in index order (wave-aggregated: one LDS atomic per wave and
+    // round instead of one per tile on a single hot counter); the rest into NB work classes
+    auto bucket = [&](uint32_t w) -> uint32_t {
+        return (uint32_t)(ORDER_BUCKETS - 1) - (uint32_t)(((uint64_t)w * (ORDER_BUCKETS - 1)) / wmax);
+    };
+    for (int t = tid; t < T; t += 1024) {
+        const uint32_t w = work_of(t);
+        if (w > 0) atomicAdd(&s_cnt[bucket(w)], 1u);
+    }
+    // exclusive scan of the class counts
+    __syncthreads();
+    const uint32_t c = s_cnt[tid];
+    uint32_t inc = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+        if (lane >= d) inc += y;
+    }
+    if (lane == 63) s_wsum[wid] = inc;
+    __syncthreads();
+    uint32_t before = 0, nonzero = 0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) {
+        before += w < wid ? s_wsum[w] : 0u;
+        nonzero += s_wsum[w];
+    }
+    s_cnt[tid] = before + inc - c;
+    __syncthreads();
+    for (int t0 = 0; t0 < T; t0 += 1024) {
+        const int t = t0 + tid;
+        const uint32_t w = t < T ? work_of(t) : 1u;
+        const uint64_t zb = __ballot(w == 0);
+        uint32_t zbase = 0;
+        if (zb) {
+            if (lane == 0) zbase = atomicAdd(&s_zero, (uint32_t)__popcll(zb));
+            zbase = (uint32_t)__shfl((int)zbase, 0, 64);
+        }
+        if (t < T) {
+            if (w > 0) order[atomicAdd(&s_cnt[bucket(w)], 1u)] = (uint32_t)t;
+            else order[nonzero + zbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(zb >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)zb, 0))] = (uint32_t)t;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 {
 #pragma clang fp contract(fast)
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = a.tile_order[blockIdx.x];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int tid = threadIdx.x;
     const int lane = tid & 63, wid = tid >> 6;
@@ -195,6 +280,12 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
         }
     }
 
+    __shared__ uint32_t s_lc[4];
+    const uint32_t wl = wave_max_u32(last_contributor);
+    if (lane == 0) s_lc[wid] = wl;
+    __syncthreads();
+    if (tid == 0) a.tile_work[tile] = max(max(s_lc[0], s_lc[1]), max(s_lc[2], s_lc[3]));
+
     if (inside) {
         const uint32_t pix_id = (uint32_t)a.W * py + px;
         const size_t HW = (size_t)a.H * a.W;
@@ -206,13 +297,6 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
         if (a.invdepth) a.invdepth[pix_id] = ID;
         a.accum[pix_id] = make_float4(C0, C1, C2, ID);
     }
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
-{
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
-    return v;
 }
 
 // ---- transposed wave reduction (CDNA4 cross-lane ops, no LDS) ------------------------------
@@ -235,38 +319,33 @@ __device__ __forceinline__ float dpp(float x)
 }
 constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_QUAD_2301 = 0x4E, DPP_QUAD_1032 = 0xB1;
 
-// Sums 64 per-lane values over the 64 lanes of the wave and returns, in lane l, the wave
-// total of v[l].  Recursive halving: each exchange step hands half of the live values to the
-// partner lane (v_permlane32_swap, v_permlane16_swap, then DPP row_mirror / row_half_mirror /
-// quad_perm fused into v_add_f32_dpp), so 64 totals cost ~141 VALU ops instead of the
-// 64 x 6 shuffle+add pairs of per-value butterflies.
-__device__ __forceinline__ float wave_transpose_reduce64(float (&v)[64], int lane)
+// Sums 32 per-lane values over the 64 lanes of the wave and returns, in lanes 2k and 2k + 1, the
+// wave total of v[k].  Recursive halving: each exchange step hands half of the live values to
+// the partner lane (v_permlane32_swap, v_permlane16_swap, then DPP row_mirror / row_half_mirror /
+// quad_perm fused into v_add_f32_dpp), and a last quad_perm butterfly adds the two lanes that
+// still hold halves of one total: 32 exchanges for 32 totals instead of the 32 x 6 shuffle+add
+// pairs of per-value butterflies, in half the registers of a 64-value transpose.
+__device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lane)
 {
 #pragma unroll
-    for (int i = 0; i < 32; i++) { xswap32(v[i], v[i + 32]); v[i] = v[i] + v[i + 32]; }
+    for (int i = 0; i < 16; i++) { xswap32(v[i], v[i + 16]); v[i] = v[i] + v[i + 16]; }
 #pragma unroll
-    for (int i = 0; i < 16; i++) { xswap16(v[i], v[i + 16]); v[i] = v[i] + v[i + 16]; }
-    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+    for (int i = 0; i < 8; i++) { xswap16(v[i], v[i + 8]); v[i] = v[i] + v[i + 8]; }
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const float keep = b3 ? v[i + 8] : v[i], send = b3 ? v[i] : v[i + 8];
+    for (int i = 0; i < 4; i++) {
+        const float keep = b3 ? v[i + 4] : v[i], send = b3 ? v[i] : v[i + 4];
         v[i] = keep + dpp<DPP_ROW_MIRROR>(send);
     }
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float keep = b2 ? v[i + 4] : v[i], send = b2 ? v[i] : v[i + 4];
+    for (int i = 0; i < 2; i++) {
+        const float keep = b2 ? v[i + 2] : v[i], send = b2 ? v[i] : v[i + 2];
         v[i] = keep + dpp<DPP_ROW_HALF_MIRROR>(send);
     }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const float keep = b1 ? v[i + 2] : v[i], send = b1 ? v[i] : v[i + 2];
-        v[i] = keep + dpp<DPP_QUAD_2301>(send);
-    }
-    const float keep = b0 ? v[1] : v[0], send = b0 ? v[0] : v[1];
-    return keep + dpp<DPP_QUAD_1032>(send);
+    const float keep = b1 ? v[1] : v[0], send = b1 ? v[0] : v[1];
+    const float h = keep + dpp<DPP_QUAD_2301>(send);
+    return h + dpp<DPP_QUAD_1032>(h);
 }
-
-
 
 // State of two pixels of the backward pass (backward.cu:498-528, restated front to back).
 // Pixels outside the image carry last_contributor = 0, so no list entry contributes to them.
@@ -333,8 +412,8 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 // cross-wave combine.  The list is walked front to back in batches of 64 entries up to the
 // tile's largest n_contrib; each lane stages one record in LDS and computes its quadrant mask
 // (exact ellipse test + per-quadrant max n_contrib); the surviving entries are taken from the
-// ballot in list order, six at a time: every lane accumulates its pixels' ten gradient terms,
-// the transposed reduction sums the 64 lanes, and lanes 0..59 store the 6 records (10
+// ballot in list order, three at a time: every lane accumulates its pixels' ten gradient terms,
+// the transposed reduction sums the 64 lanes, and the even lanes 0..58 store the 3 records (10
 // contiguous floats each) at their emission slots and flag them valid; entries that survive
 // no quadrant get no record.  No atomics:
 // per-(tile, Gaussian) sums are bitwise reproducible.
@@ -342,8 +421,8 @@ template <bool HAS_INV>
 __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 {
 #pragma clang fp contract(fast)
-    constexpr int G = 6;  // Gaussians per transposed reduction (6 x 10 gradient terms <= 64 lanes)
-    const uint32_t tile = blockIdx.x;
+    constexpr int G = 3;  // Gaussians per transposed reduction (3 x 10 gradient terms <= 32 values)
+    const uint32_t tile = a.tile_order[blockIdx.x];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int lane = threadIdx.x;
     const uint2 range = a.ranges[tile];
@@ -427,7 +506,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                 js[jj] = rem ? (int)__builtin_ctzll(rem) : -1;
                 rem &= rem - 1;
             }
-            float v[64];
+            float v[32];
             float4 xy = s_rec[0][js[0]], co = s_rec[1][js[0]], col = s_rec[2][js[0]];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
@@ -461,18 +540,26 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                 }
             }
 #pragma unroll
-            for (int q = G * GF_NUM; q < 64; q++) v[q] = 0.f;
-            const float r = wave_transpose_reduce64(v, lane);
-            const int jj = lane / GF_NUM;
+            for (int q = G * GF_NUM; q < 32; q++) v[q] = 0.f;
+            const float r = wave_transpose_reduce32(v, lane);
+            const int k = lane >> 1;  // value held by this lane (lanes 2k, 2k + 1)
+            const int jj = k / GF_NUM;
             const int jl = s_list[min(g0 + jj, 63)];
             const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // emission slot of entry jl
-            if (lane < G * GF_NUM && g0 + jj < cnt) {
-                a.grad_inst[(size_t)dst * GRAD_REC + (lane - jj * GF_NUM)] = r;
-                if (lane == jj * GF_NUM) a.valid[dst] = 1;
+            if ((lane & 1) == 0 && k < G * GF_NUM && g0 + jj < cnt) {
+                a.grad_inst[(size_t)dst * GRAD_REC + (k - jj * GF_NUM)] = r;
+                if (k == jj * GF_NUM) a.valid[dst] = 1;
             }
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
     }
+}
+
+hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s)
+{
+    if (T <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
+    return hipGetLastError();
 }
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
