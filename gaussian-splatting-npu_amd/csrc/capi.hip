@@ -48,10 +48,13 @@ int fail_hip(hipError_t e, int line)
         }                                                                                     \
     } while (0)
 
+// Pinned, device-mapped host words of this host thread.  The forward's kernels store the
+// prefiltered-violation flag and num_rendered straight into them (system-scope stores), so the
+// forward needs neither a device memset nor a D2H copy before its one stream synchronisation.
 int pinned(uint32_t** out)
 {
     if (!g_pinned) {
-        hipError_t e = hipHostMalloc((void**)&g_pinned, 64, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc((void**)&g_pinned, 64, hipHostMallocMapped | hipHostMallocCoherent);
         if (e != hipSuccess) return fail_hip(e, __LINE__);
     }
     *out = g_pinned;
@@ -203,8 +206,15 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
 
     const GeomLayout g = geom_layout(P);
     char* gb = geometry_buffer;
-    uint32_t* flags = at<uint32_t>(gb, g.off[GEOM_FLAGS]);
-    HIP_TRY(hipMemsetAsync(flags, 0, 256, s));
+    // h[0]: prefiltered violation (written by preprocess), h[2]: num_rendered (written by the scan).
+    // This thread's previous forward has synchronised its stream, so no kernel still writes them.
+    uint32_t* h;
+    int rc = pinned(&h);
+    if (rc) return rc;
+    h[0] = 0;
+    h[2] = 0;
+    uint32_t* h_dev = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&h_dev, h, 0));
 
     // 1. preprocess (forward.cu:154-272)
     PreprocessArgs a;
@@ -226,7 +236,9 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     a.conic_opacity = at<float>(gb, g.off[GEOM_CONIC_OPACITY]);
     a.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
     a.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
-    a.flags = flags;
+    a.host_flags = h_dev;
+    a.scan_status = at<uint64_t>(gb, g.off[GEOM_SCAN_SCRATCH]);
+    a.scan_status_words = scan_status_words(P);
     a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     a.dkey = at<uint32_t>(gb, g.off[GEOM_DKEY]);
     {
@@ -254,17 +266,12 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
     {
         ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, at<uint32_t>(gb, g.off[GEOM_SCAN_SCRATCH]), flags + 2,
-                                      s));
+        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, a.scan_status, h_dev + 2, s));
     }
     DEBUG_SYNC(s);
 
-    // 4. the one D2H of the forward: num_rendered (rasterizer_impl.cu:283-284), plus error flags
-    uint32_t* h;
-    int rc = pinned(&h);
-    if (rc) return rc;
-    // flags[0]: prefiltered violation, flags[2]: total of the tile-count scan (= num_rendered)
-    HIP_TRY(hipMemcpyAsync(h, flags, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    // 4. the one device->host hand-off of the forward: num_rendered (rasterizer_impl.cu:283-284),
+    //    stored by the scan into pinned memory, plus the error flag
     HIP_TRY(hipStreamSynchronize(s));
     if (h[0] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
@@ -311,7 +318,8 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
                                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), at<float2>(gb, g.off[GEOM_MEANS2D]),
-                                          rad, gx, gy, tile_keys, gids, emit_start, s));
+                                          rad, gx, gy, tile_keys, gids, emit_start, at<uint8_t>(bb, b.off[BIN_VALID]),
+                                          at<uint2>(ib, im.off[IMG_RANGES]), T, s));
         }
         DEBUG_SYNC(s);
         // stable sort by tile id over bits [0, bit) (rasterizer_impl.cu:303-311 sorts [0, 32+bit))
@@ -432,8 +440,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
                                       at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
         }
         {
-            ProfScope ps_(PK_RENDER_BWD, s);
-            HIP_TRY(hipMemsetAsync(r.valid, 0, (size_t)R, s));
+            ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emit_instances
             HIP_TRY(launch_render_bwd(r, T, s));
         }
         DEBUG_SYNC(s);

@@ -144,14 +144,14 @@ enum GeomArray {
     GEOM_TILES_TOUCHED,   // u32[P]
     GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched in depth order
     GEOM_COV3D,           // f32[6P]
-    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {conic a, b, c, opacity} {r, g, b, 1/depth}
+    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {ka, kb, kc, opacity} {r, g, b, 1/depth}
+                          // (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic; cullK scaled by log2(e)/2
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
     GEOM_EMIT_START,      // u32[P] first emission slot of each Gaussian
     GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
-    GEOM_SCAN_SCRATCH,    // u32[scan blocks + 64]
-    GEOM_FLAGS,           // u32[64] error flags / misc
+    GEOM_SCAN_SCRATCH,    // u64[scan chunks + 1] look-back status words + chunk ticket (zeroed by preprocess)
     GEOM_COUNT
 };
 
@@ -190,7 +190,7 @@ inline GeomLayout geom_layout(int P)
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p, 48 * p,
                                 4 * p, 4 * p, 4 * p, 16 * p + 1024, radix_status_bytes(P, 4),
-                                4 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 64), 4 * 64};
+                                8 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
     GeomLayout l;
     size_t o = 0;
     for (int i = 0; i < GEOM_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -30,7 +30,9 @@ struct PreprocessArgs {
     float* conic_opacity;
     uint8_t* clamped;
     uint32_t* tiles_touched;
-    uint32_t* flags;
+    uint32_t* host_flags;     // pinned host word: set to 1 on a prefiltered violation (no device memset)
+    uint64_t* scan_status;    // look-back status words of the tiles_touched scan, zeroed here
+    int scan_status_words;
     float4* splat;  // 3 x float4 per Gaussian (GEOM_SPLAT)
     uint32_t* dkey; // depth-sort key per Gaussian
 };
@@ -120,16 +122,21 @@ struct PreprocessBwdArgs {
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
-// inclusive scan of in[gather[i]] (gather may be null)
-hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
+// Inclusive scan of in[gather[i]] (gather may be null): one launch, chained chunks with decoupled
+// look-back over `status` (scan_status_words(n) u64 words, zero on entry: preprocess clears them).
+// The total goes to *total_out (pinned host memory is fine).
+int scan_status_words(int n);
+hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
                                  uint32_t* total_out, hipStream_t s);
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s);
+// Also clears valid[slot] (the backward's record flags) and ranges[0..T) for tile_ranges.
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
                                  const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, hipStream_t s);
+                                 uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s);
+// ranges must be zero on entry unless L == 0 (emit_instances clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
                              uint64_t* keys, hipStream_t s);

@@ -126,7 +126,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     // in_frustum (auxiliary.h:151-176)
     const f3 p_view = transformPoint4x3(p_orig, a.view);
     if (p_view.z <= 0.2f) {
-        if (a.prefiltered) atomicOr(a.flags, 1u);
+        if (a.prefiltered) __hip_atomic_store(a.host_flags, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         return;
     }
     const float4 p_hom = transformPoint4x4(p_orig, a.proj);
@@ -196,9 +196,14 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     float cullK = -1.0f;
     if (opacity >= 1.0f / 255.0f) cullK = (float)(2.0 * log(255.0 * (double)opacity) * 1.002 + 0.02);
     if (!(conic_x > 0.f && conic_z > 0.f && conic_x * conic_z - conic_y * conic_y > 0.f)) cullK = 3.0e38f;
+    // The record carries the conic pre-scaled into the log2-domain falloff the render kernels
+    // evaluate (render.hip Falloff: p2 = ka dx^2 + kb dx dy + kc dy^2 = log2(e) * power), and
+    // cullK in the same scale (q' = -(ka dx^2 + kb dx dy + kc dy^2) <= log2(e)/2 * K).
+    constexpr float LOG2E = 1.4426950408889634f;
+    if (cullK >= 0.f && cullK < 1.0e37f) cullK = cullK * (0.5f * LOG2E);
     float4* sp = a.splat + 3 * (size_t)idx;
     sp[0] = make_float4(pix_x, pix_y, cullK, 0.0f);
-    sp[1] = make_float4(conic_x, conic_y, conic_z, opacity);
+    sp[1] = make_float4((-0.5f * LOG2E) * conic_x, (-LOG2E) * conic_y, (-0.5f * LOG2E) * conic_z, opacity);
     sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
 }
 
@@ -212,6 +217,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
+    if (idx < a.scan_status_words) a.scan_status[idx] = 0;  // the scan runs after this kernel
     if (!STAGED) {
         if (idx < a.P) preprocess_one(a, idx, a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr);
         return;
@@ -239,9 +245,16 @@ __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* m
 }
 
 // ---------------------------------------------------------------------------
-// Inclusive scan of u32 counts (reduce-then-scan, 3 launches, no inter-block
-// spinning).  SCAN_ITEMS = 256 threads x 16 items per block.
+// Inclusive scan of u32 counts in one launch (cub::DeviceScan::InclusiveSum,
+// rasterizer_impl.cu:166,280): chunks of SCAN_ITEMS take a ticket (so every chunk's
+// predecessors were scheduled before it), reduce locally, publish their aggregate, then
+// resolve their exclusive prefix by decoupled look-back: one wave reads the status words of
+// the 64 preceding chunks at once and sums back to the nearest inclusive one.  A status word
+// is {flag (2 bits), value (32 bits)} in one 64-bit agent-scope atomic, so the value travels
+// with its flag.
 // ---------------------------------------------------------------------------
+constexpr uint64_t SCAN_AGG = 1ull << 62, SCAN_INC = 2ull << 62, SCAN_FLAGS = 3ull << 62;
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
     const int lane = threadIdx.x & 63;
@@ -272,64 +285,74 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* lds
     return wprefix + inc - v;
 }
 
-__device__ __forceinline__ uint32_t scan_in(const uint32_t* in, const uint32_t* gather, size_t i)
+// Exclusive prefix of chunk c from the status words of chunks < c (run by one whole wave).
+__device__ __forceinline__ uint32_t scan_lookback(uint64_t* status, int c, int lane)
 {
-    return gather ? in[gather[i]] : in[i];
-}
-
-__global__ void __launch_bounds__(256) scan_reduce_kernel(const uint32_t* in, const uint32_t* gather, int n,
-                                                          uint32_t* block_sums)
-{
-    __shared__ uint32_t lds4[4];
-    const size_t base = (size_t)blockIdx.x * SCAN_ITEMS;
-    uint32_t s = 0;
+    uint32_t excl = 0;
+    int j = c - 1;  // newest predecessor not yet summed
+    while (j >= 0) {
+        const int k = j - lane;
+        uint64_t st = k >= 0 ? __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : SCAN_INC;
+        const uint64_t inc = __ballot((st & SCAN_FLAGS) == SCAN_INC);
+        const int stop = inc ? (int)__builtin_ctzll(inc) : 63;  // lanes [0, stop] are needed
+        const uint64_t missing = __ballot((st & SCAN_FLAGS) == 0 && lane <= stop);
+        if (missing) continue;  // a needed predecessor has not published yet: re-read
+        uint32_t v = lane <= stop && k >= 0 ? (uint32_t)st : 0u;
 #pragma unroll
-    for (int k = 0; k < SCAN_ITEMS / 256; k++) {
-        size_t i = base + k * 256 + threadIdx.x;
-        if (i < (size_t)n) s += scan_in(in, gather, i);
+        for (int d = 32; d >= 1; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d, 64);
+        excl += v;
+        if (inc) break;
+        j -= 64;
     }
-    uint32_t total;
-    block_excl_scan256(s, lds4, total);
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = total;
+    return excl;
 }
 
-// single block: exclusive scan of block sums in place (nb can exceed 256; loop)
-__global__ void __launch_bounds__(256) scan_blocksums_kernel(uint32_t* block_sums, int nb, uint32_t* total_out)
+__global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, const uint32_t* gather, int n,
+                                                            int nchunks, uint64_t* status, uint32_t* out,
+                                                            uint32_t* total_out)
 {
     __shared__ uint32_t lds4[4];
-    uint32_t carry = 0;
-    for (int base = 0; base < nb; base += 256) {
-        int i = base + threadIdx.x;
-        uint32_t v = i < nb ? block_sums[i] : 0;
-        uint32_t total;
-        uint32_t ex = block_excl_scan256(v, lds4, total);
-        if (i < nb) block_sums[i] = carry + ex;
-        carry += total;
-    }
-    if (total_out && threadIdx.x == 0) *total_out = carry;
-}
-
-__global__ void __launch_bounds__(256) scan_apply_kernel(const uint32_t* in, const uint32_t* gather, int n,
-                                                         const uint32_t* block_offsets,
-                                                         uint32_t* out)
-{
-    __shared__ uint32_t lds4[4];
-    // each thread owns 16 consecutive items
-    const size_t base = (size_t)blockIdx.x * SCAN_ITEMS + (size_t)threadIdx.x * 16;
+    __shared__ uint32_t s_chunk, s_excl;
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + nchunks);
+    if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int c = (int)s_chunk;
+    // each thread owns 16 consecutive items; every load issued before the first use
+    const size_t base = (size_t)c * SCAN_ITEMS + (size_t)threadIdx.x * 16;
     uint32_t v[16];
-    uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        size_t i = base + k;
-        v[k] = i < (size_t)n ? scan_in(in, gather, i) : 0;
-        s += v[k];
+        const size_t i = base + k;
+        v[k] = i < (size_t)n ? (gather ? gather[i] : (uint32_t)i) : 0u;
     }
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = base + k < (size_t)n ? in[v[k]] : 0u;
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) s += v[k];
     uint32_t total;
-    uint32_t ex = block_excl_scan256(s, lds4, total) + block_offsets[blockIdx.x];
+    uint32_t ex = block_excl_scan256(s, lds4, total);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        if (lane == 0)
+            __hip_atomic_store(status + c, (c == 0 ? SCAN_INC : SCAN_AGG) | total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t excl = c == 0 ? 0u : scan_lookback(status, c, lane);
+        if (lane == 0) {
+            if (c > 0)
+                __hip_atomic_store(status + c, SCAN_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (c == nchunks - 1)
+                __hip_atomic_store(total_out, excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            s_excl = excl;
+        }
+    }
+    __syncthreads();
+    ex += s_excl;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         ex += v[k];
-        size_t i = base + k;
+        const size_t i = base + k;
         if (i < (size_t)n) out[i] = ex;
     }
 }
@@ -357,14 +380,14 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
     return hipGetLastError();
 }
 
-hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint32_t* scratch,
+int scan_status_words(int n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS + 1; }  // + the ticket
+
+hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
                                  uint32_t* total_out, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch);
-    hipLaunchKernelGGL(scan_blocksums_kernel, dim3(1), dim3(256), 0, s, scratch, nb, total_out);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, scratch, out);
+    hipLaunchKernelGGL(scan_lookback_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, nb, status, out, total_out);
     return hipGetLastError();
 }
 

@@ -29,13 +29,15 @@
 namespace gsr {
 
 constexpr int RS_THREADS = 256;
-constexpr int RS_ITEMS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ITEMS;  // 4096 elements per chunk
+constexpr int RS_ITEMS = 16;                    // elements per thread, long sorts (the tile sort)
+constexpr int RS_ITEMS_SHORT = 4;               // short sorts (the depth sort): 4x the workgroups
+constexpr int RS_SHORT_MAX = 1 << 21;           // n up to which a sort counts as short
 constexpr int RS_MAXBINS = 256;
 
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
 // (1) counts[d * nchunks + c] = number of elements of chunk c with digit d.
+template <int ITEMS>
 __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t* keys, int n, int shift, int nbits,
                                                                 int nchunks, uint32_t* counts)
 {
@@ -44,12 +46,12 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t*
     const uint32_t nb = 1u << nbits, mask = nb - 1u;
     for (int q = 0; q < 4; q++) h[q][tid] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * RS_TILE;
-    uint32_t k[RS_ITEMS];
+    const size_t base = (size_t)blockIdx.x * (RS_THREADS * ITEMS);
+    uint32_t k[ITEMS];
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
+    for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++)
+    for (int i = 0; i < ITEMS; i++)
         if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
     __syncthreads();
     if ((uint32_t)tid < nb) counts[(size_t)tid * nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
@@ -102,15 +104,16 @@ struct SortPassArgs {
 };
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
-template <bool PAIR>
+template <int ITEMS, bool PAIR>
 __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs a)
 {
+    constexpr int TILE = RS_THREADS * ITEMS;
     using Val = typename std::conditional<PAIR, uint2, uint32_t>::type;
     __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
     __shared__ uint32_t s_blk[RS_MAXBINS];     // block-local start of each digit
     __shared__ uint32_t s_base[RS_MAXBINS];    // global start of each digit for this chunk
-    __shared__ uint32_t s_keys[RS_TILE];
-    __shared__ Val s_vals[RS_TILE];
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ Val s_vals[TILE];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nb = 1u << a.nbits, mask = nb - 1u;
@@ -129,28 +132,28 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     }
     const uint32_t gbase = s_base[tid] - tot + rowp;
 
-    const size_t base = (size_t)chunk * RS_TILE;
-    const int nvalid = (int)min((size_t)RS_TILE, (size_t)a.n - base);
-    uint32_t key[RS_ITEMS], rank[RS_ITEMS];
-    Val val[RS_ITEMS];
+    const size_t base = (size_t)chunk * TILE;
+    const int nvalid = (int)min((size_t)TILE, (size_t)a.n - base);
+    uint32_t key[ITEMS], rank[ITEMS];
+    Val val[ITEMS];
     const uint64_t lt = (1ull << lane) - 1ull;
     // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
-    auto gidx = [&](int i) { return base + (size_t)min(w * (RS_ITEMS * 64) + i * 64 + lane, nvalid - 1); };
+    auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) key[i] = a.keys_in[gidx(i)];
+    for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
     if (a.vals_in) {
 #pragma unroll
-        for (int i = 0; i < RS_ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
+        for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
     } else {
 #pragma unroll
-        for (int i = 0; i < RS_ITEMS; i++) {
+        for (int i = 0; i < ITEMS; i++) {
             if constexpr (PAIR) val[i] = make_uint2((uint32_t)gidx(i), a.gids[gidx(i)]);
             else val[i] = (uint32_t)gidx(i);
         }
     }
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) {
-        const int li = w * (RS_ITEMS * 64) + i * 64 + lane;
+    for (int i = 0; i < ITEMS; i++) {
+        const int li = w * (ITEMS * 64) + i * 64 + lane;
         const bool valid = li < nvalid;
         const uint32_t d = digit_of(key[i], a.shift, mask);
         uint64_t peers = __ballot(valid);
@@ -189,7 +192,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 
     // scatter into LDS in block-local sorted (stable) order
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) {
+    for (int i = 0; i < ITEMS; i++) {
         if (rank[i] != 0xFFFFFFFFu) {
             const uint32_t d = digit_of(key[i], a.shift, mask);
             const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
@@ -200,7 +203,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     __syncthreads();
     // contiguous write-out: runs of one digit map to consecutive global addresses
 #pragma unroll
-    for (int i = 0; i < RS_ITEMS; i++) {
+    for (int i = 0; i < ITEMS; i++) {
         const int lpos = i * RS_THREADS + tid;
         if (lpos < nvalid) {
             const uint32_t k = s_keys[lpos];
@@ -232,11 +235,14 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
                                                              const uint32_t* offsets_d, const float2* means2D,
                                                              const int* radii, uint32_t gx, uint32_t gy,
                                                              uint32_t* tile_keys, uint32_t* gids,
-                                                             uint32_t* emit_start)
+                                                             uint32_t* emit_start, uint8_t* valid, uint2* ranges,
+                                                             int T)
 {
     __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k0 = (blockIdx.x * 4 + w) * 64;
+    // ranges must be zero for tile_ranges (empty tiles keep (0, 0)): cleared here, not by a memset
+    for (int t = blockIdx.x * 256 + (int)threadIdx.x; t < T; t += gridDim.x * 256) ranges[t] = make_uint2(0u, 0u);
     if (k0 >= P) return;  // whole wave out of range (waves are independent: no block barriers)
     const int k = k0 + lane;
     uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1, g = 0;
@@ -275,6 +281,7 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
         const uint32_t yy = local / wj, xx = local - yy * wj;
         tile_keys[sl] = (s_y0[w][j] + yy) * gx + (s_x0[w][j] + xx);
         gids[sl] = s_g[w][j];
+        valid[sl] = 0;  // the backward flags the records it writes
     }
 }
 
@@ -302,7 +309,12 @@ __global__ void __launch_bounds__(256) debug_keys_kernel(int L, const uint32_t* 
     keys[idx] = ((uint64_t)sorted_tiles[idx] << 32) | __float_as_uint(depths[point_list[idx]]);
 }
 
-static inline size_t rs_chunks(int n) { return ((size_t)(n > 0 ? n : 0) + RS_TILE - 1) / RS_TILE; }
+static inline int rs_items(int n) { return n <= RS_SHORT_MAX ? RS_ITEMS_SHORT : RS_ITEMS; }
+static inline size_t rs_chunks(int n)
+{
+    const size_t tile = (size_t)RS_THREADS * rs_items(n);
+    return ((size_t)(n > 0 ? n : 0) + tile - 1) / tile;
+}
 
 // Scratch of one sort: the (bins x chunks) count matrix and the bin totals (reused by every pass).
 size_t radix_status_bytes(int n, int npass)
@@ -331,8 +343,13 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
     for (int p = 0; p < npass; p++) {
         const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
         const bool last = p == npass - 1;
-        hipLaunchKernelGGL(radix_count_kernel, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, kin, n, shift, w,
-                           nchunks, counts);
+        const bool shrt = rs_items(n) == RS_ITEMS_SHORT;
+        if (shrt)
+            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS_SHORT>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s,
+                               kin, n, shift, w, nchunks, counts);
+        else
+            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, kin,
+                               n, shift, w, nchunks, counts);
         hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks, totals);
         SortPassArgs a;
         a.n = n;
@@ -349,8 +366,14 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
         a.sorted_keys = sorted_keys;
         a.row_prefix = counts;
         a.totals = totals;
-        if (gids) hipLaunchKernelGGL(radix_scatter_kernel<true>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, a);
-        else hipLaunchKernelGGL(radix_scatter_kernel<false>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, a);
+        const dim3 g((unsigned)nchunks), b(RS_THREADS);
+        if (shrt) {
+            if (gids) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, true>), g, b, 0, s, a);
+            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, false>), g, b, 0, s, a);
+        } else {
+            if (gids) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, a);
+            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false>), g, b, 0, s, a);
+        }
         kin = a.keys_out;
         vin = a.vals_out;
         shift += w;
@@ -360,18 +383,17 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
 
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
                                  const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, hipStream_t s)
+                                 uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       means2D, radii, gx, gy, tile_keys, gids, emit_start);
+                       means2D, radii, gx, gy, tile_keys, gids, emit_start, valid, ranges, T);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);
-    if (e != hipSuccess || L <= 0) return e;
+    if (L <= 0) return hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);  // no emit ran to clear them
     hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, sorted_tiles, ranges);
     return hipGetLastError();
 }

@@ -69,18 +69,20 @@ __device__ __forceinline__ float box_min_quadform(float a, float b, float c, flo
 
 // 4-bit mask: bit w set <=> some pixel centre of wave w's 8x8 quadrant lies inside the
 // record's cull ellipse (d^T conic d <= cullK, see preprocess.hip), i.e. can reach
-// alpha >= 1/255.  Evaluated once per loaded record by one lane (lane-parallel).
-__device__ __forceinline__ uint32_t quad_mask(const float4 r0, const float4 co, uint32_t tx, uint32_t ty)
+// alpha >= 1/255.  The record holds the conic and cullK both scaled by log2(e)/2 (the falloff
+// form (ka, kb, kc) = -log2(e) (a/2, b, c/2)).  Evaluated once per loaded record by one lane.
+__device__ __forceinline__ uint32_t quad_mask(const float4 r0, const float4 k, uint32_t tx, uint32_t ty)
 {
     const float K = r0.z;
     if (K > 1.0e37f) return 0xFu;  // degenerate conic: never cull
     if (K < 0.f) return 0u;
     const float dx0 = (float)(tx * GSR_BLOCK_X) - r0.x, dy0 = (float)(ty * GSR_BLOCK_Y) - r0.y;
+    const float qa = -k.x, qb = -0.5f * k.y, qc = -k.z;
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const float ox = dx0 + (float)((q & 1) * 8), oy = dy0 + (float)((q >> 1) * 8);
-        if (box_min_quadform(co.x, co.y, co.z, ox, ox + 7.f, oy, oy + 7.f) <= K) m |= 1u << q;
+        if (box_min_quadform(qa, qb, qc, ox, ox + 7.f, oy, oy + 7.f) <= K) m |= 1u << q;
     }
     return m;
 }
@@ -96,14 +98,11 @@ __device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elem
 // Gaussian falloff exponent in the log2 domain, shared by forward and backward so that both
 // make identical alpha decisions: with (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic,
 // p2 = (ka dx + kb dy) dx + kc dy^2 = log2(e) * power (forward.cu:353-354), G = 2^p2.
+// preprocess stores (ka, kb, kc) in the render record (.xyz of its second float4).
 struct Falloff {
     float ka, kb, kc;
 };
-constexpr float LOG2E = 1.4426950408889634f;
-__device__ __forceinline__ Falloff falloff(const float4 co)
-{
-    return {-0.5f * LOG2E * co.x, -LOG2E * co.y, -0.5f * LOG2E * co.z};
-}
+__device__ __forceinline__ Falloff falloff(const float4 co) { return {co.x, co.y, co.z}; }
 __device__ __forceinline__ float falloff_p2(const Falloff f, float dx, float dy)
 {
     const float bq = f.kb * dy;
@@ -147,20 +146,29 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, c
     s_cnt[tid] = 0;
     if (tid == 0) { s_max = 0; s_zero = 0; }
     uint32_t mx = 0;
-    for (int t = tid; t < T; t += 1024) {
-        const uint32_t w = load_work(t);
-        if (t < ORDER_CACHE) s_work[t] = w;
-        mx = max(mx, w);
+    {  // all loads of the cached part in flight at once (one HBM round trip, not T/1024)
+        uint32_t w[ORDER_CACHE / 1024];
+#pragma unroll
+        for (int i = 0; i < ORDER_CACHE / 1024; i++) {
+            const int t = i * 1024 + tid;
+            w[i] = t < T ? load_work(t) : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < ORDER_CACHE / 1024; i++) {
+            s_work[i * 1024 + tid] = w[i];
+            mx = max(mx, w[i]);
+        }
     }
+    for (int t = ORDER_CACHE + tid; t < T; t += 1024) mx = max(mx, load_work(t));
     mx = wave_max_u32(mx);
     __syncthreads();
     if (lane == 0) atomicMax(&s_max, mx);
     __syncthreads();
-    const uint64_t wmax = max(s_max, 1u);
+    const float scale = (float)(ORDER_BUCKETS - 1) / (float)max(s_max, 1u);  // no 64-bit division
     // tiles with no work go last, in index order (wave-aggregated: one LDS atomic per wave and
     // round instead of one per tile on a single hot counter); the rest into NB work classes
     auto bucket = [&](uint32_t w) -> uint32_t {
-        return (uint32_t)(ORDER_BUCKETS - 1) - (uint32_t)(((uint64_t)w * (ORDER_BUCKETS - 1)) / wmax);
+        return (uint32_t)(ORDER_BUCKETS - 1) - min((uint32_t)((float)w * scale), (uint32_t)(ORDER_BUCKETS - 1));
     };
     for (int t = tid; t < T; t += 1024) {
         const uint32_t w = work_of(t);
