@@ -257,8 +257,11 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
         uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + 2 * q);
         uint32_t* v1 = reinterpret_cast<uint32_t*>(tmp + 3 * q);
         ProfScope ps_(PK_DEPTH_SORT, s);
+        // the last pass also lays tiles_touched out in depth order (into point_offsets, which
+        // the scan then turns into offsets in place)
         HIP_TRY(radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
-                           gb + g.off[GEOM_RADIX_SCRATCH], s));
+                           gb + g.off[GEOM_RADIX_SCRATCH], s, a.tiles_touched,
+                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])));
     }
     DEBUG_SYNC(s);
 
@@ -266,7 +269,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
     {
         ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(a.tiles_touched, sorted_ids, offsets, P, a.scan_status, h_dev + 2, s));
+        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s));
     }
     DEBUG_SYNC(s);
 

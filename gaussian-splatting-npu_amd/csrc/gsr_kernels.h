@@ -131,7 +131,8 @@ hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uin
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
-                      char* scratch, hipStream_t s);
+                      char* scratch, hipStream_t s, const uint32_t* gather_tab = nullptr,
+                      uint32_t* gather_out = nullptr);
 // Also clears valid[slot] (the backward's record flags) and ranges[0..T) for tile_ranges.
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
                                  const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,

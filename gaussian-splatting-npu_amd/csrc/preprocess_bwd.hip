@@ -13,15 +13,80 @@ namespace gsr {
 
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
+// Per-Gaussian inputs, loaded before the workgroup's SH staging so that their memory round trips
+// overlap it (and each other): every load is issued unconditionally (clamped indices, values
+// masked after), so no branch sits between a load and the next one.
+struct BwdIn {
+    bool visible;
+    float g[GF_NUM];  // sums of this Gaussian's per-tile gradient records
+    float4 co;        // conic + (rendered) opacity
+    float cov[6];
+    f3 mean;
+    float4 rot;
+    f3 scale;
+    float opacity;
+    uint8_t clamped;
+};
+
+__device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in)
+{
+    const size_t i = (size_t)idx;
+    in.visible = a.radii[idx] > 0;
+    in.co = a.conic_opacity[idx];
+#pragma unroll
+    for (int k = 0; k < 6; k++) in.cov[k] = a.cov3Ds[6 * i + k];
+    in.mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
+    in.opacity = a.opacities[idx];
+    in.clamped = a.clamped[idx];
+    if (a.scales) {  // uniform over the launch
+        const float* rp = a.rotations + 4 * i;
+        in.rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        in.scale = {a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]};
+    }
+#pragma unroll
+    for (int q = 0; q < GF_NUM; q++) in.g[q] = 0.f;
+    // This Gaussian's records are contiguous (emission order); entries that contributed to no
+    // pixel were never written (valid = 0) and are not read (most slots: records are sparse).
+    // Eight flags per step in flight together, then the flagged records; the sum order stays
+    // the slot order (bitwise reproducible).
+    const uint32_t e0 = a.emit_start[idx];
+    const uint32_t e1 = e0 + a.tiles_touched[idx];  // 0 tiles for culled Gaussians
+    for (uint32_t e = e0; e < e1; e += 8) {
+        bool v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = a.valid[min(e + k, e1 - 1)] != 0 && e + k < e1;
+        float4 r[8][3];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (v[k]) {
+                const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)(e + k) * GRAD_REC);
+                r[k][0] = rec[0];
+                r[k][1] = rec[1];
+                r[k][2] = rec[2];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (v[k]) {
+                float* g = in.g;
+                g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
+                g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
+                g[8] += r[k][2].x; g[9] += r[k][2].y;
+            }
+        }
+    }
+}
+
 // One Gaussian.  `sh` / `dsh` point at this Gaussian's SH coefficients and SH gradient,
 // either in global memory or in the workgroup's LDS staging slot (the same slot for both).
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const float* sh, float* dsh)
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in,
+                                                   const float* sh, float* dsh)
 {
     const size_t i = (size_t)idx;
     float* dmean = a.dL_dmean3D + 3 * i;
     float* dcov = a.dL_dcov3D + 6 * i;
 
-    if (!(a.radii[idx] > 0)) {
+    if (!in.visible) {
         a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
         a.dL_dconic[4 * i] = 0.f; a.dL_dconic[4 * i + 1] = 0.f; a.dL_dconic[4 * i + 2] = 0.f;
         a.dL_dconic[4 * i + 3] = 0.f;
@@ -38,43 +103,12 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         return;
     }
 
-    // ------- gather this Gaussian's per-tile gradient records (deterministic order) -------
     float g[GF_NUM];
 #pragma unroll
-    for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
-    {
-        // This Gaussian's records are contiguous (emission order); entries that contributed to
-        // no pixel were never written (valid = 0) and are skipped.  Four slots per step so that
-        // their loads are in flight together; the sum order stays the slot order.
-        const uint32_t e0 = a.emit_start[idx];
-        const uint32_t e1 = e0 + a.tiles_touched[idx];
-        for (uint32_t e = e0; e < e1; e += 4) {
-            bool v[4];
-            float4 r[4][3];
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = e + k < e1 && a.valid[e + k];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (v[k]) {
-                    const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)(e + k) * GRAD_REC);
-                    r[k][0] = rec[0];
-                    r[k][1] = rec[1];
-                    r[k][2] = rec[2];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                if (v[k]) {
-                    g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
-                    g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
-                    g[8] += r[k][2].x; g[9] += r[k][2].y;
-                }
-            }
-        }
-    }
+    for (int q = 0; q < GF_NUM; q++) g[q] = in.g[q];
     {
         // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
-        const float4 co = a.conic_opacity[idx];
+        const float4 co = in.co;
         const float op = co.w;
         const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
         g[GF_MEAN2D_X] = (co.x * sx + co.y * sy) * (-op * (0.5f * a.W));
@@ -91,8 +125,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
 
     // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
-    const float* cov3D = a.cov3Ds + 6 * i;
-    const f3 mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
+    const float* cov3D = in.cov;
+    const f3 mean = in.mean;
     const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
     const float* view = a.view;
     f3 t = transformPoint4x3(mean, view);
@@ -124,7 +158,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
         const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
         const float dL_dopacity_v = g[GF_OPACITY];
-        const float d_h_convolution_scaling = dL_dopacity_v * a.opacities[idx];
+        const float d_h_convolution_scaling = dL_dopacity_v * in.opacity;
         a.dL_dopacity[idx] = dL_dopacity_v * h_convolution_scaling;
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
                                                                     : d_h_convolution_scaling / (2 * h_convolution_scaling);
@@ -213,7 +247,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
         const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
         const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-        const uint8_t cl = a.clamped[idx];
+        const uint8_t cl = in.clamped;
         float dRGB[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) {
@@ -314,15 +348,14 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 
     // ---------------- computeCov3D backward (backward.cu:330-393) ----------------
     if (a.scales) {
-        const float* rp = a.rotations + 4 * i;
-        const float r = rp[0], x = rp[1], y = rp[2], z = rp[3];
+        const float r = in.rot.x, x = in.rot.y, y = in.rot.z, z = in.rot.w;
         const mat3 R = mat3_cols(
             1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
             2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
             2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
         mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
         const float mod = a.scale_modifier;
-        const f3 s = {mod * a.scales[3 * i], mod * a.scales[3 * i + 1], mod * a.scales[3 * i + 2]};
+        const f3 s = {mod * in.scale.x, mod * in.scale.y, mod * in.scale.z};
         S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
         const mat3 M = mat3_mul(S, R);
         const float* d = dcov;
@@ -370,10 +403,13 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
+    BwdIn in;
+    if (idx < a.P) bwd_gather(a, idx, in);  // in flight during the SH staging below
     if (!STAGED) {
         if (idx < a.P) {
             const size_t w3 = (size_t)a.M * 3;
-            preprocess_bwd_one(a, idx, a.shs ? a.shs + idx * w3 : nullptr, a.dL_dsh ? a.dL_dsh + idx * w3 : nullptr);
+            preprocess_bwd_one(a, idx, in, a.shs ? a.shs + idx * w3 : nullptr,
+                               a.dL_dsh ? a.dL_dsh + idx * w3 : nullptr);
         }
         return;
     }
@@ -390,7 +426,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     __syncthreads();
     if (idx < a.P) {
         float* row = s_sh + threadIdx.x * lds_stride;
-        preprocess_bwd_one(a, idx, row, row);
+        preprocess_bwd_one(a, idx, in, row, row);
     }
     __syncthreads();
     float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * W3);

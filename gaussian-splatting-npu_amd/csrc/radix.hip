@@ -99,6 +99,8 @@ struct SortPassArgs {
     uint32_t* out_x;
     uint32_t* out_y;
     uint32_t* sorted_keys;
+    const uint32_t* gather_tab;  // final pass, single payload: gather_out[dst] = gather_tab[v] (may be null)
+    uint32_t* gather_out;
     const uint32_t* row_prefix;  // (nbins, nchunks) exclusive row scans
     const uint32_t* totals;      // (nbins) digit totals
 };
@@ -219,6 +221,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
                     if (a.out_y) a.out_y[dst] = v.y;
                 } else {
                     if (a.out_x) a.out_x[dst] = v;
+                    if (a.gather_tab) a.gather_out[dst] = a.gather_tab[v];
                 }
                 if (a.sorted_keys) a.sorted_keys[dst] = k;
             }
@@ -326,10 +329,11 @@ size_t radix_status_bytes(int n, int npass)
 // Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, and
 // with `gids` also gids[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
 // gids); the last pass writes out_x[dst] = i, out_y[dst] = gids[i] and sorted_keys[dst] = key
-// (any of them may be null).  All writes are contiguous runs: no gathers, no scattered stores.
+// (any of them may be null); without gids it can also write gather_out[dst] = gather_tab[i].
+// All writes are contiguous runs: no scattered stores.
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
-                      char* scratch, hipStream_t s)
+                      char* scratch, hipStream_t s, const uint32_t* gather_tab, uint32_t* gather_out)
 {
     if (n <= 0) return hipSuccess;
     const int nchunks = (int)rs_chunks(n);
@@ -364,6 +368,8 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
         a.out_x = out_x;
         a.out_y = out_y;
         a.sorted_keys = sorted_keys;
+        a.gather_tab = (last && !gids) ? gather_tab : nullptr;
+        a.gather_out = gather_out;
         a.row_prefix = counts;
         a.totals = totals;
         const dim3 g((unsigned)nchunks), b(RS_THREADS);

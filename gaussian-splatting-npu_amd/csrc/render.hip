@@ -124,89 +124,102 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 }
 
 // ---- longest-first tile order ---------------------------------------------------------------
-// One 1024-thread workgroup buckets the T tiles by work into NB classes, heaviest first, and
-// writes the launch order.  Workgroups start roughly in blockIdx order, so the long tiles are
-// dispatched first and the tail of the launch is made of short ones (list scheduling, LPT).
-// The order inside a class is whatever the LDS atomics give: tiles are independent, so the
-// launch order changes timing only, never a result.
-constexpr int ORDER_BUCKETS = 1024;
+// One 1024-thread workgroup sorts the T tiles into 64 work classes, heaviest first, and writes
+// the launch order.  Workgroups start roughly in blockIdx order,
+// so the long tiles are dispatched first and the tail of the launch is made of short ones
+// (list scheduling, LPT; 64 classes schedule within 1 % of an exact sort on the 1080p scene).
+// Ranking is atomic-free: each wave matches its 64 lanes' classes with 6 ballots, like the
+// radix scatter, so the order is deterministic.  Tiles are independent, so the launch order
+// changes timing only, never a result.
+constexpr int ORDER_BITS = 6;         // 64 work classes; tiles without work join the last one
+constexpr int ORDER_PER_THREAD = 16;  // tiles per thread and pass: 16,384 per pass
 
-constexpr int ORDER_CACHE = 16384;  // tiles whose work stays in LDS (4K UHD: 32,400 tiles reload)
-
+template <bool FROM_RANGES>
 __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, const uint32_t* work, int T,
                                                           uint32_t* order)
 {
-    __shared__ uint32_t s_cnt[ORDER_BUCKETS];
-    __shared__ uint32_t s_work[ORDER_CACHE];
-    __shared__ uint32_t s_wsum[16];
-    __shared__ uint32_t s_max, s_zero;
+    __shared__ uint32_t s_cnt[16][1 << ORDER_BITS];  // per-wave class counts, then per-wave starts
+    __shared__ uint32_t s_order[1024 * ORDER_PER_THREAD];  // the pass's order, stored out coalesced
+    __shared__ uint32_t s_max;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    auto load_work = [&](int t) -> uint32_t { return ranges ? ranges[t].y - ranges[t].x : work[t]; };
-    auto work_of = [&](int t) -> uint32_t { return t < ORDER_CACHE ? s_work[t] : load_work(t); };
-    s_cnt[tid] = 0;
-    if (tid == 0) { s_max = 0; s_zero = 0; }
-    uint32_t mx = 0;
-    {  // all loads of the cached part in flight at once (one HBM round trip, not T/1024)
-        uint32_t w[ORDER_CACHE / 1024];
-#pragma unroll
-        for (int i = 0; i < ORDER_CACHE / 1024; i++) {
-            const int t = i * 1024 + tid;
-            w[i] = t < T ? load_work(t) : 0u;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    // unconditional (clamped) loads, so that a pass has all of them in flight at once
+    auto load_work = [&](int t) -> uint32_t {
+        const int tc = min(t, T - 1);
+        uint32_t v;
+        if constexpr (FROM_RANGES) {
+            const uint2 r = ranges[tc];
+            v = r.y - r.x;
+        } else {
+            v = work[tc];
         }
-#pragma unroll
-        for (int i = 0; i < ORDER_CACHE / 1024; i++) {
-            s_work[i * 1024 + tid] = w[i];
-            mx = max(mx, w[i]);
-        }
-    }
-    for (int t = ORDER_CACHE + tid; t < T; t += 1024) mx = max(mx, load_work(t));
-    mx = wave_max_u32(mx);
-    __syncthreads();
-    if (lane == 0) atomicMax(&s_max, mx);
-    __syncthreads();
-    const float scale = (float)(ORDER_BUCKETS - 1) / (float)max(s_max, 1u);  // no 64-bit division
-    // tiles with no work go last, in index order (wave-aggregated: one LDS atomic per wave and
-    // round instead of one per tile on a single hot counter); the rest into NB work classes
-    auto bucket = [&](uint32_t w) -> uint32_t {
-        return (uint32_t)(ORDER_BUCKETS - 1) - min((uint32_t)((float)w * scale), (uint32_t)(ORDER_BUCKETS - 1));
+        return t < T ? v : 0u;
     };
-    for (int t = tid; t < T; t += 1024) {
-        const uint32_t w = work_of(t);
-        if (w > 0) atomicAdd(&s_cnt[bucket(w)], 1u);
-    }
-    // exclusive scan of the class counts
-    __syncthreads();
-    const uint32_t c = s_cnt[tid];
-    uint32_t inc = c;
+    if (tid == 0) s_max = 0;
+    // Above 16,384 tiles the passes order each 16K block separately (longest-first inside it).
+    for (int t0 = 0; t0 < T; t0 += 1024 * ORDER_PER_THREAD) {
+        uint32_t w[ORDER_PER_THREAD];  // wave wid, item i: the 64 consecutive tiles t0 + (i * 16 + wid) * 64 + lane
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
-        if (lane >= d) inc += y;
-    }
-    if (lane == 63) s_wsum[wid] = inc;
-    __syncthreads();
-    uint32_t before = 0, nonzero = 0;
+        for (int i = 0; i < ORDER_PER_THREAD; i++) w[i] = load_work(t0 + (i * 16 + wid) * 64 + lane);
+        for (int q = tid; q < 16 * (1 << ORDER_BITS); q += 1024) (&s_cnt[0][0])[q] = 0;
+        if (t0 == 0) {  // classes are relative to the largest work of ALL tiles
+            uint32_t mx = 0;
+            for (int t = 1024 * ORDER_PER_THREAD + tid; t < T; t += 1024) mx = max(mx, load_work(t));
 #pragma unroll
-    for (int w = 0; w < 16; w++) {
-        before += w < wid ? s_wsum[w] : 0u;
-        nonzero += s_wsum[w];
-    }
-    s_cnt[tid] = before + inc - c;
-    __syncthreads();
-    for (int t0 = 0; t0 < T; t0 += 1024) {
-        const int t = t0 + tid;
-        const uint32_t w = t < T ? work_of(t) : 1u;
-        const uint64_t zb = __ballot(w == 0);
-        uint32_t zbase = 0;
-        if (zb) {
-            if (lane == 0) zbase = atomicAdd(&s_zero, (uint32_t)__popcll(zb));
-            zbase = (uint32_t)__shfl((int)zbase, 0, 64);
+            for (int i = 0; i < ORDER_PER_THREAD; i++) mx = max(mx, w[i]);
+            mx = wave_max_u32(mx);
+            __syncthreads();
+            if (lane == 0) atomicMax(&s_max, mx);
         }
-        if (t < T) {
-            if (w > 0) order[atomicAdd(&s_cnt[bucket(w)], 1u)] = (uint32_t)t;
-            else order[nonzero + zbase + __builtin_amdgcn_mbcnt_hi((uint32_t)(zb >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)zb, 0))] = (uint32_t)t;
+        __syncthreads();
+        const float scale = 63.0f / (float)max(s_max, 1u);
+        uint32_t cls[ORDER_PER_THREAD], rank[ORDER_PER_THREAD];
+#pragma unroll
+        for (int i = 0; i < ORDER_PER_THREAD; i++) {
+            const int t = t0 + (i * 16 + wid) * 64 + lane;
+            const uint32_t c = 63u - min((uint32_t)((float)w[i] * scale), 63u);
+            cls[i] = c;
+            uint64_t peers = __ballot(t < T);
+#pragma unroll
+            for (int bit = 0; bit < ORDER_BITS; bit++) {
+                const uint64_t bal = __ballot((c >> bit) & 1u);
+                peers &= ((c >> bit) & 1u) ? bal : ~bal;
+            }
+            const uint32_t before = s_cnt[wid][c];  // the wave's running count of class c
+            rank[i] = before + (uint32_t)__popcll(peers & lt);
+            if (t < T && (peers & lt) == 0ull) s_cnt[wid][c] = before + (uint32_t)__popcll(peers);
+            __builtin_amdgcn_wave_barrier();
         }
+        __syncthreads();
+        // thread (wave q, class c = lane): start of wave q's class-c tiles = class start + the
+        // class-c counts of waves < q; class starts = exclusive scan of the class totals
+        {
+            uint32_t tot = 0, mine = 0;
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t n = s_cnt[q][lane];
+                mine += q < wid ? n : 0u;
+                tot += n;
+            }
+            uint32_t inc = tot;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc += y;
+            }
+            __syncthreads();
+            s_cnt[wid][lane] = inc - tot + mine;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ORDER_PER_THREAD; i++) {
+            const int t = t0 + (i * 16 + wid) * 64 + lane;
+            if (t < T) s_order[s_cnt[wid][cls[i]] + rank[i]] = (uint32_t)t;
+        }
+        __syncthreads();
+        const int n = min(T - t0, 1024 * ORDER_PER_THREAD);
+        for (int q = tid; q < n; q += 1024) order[t0 + q] = s_order[q];
+        __syncthreads();
     }
 }
 
@@ -232,20 +245,20 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
     float C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
     uint32_t last_contributor = 0;
 
+    // list ids are fetched one batch ahead, so a batch waits for its record gather only
+    uint32_t next_id = todo > 0 ? a.point_list[range.x + min(tid, todo - 1)] : 0u;
     for (int base = 0; base < todo; base += BATCH) {
         if (__syncthreads_and(done)) break;
         const int k = base + tid;
-        uint32_t m = 0;
-        if (k < todo) {
-            const uint32_t id = a.point_list[range.x + k];
-            const float4* r = a.splat + 3 * (size_t)id;
-            const float4 r0 = r[0];
-            s_rec[tid] = r0;
-            const float4 r1 = r[1];
-            s_rec[BATCH + tid] = r1;
-            s_rec[2 * BATCH + tid] = r[2];
-            m = quad_mask(r0, r1, tx, ty);
-        }
+        const uint32_t id = next_id;
+        next_id = a.point_list[range.x + min(k + BATCH, todo - 1)];
+        // unconditional (clamped) record loads: no branch between issue and use
+        const float4* r = a.splat + 3 * (size_t)id;
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+        s_rec[tid] = r0;
+        s_rec[BATCH + tid] = r1;
+        s_rec[2 * BATCH + tid] = r2;
+        const uint32_t m = k < todo ? quad_mask(r0, r1, tx, ty) : 0u;
         s_mask[tid] = (uint8_t)m;
         __syncthreads();
         const int n = min(BATCH, todo - base);
@@ -439,39 +452,54 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     const float py0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
     const v2f pfx = {px0, px0 + 8.f};
 
+    // Pixel state: every load issued before the first use (clamped addresses, masked after), so
+    // the prologue costs one memory round trip instead of one per pixel.
+    float Tf[4], dp0[4], dp1[4], dp2[4], dinv[4];
+    float4 acc[4];
+    uint32_t lc[4];
+    bool inside[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {  // q = 2 h + e: pixel (x + 8 e, y + 8 h)
+        const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * (q & 1);
+        const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * (q >> 1);
+        inside[q] = px < (uint32_t)a.W && py < (uint32_t)a.H;
+        const uint32_t pix_id = inside[q] ? (uint32_t)a.W * py + px : 0u;
+        Tf[q] = a.final_Ts[pix_id];
+        acc[q] = a.accum[pix_id];
+        lc[q] = a.n_contrib[pix_id];
+        dp0[q] = a.dL_dpixels[0 * HW + pix_id];
+        dp1[q] = a.dL_dpixels[1 * HW + pix_id];
+        dp2[q] = a.dL_dpixels[2 * HW + pix_id];
+        dinv[q] = HAS_INV ? a.dL_invdepths[pix_id] : 0.f;
+    }
+    const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
     uint32_t qmax[4];
+    float R[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (!inside[q]) {
+            Tf[q] = 0.f;
+            acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            lc[q] = 0u;
+            dp0[q] = dp1[q] = dp2[q] = dinv[q] = 0.f;
+        }
+        R[q] = (acc[q].x + Tf[q] * bg0) * dp0[q] + (acc[q].y + Tf[q] * bg1) * dp1[q] +
+               (acc[q].z + Tf[q] * bg2) * dp2[q] + acc[q].w * dinv[q];
+        qmax[q] = __builtin_amdgcn_readfirstlane(wave_max_u32(lc[q]));
+    }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        float dp0[2], dp1[2], dp2[2], dinv[2], R[2];
-        uint32_t lc[2];
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * e;
-            const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * h;
-            const bool inside = px < (uint32_t)a.W && py < (uint32_t)a.H;
-            const uint32_t pix_id = (uint32_t)a.W * py + px;
-            const float Tf = inside ? a.final_Ts[pix_id] : 0.f;
-            const float4 acc = inside ? a.accum[pix_id] : make_float4(0.f, 0.f, 0.f, 0.f);
-            lc[e] = inside ? a.n_contrib[pix_id] : 0u;
-            dp0[e] = inside ? a.dL_dpixels[0 * HW + pix_id] : 0.f;
-            dp1[e] = inside ? a.dL_dpixels[1 * HW + pix_id] : 0.f;
-            dp2[e] = inside ? a.dL_dpixels[2 * HW + pix_id] : 0.f;
-            dinv[e] = (inside && HAS_INV) ? a.dL_invdepths[pix_id] : 0.f;
-            R[e] = (acc.x + Tf * a.bg[0]) * dp0[e] + (acc.y + Tf * a.bg[1]) * dp1[e] +
-                   (acc.z + Tf * a.bg[2]) * dp2[e] + acc.w * dinv[e];
-            qmax[2 * h + e] = __builtin_amdgcn_readfirstlane(wave_max_u32(lc[e]));
-        }
         BwdPair& s = st[h];
         s.T = (v2f)(1.f);
-        s.R = {R[0], R[1]};
+        s.R = {R[2 * h], R[2 * h + 1]};
         s.Fd = (v2f)(0.f);
-        s.dp0 = {dp0[0], dp0[1]};
-        s.dp1 = {dp1[0], dp1[1]};
-        s.dp2 = {dp2[0], dp2[1]};
-        s.dinv = {dinv[0], dinv[1]};
-        s.lc0 = lc[0];
-        s.lc1 = lc[1];
+        s.dp0 = {dp0[2 * h], dp0[2 * h + 1]};
+        s.dp1 = {dp1[2 * h], dp1[2 * h + 1]};
+        s.dp2 = {dp2[2 * h], dp2[2 * h + 1]};
+        s.dinv = {dinv[2 * h], dinv[2 * h + 1]};
+        s.lc0 = lc[2 * h];
+        s.lc1 = lc[2 * h + 1];
     }
     const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
 
@@ -481,17 +509,25 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     // Entries that contribute to no pixel (list positions >= tmax, or culled for every quadrant)
     // get no record: valid[slot] stays 0 and preprocess_bwd skips them.
 
+    // list ids and slots are fetched one batch ahead; record loads are unconditional (clamped)
+    const int last = (int)tmax - 1;
+    uint32_t next_id = 0, next_slot = 0;
+    if (tmax > 0) {
+        next_id = a.point_list[range.x + min(lane, last)];
+        next_slot = a.slot[range.x + min(lane, last)];
+    }
     for (int p0 = 0; p0 < (int)tmax; p0 += 64) {
         const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
-        uint32_t m = 0, myslot = 0;
+        const uint32_t id = next_id, myslot = next_slot;
+        next_id = a.point_list[range.x + min(pos_l + 64, last)];
+        next_slot = a.slot[range.x + min(pos_l + 64, last)];
+        const float4* r = a.splat + 3 * (size_t)id;
+        const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+        s_rec[0][lane] = r0;
+        s_rec[1][lane] = r1;
+        s_rec[2][lane] = r2;
+        uint32_t m = 0;
         if (pos_l < (int)tmax) {
-            const uint32_t id = a.point_list[range.x + pos_l];
-            myslot = a.slot[range.x + pos_l];
-            const float4* r = a.splat + 3 * (size_t)id;
-            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            s_rec[0][lane] = r0;
-            s_rec[1][lane] = r1;
-            s_rec[2][lane] = r2;
             m = quad_mask(r0, r1, tx, ty);
             m &= (uint32_t)((uint32_t)pos_l < qmax[0]) | ((uint32_t)((uint32_t)pos_l < qmax[1]) << 1) |
                  ((uint32_t)((uint32_t)pos_l < qmax[2]) << 2) | ((uint32_t)((uint32_t)pos_l < qmax[3]) << 3);
@@ -566,7 +602,8 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
 hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
+    if (ranges) hipLaunchKernelGGL(tile_order_kernel<true>, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
+    else hipLaunchKernelGGL(tile_order_kernel<false>, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
     return hipGetLastError();
 }
 

@@ -152,6 +152,20 @@ def test_1080p_view_properties():
         assert ok_, f"grad {hk} rel err {rel:.3e}"
 
 
+def test_uhd_view_multi_pass_tile_order():
+    """3840x2176 (32,640 tiles): the longest-first tile order runs in two 16K-tile passes;
+    every tile must still be rendered exactly once, forward and backward."""
+    case = common.make_case(P=20000, H=2176, W=3840)
+    o, og = common.run_oracle(case, nthreads=8)
+    color, radii, inv, g = run_hip(case)
+    np.testing.assert_array_equal(radii, o.radii)
+    _check_image(color, o.color, "color")
+    _check_image(inv, o.invdepth, "invdepth")
+    for hk, ok in {"means3D": "dL_dmeans3D", "opacities": "dL_dopacity", "means2D": "dL_dmean2D"}.items():
+        ok_, rel = common.allclose_rel(g[hk], og[ok].reshape(g[hk].shape), rtol=5e-4)
+        assert ok_, f"grad {hk} rel err {rel:.3e}"
+
+
 def test_mark_visible():
     import oracle
     dgr = _dgr()
