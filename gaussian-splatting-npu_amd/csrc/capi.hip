@@ -231,7 +231,6 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     a.radii = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
     a.means2D = at<float>(gb, g.off[GEOM_MEANS2D]);
     a.depths = at<float>(gb, g.off[GEOM_DEPTH]);
-    a.cov3D_out = at<float>(gb, g.off[GEOM_COV3D]);
     a.rgb = at<float>(gb, g.off[GEOM_RGB]);
     a.conic_opacity = at<float>(gb, g.off[GEOM_CONIC_OPACITY]);
     a.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
@@ -241,6 +240,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     a.scan_status_words = scan_status_words(P);
     a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     a.dkey = at<uint32_t>(gb, g.off[GEOM_DKEY]);
+    a.rect = at<uint2>(gb, g.off[GEOM_RECT]);
     {
         ProfScope ps_(PK_PREPROCESS, s);
         HIP_TRY(launch_preprocess(a, s));
@@ -257,10 +257,10 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
         uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + 2 * q);
         uint32_t* v1 = reinterpret_cast<uint32_t*>(tmp + 3 * q);
         ProfScope ps_(PK_DEPTH_SORT, s);
-        // the last pass also lays tiles_touched out in depth order (into point_offsets, which
-        // the scan then turns into offsets in place)
+        // the last pass also lays the tile rects and tile counts out in depth order (the counts
+        // into point_offsets, which the scan then turns into offsets in place)
         HIP_TRY(radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
-                           gb + g.off[GEOM_RADIX_SCRATCH], s, a.tiles_touched,
+                           gb + g.off[GEOM_RADIX_SCRATCH], s, a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
                            at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])));
     }
     DEBUG_SYNC(s);
@@ -301,7 +301,6 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     const int T = (int)(gx * gy);
-    const int* rad = radii ? radii : at<int>(gb, g.off[GEOM_RADII]);
     uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     uint32_t* sorted_tiles = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr;
     uint32_t* slot = L > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
@@ -320,8 +319,9 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
         {
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
-                                          at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), at<float2>(gb, g.off[GEOM_MEANS2D]),
-                                          rad, gx, gy, tile_keys, gids, emit_start, at<uint8_t>(bb, b.off[BIN_VALID]),
+                                          at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
+                                          at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx, tile_keys, gids, emit_start,
+                                          at<uint8_t>(bb, b.off[BIN_VALID]),
                                           at<uint2>(ib, im.off[IMG_RANGES]), T, s));
         }
         DEBUG_SYNC(s);
@@ -455,7 +455,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.means3D = means3D; p.radii = rad; p.shs = shs;
     p.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
     p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
-    p.cov3Ds = cov3D_precomp ? cov3D_precomp : at<float>(gb, g.off[GEOM_COV3D]);
+    p.cov3D_precomp = cov3D_precomp;
     p.view = viewmatrix; p.proj = projmatrix;
     p.focal_y = height / (2.0f * tan_fovy);
     p.focal_x = width / (2.0f * tan_fovx);

@@ -127,6 +127,28 @@ __device__ __forceinline__ void getRect(float px, float py, int max_radius, uint
     rmaxy = (uint32_t)a < gy ? (uint32_t)a : gy;
 }
 
+// forward.cu:114-151 (also the backward's recomputation: bit-identical under -ffp-contract=off)
+__device__ __forceinline__ void computeCov3D(const float* scale, float mod, const float4 rot, float* cov3D)
+{
+    mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+    S.m[0][0] = mod * scale[0];
+    S.m[1][1] = mod * scale[1];
+    S.m[2][2] = mod * scale[2];
+    const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
+    mat3 R = mat3_cols(
+        1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+        2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+        2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    mat3 M = mat3_mul(S, R);
+    mat3 Sigma = mat3_mul(mat3_T(M), M);
+    cov3D[0] = Sigma.m[0][0];
+    cov3D[1] = Sigma.m[0][1];
+    cov3D[2] = Sigma.m[0][2];
+    cov3D[3] = Sigma.m[1][1];
+    cov3D[4] = Sigma.m[1][2];
+    cov3D[5] = Sigma.m[2][2];
+}
+
 // ----------------------------------------------------------------------------
 // State-buffer layouts (the reference's GeometryState / ImageState /
 // BinningState, rasterizer_impl.h:29-65, re-laid out for this implementation).
@@ -143,12 +165,13 @@ enum GeomArray {
     GEOM_RGB,             // f32[3P]
     GEOM_TILES_TOUCHED,   // u32[P]
     GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched in depth order
-    GEOM_COV3D,           // f32[6P]
     GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {ka, kb, kc, opacity} {r, g, b, 1/depth}
                           // (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic; cullK scaled by log2(e)/2
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
     GEOM_EMIT_START,      // u32[P] first emission slot of each Gaussian
+    GEOM_RECT,            // u16x4[P] tile rect {x0, y0, x1, y1} (getRect), zero if culled
+    GEOM_SORTED_RECT,     // u16x4[P] the rects in depth order (last depth-sort pass)
     GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
     GEOM_SCAN_SCRATCH,    // u64[scan chunks + 1] look-back status words + chunk ticket (zeroed by preprocess)
@@ -188,8 +211,8 @@ size_t radix_status_bytes(int n, int npass);
 inline GeomLayout geom_layout(int P)
 {
     size_t p = (size_t)(P > 0 ? P : 0);
-    size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 24 * p, 48 * p,
-                                4 * p, 4 * p, 4 * p, 16 * p + 1024, radix_status_bytes(P, 4),
+    size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 48 * p,
+                                4 * p, 4 * p, 4 * p, 8 * p, 8 * p, 16 * p + 1024, radix_status_bytes(P, 4),
                                 8 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
     GeomLayout l;
     size_t o = 0;

@@ -25,7 +25,6 @@ struct PreprocessArgs {
     int* radii;
     float* means2D;
     float* depths;
-    float* cov3D_out;
     float* rgb;
     float* conic_opacity;
     uint8_t* clamped;
@@ -35,6 +34,7 @@ struct PreprocessArgs {
     int scan_status_words;
     float4* splat;  // 3 x float4 per Gaussian (GEOM_SPLAT)
     uint32_t* dkey; // depth-sort key per Gaussian
+    uint2* rect;    // {x0 | y0 << 16, x1 | y1 << 16} per Gaussian (zero if culled)
 };
 
 struct RenderFwdArgs {
@@ -92,7 +92,7 @@ struct PreprocessBwdArgs {
     const float* scales;
     const float* rotations;
     float scale_modifier;
-    const float* cov3Ds;
+    const float* cov3D_precomp;  // null: cov3D is recomputed from scales/rotations
     const float* view;
     const float* proj;
     float focal_x, focal_y, tan_fovx, tan_fovy;
@@ -131,11 +131,11 @@ hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uin
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
-                      char* scratch, hipStream_t s, const uint32_t* gather_tab = nullptr,
-                      uint32_t* gather_out = nullptr);
+                      char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
+                      uint32_t* sorted_counts = nullptr);
 // Also clears valid[slot] (the backward's record flags) and ranges[0..T) for tile_ranges.
-hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
-                                 const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
+hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
+                                 uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
                                  uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s);
 // ranges must be zero on entry unless L == 0 (emit_instances clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);

@@ -7,33 +7,12 @@
 // bit-identical to oracle/gsr_oracle.c (depth bits, radii, rect, tile counts).
 // One thread per Gaussian, 256-thread blocks (4 wave64s).  HBM-bound: the
 // per-Gaussian input is 236 B at SH degree 3 (means 12, scales 12, rot 16,
-// opacity 4, SH 192); output record 44 B (+24 B cov3D).
+// opacity 4, SH 192); output record 44 B.
 #include "gsr_common.h"
 #include "gsr_kernels.h"
 
 namespace gsr {
 
-// forward.cu:114-151
-__device__ __forceinline__ void computeCov3D(const float* scale, float mod, const float4 rot, float* cov3D)
-{
-    mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
-    S.m[0][0] = mod * scale[0];
-    S.m[1][1] = mod * scale[1];
-    S.m[2][2] = mod * scale[2];
-    const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
-    mat3 R = mat3_cols(
-        1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
-        2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
-        2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
-    mat3 M = mat3_mul(S, R);
-    mat3 Sigma = mat3_mul(mat3_T(M), M);
-    cov3D[0] = Sigma.m[0][0];
-    cov3D[1] = Sigma.m[0][1];
-    cov3D[2] = Sigma.m[0][2];
-    cov3D[3] = Sigma.m[1][1];
-    cov3D[4] = Sigma.m[1][2];
-    cov3D[5] = Sigma.m[2][2];
-}
 
 // forward.cu:74-109
 __device__ __forceinline__ f3 computeCov2D(const f3 mean, float focal_x, float focal_y, float tan_fovx,
@@ -110,6 +89,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
 
     a.radii[idx] = 0;
     a.tiles_touched[idx] = 0;
+    a.rect[idx] = make_uint2(0u, 0u);
     a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
 
     // Issue every per-Gaussian load up front (one memory round trip instead of one per phase).
@@ -138,9 +118,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     if (a.cov3D_precomp) {
         cov3D = a.cov3D_precomp + (size_t)idx * 6;
     } else {
-        computeCov3D(scl, a.scale_modifier, rot, cov3D_local);
-#pragma unroll
-        for (int i = 0; i < 6; i++) a.cov3D_out[(size_t)idx * 6 + i] = cov3D_local[i];
+        computeCov3D(scl, a.scale_modifier, rot, cov3D_local);  // recomputed by preprocess_bwd, not stored
         cov3D = cov3D_local;
     }
 
@@ -186,6 +164,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     const float opacity = opacity_in * h_convolution_scaling;
     reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
+    a.rect[idx] = make_uint2(rminx | (rminy << 16), rmaxx | (rmaxy << 16));
 
     // Render record.  cullK bounds the ellipse d^T Q d <= K = 2 ln(255 opacity) outside which
     // alpha = opacity * exp(power) < 1/255 (Q = the fp32 conic the render kernels evaluate),

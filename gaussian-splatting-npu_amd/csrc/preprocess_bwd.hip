@@ -33,8 +33,10 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
     const size_t i = (size_t)idx;
     in.visible = a.radii[idx] > 0;
     in.co = a.conic_opacity[idx];
+    if (a.cov3D_precomp) {  // uniform over the launch
 #pragma unroll
-    for (int k = 0; k < 6; k++) in.cov[k] = a.cov3Ds[6 * i + k];
+        for (int k = 0; k < 6; k++) in.cov[k] = a.cov3D_precomp[6 * i + k];
+    }
     in.mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
     in.opacity = a.opacities[idx];
     in.clamped = a.clamped[idx];
@@ -125,7 +127,13 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
 
     // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
+    float cov_local[6];
     const float* cov3D = in.cov;
+    if (!a.cov3D_precomp) {  // forward.cu:114-151 recomputed (bit-identical to the forward's)
+        const float scl[3] = {in.scale.x, in.scale.y, in.scale.z};
+        computeCov3D(scl, a.scale_modifier, in.rot, cov_local);
+        cov3D = cov_local;
+    }
     const f3 mean = in.mean;
     const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
     const float* view = a.view;

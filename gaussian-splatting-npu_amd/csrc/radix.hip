@@ -99,8 +99,11 @@ struct SortPassArgs {
     uint32_t* out_x;
     uint32_t* out_y;
     uint32_t* sorted_keys;
-    const uint32_t* gather_tab;  // final pass, single payload: gather_out[dst] = gather_tab[v] (may be null)
-    uint32_t* gather_out;
+    // final pass, single payload (the depth sort): sorted_rects[dst] = rects[v] and
+    // sorted_counts[dst] = its tile count (may be null)
+    const uint2* rects;
+    uint2* sorted_rects;
+    uint32_t* sorted_counts;
     const uint32_t* row_prefix;  // (nbins, nchunks) exclusive row scans
     const uint32_t* totals;      // (nbins) digit totals
 };
@@ -221,7 +224,11 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
                     if (a.out_y) a.out_y[dst] = v.y;
                 } else {
                     if (a.out_x) a.out_x[dst] = v;
-                    if (a.gather_tab) a.gather_out[dst] = a.gather_tab[v];
+                    if (a.rects) {
+                        const uint2 rc = a.rects[v];
+                        a.sorted_rects[dst] = rc;
+                        a.sorted_counts[dst] = ((rc.y & 0xFFFFu) - (rc.x & 0xFFFFu)) * ((rc.y >> 16) - (rc.x >> 16));
+                    }
                 }
                 if (a.sorted_keys) a.sorted_keys[dst] = k;
             }
@@ -231,13 +238,13 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 
 // Emission in depth order: instance slots [off(k-1), off(k)) of depth rank k belong to
 // Gaussian g = sorted_ids[k]; tiles y-major then x inside its rect (rasterizer_impl.cu:98-109).
-// One wave per 64 consecutive ranks: the lanes first publish their rects in LDS, then the wave
-// fills its whole slot range 64 consecutive slots at a time (coalesced stores), each lane
-// finding the owner of its slot by a binary search over the 64 rect starts.
+// One wave per 64 consecutive ranks: the lanes first publish their rects (read in depth order:
+// the depth sort laid them out, no gathers by Gaussian id) in LDS, then the wave fills its whole
+// slot range 64 consecutive slots at a time (coalesced stores), each lane finding the owner of
+// its slot by a binary search over the 64 rect starts.
 __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
-                                                             const uint32_t* offsets_d, const float2* means2D,
-                                                             const int* radii, uint32_t gx, uint32_t gy,
-                                                             uint32_t* tile_keys, uint32_t* gids,
+                                                             const uint32_t* offsets_d, const uint2* sorted_rects,
+                                                             uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
                                                              uint32_t* emit_start, uint8_t* valid, uint2* ranges,
                                                              int T)
 {
@@ -248,20 +255,18 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
     for (int t = blockIdx.x * 256 + (int)threadIdx.x; t < T; t += gridDim.x * 256) ranges[t] = make_uint2(0u, 0u);
     if (k0 >= P) return;  // whole wave out of range (waves are independent: no block barriers)
     const int k = k0 + lane;
-    uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1, g = 0;
+    const int kc = min(k, P - 1);
+    const uint32_t g = sorted_ids[kc];
+    const uint32_t prev = offsets_d[max(kc - 1, 0)];
+    const uint2 rc = sorted_rects[kc];
+    const uint32_t wend = offsets_d[min(k0 + 63, P - 1)];
+    uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1;
     if (k < P) {
-        g = sorted_ids[k];
-        start = k == 0 ? 0u : offsets_d[k - 1];
+        start = k == 0 ? 0u : prev;
         emit_start[g] = start;
-        const int r = radii[g];
-        if (r > 0) {
-            const float2 xy = means2D[g];
-            uint32_t rminx, rminy, rmaxx, rmaxy;
-            getRect(xy.x, xy.y, r, gx, gy, rminx, rminy, rmaxx, rmaxy);
-            x0 = rminx;
-            y0 = rminy;
-            wd = max(rmaxx - rminx, 1u);
-        }
+        x0 = rc.x & 0xFFFFu;
+        y0 = rc.x >> 16;
+        wd = max((rc.y & 0xFFFFu) - x0, 1u);
     }
     s_start[w][lane] = start;
     s_x0[w][lane] = x0;
@@ -269,7 +274,6 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
     s_w[w][lane] = wd;
     s_g[w][lane] = g;
     const uint32_t wbeg = (uint32_t)__shfl((int)start, 0, 64);
-    const uint32_t wend = offsets_d[min(k0 + 63, P - 1)];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -329,11 +333,11 @@ size_t radix_status_bytes(int n, int npass)
 // Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, and
 // with `gids` also gids[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
 // gids); the last pass writes out_x[dst] = i, out_y[dst] = gids[i] and sorted_keys[dst] = key
-// (any of them may be null); without gids it can also write gather_out[dst] = gather_tab[i].
-// All writes are contiguous runs: no scattered stores.
+// (any of them may be null); without gids it can also lay out rects[i] and their tile counts
+// in sorted order.  All writes are contiguous runs: no scattered stores.
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
-                      char* scratch, hipStream_t s, const uint32_t* gather_tab, uint32_t* gather_out)
+                      char* scratch, hipStream_t s, const uint2* rects, uint2* sorted_rects, uint32_t* sorted_counts)
 {
     if (n <= 0) return hipSuccess;
     const int nchunks = (int)rs_chunks(n);
@@ -368,8 +372,9 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
         a.out_x = out_x;
         a.out_y = out_y;
         a.sorted_keys = sorted_keys;
-        a.gather_tab = (last && !gids) ? gather_tab : nullptr;
-        a.gather_out = gather_out;
+        a.rects = (last && !gids) ? rects : nullptr;
+        a.sorted_rects = sorted_rects;
+        a.sorted_counts = sorted_counts;
         a.row_prefix = counts;
         a.totals = totals;
         const dim3 g((unsigned)nchunks), b(RS_THREADS);
@@ -387,13 +392,13 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
     return hipGetLastError();
 }
 
-hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const float2* means2D,
-                                 const int* radii, uint32_t gx, uint32_t gy, uint32_t* tile_keys, uint32_t* gids,
+hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
+                                 uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
                                  uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       means2D, radii, gx, gy, tile_keys, gids, emit_start, valid, ranges, T);
+                       sorted_rects, gx, tile_keys, gids, emit_start, valid, ranges, T);
     return hipGetLastError();
 }
 
