@@ -391,7 +391,8 @@ struct BwdPair {
 // GradField): with u = G * dL/dalpha the record holds sum u (opacity), sum u*dx and sum u*dy
 // (mean2D: (a Sx + b Sy, b Sx + c Sy) times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy,
 // u*dy*dy (conic, times -opacity/2).
-template <bool HAS_INV>
+// FIRST: o[] is assigned, not accumulated (the entry's first half: no zero-initialisation).
+template <bool HAS_INV, bool FIRST>
 __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_t pos, const float4 xy,
                                          const Falloff f, const float4 co, const float4 col, v2f* o)
 {
@@ -414,18 +415,31 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
     s.Fd = fma2(aT, cd, s.Fd);
     const v2f dL = fma2(s.T, cd, -(s.R - s.Fd) * r_om);
     s.T = s.T * one_m;
-    o[GF_COLOR_R] = fma2(aT, s.dp0, o[GF_COLOR_R]);
-    o[GF_COLOR_G] = fma2(aT, s.dp1, o[GF_COLOR_G]);
-    o[GF_COLOR_B] = fma2(aT, s.dp2, o[GF_COLOR_B]);
-    if constexpr (HAS_INV) o[GF_INVDEPTH] = fma2(aT, s.dinv, o[GF_INVDEPTH]);
     const v2f u = Gc * dL;
     const v2f ux = u * dx, uy = u * dy;
-    o[GF_OPACITY] += u;
-    o[GF_MEAN2D_X] += ux;  // sum u dx, sum u dy: the conic (a, b, c) is applied per Gaussian
-    o[GF_MEAN2D_Y] += uy;
-    o[GF_CONIC_A] = fma2(ux, dx, o[GF_CONIC_A]);
-    o[GF_CONIC_B] = fma2(ux, (v2f)(dy), o[GF_CONIC_B]);
-    o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
+    if constexpr (FIRST) {
+        o[GF_COLOR_R] = aT * s.dp0;
+        o[GF_COLOR_G] = aT * s.dp1;
+        o[GF_COLOR_B] = aT * s.dp2;
+        o[GF_INVDEPTH] = HAS_INV ? aT * s.dinv : (v2f)(0.f);
+        o[GF_OPACITY] = u;
+        o[GF_MEAN2D_X] = ux;  // sum u dx, sum u dy: the conic (a, b, c) is applied per Gaussian
+        o[GF_MEAN2D_Y] = uy;
+        o[GF_CONIC_A] = ux * dx;
+        o[GF_CONIC_B] = ux * dy;
+        o[GF_CONIC_C] = uy * dy;
+    } else {
+        o[GF_COLOR_R] = fma2(aT, s.dp0, o[GF_COLOR_R]);
+        o[GF_COLOR_G] = fma2(aT, s.dp1, o[GF_COLOR_G]);
+        o[GF_COLOR_B] = fma2(aT, s.dp2, o[GF_COLOR_B]);
+        if constexpr (HAS_INV) o[GF_INVDEPTH] = fma2(aT, s.dinv, o[GF_INVDEPTH]);
+        o[GF_OPACITY] += u;
+        o[GF_MEAN2D_X] += ux;
+        o[GF_MEAN2D_Y] += uy;
+        o[GF_CONIC_A] = fma2(ux, dx, o[GF_CONIC_A]);
+        o[GF_CONIC_B] = fma2(ux, (v2f)(dy), o[GF_CONIC_B]);
+        o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
+    }
 }
 
 // Backward: ONE wave per 16x16 tile, each lane owning 4 pixels as two packed pairs (upper half:
@@ -567,10 +581,16 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
                     const uint32_t pos = (uint32_t)(p0 + j);
                     const Falloff f = falloff(co);
                     v2f o[GF_NUM];
-#pragma unroll
-                    for (int q = 0; q < GF_NUM; q++) o[q] = (v2f)(0.f);
-                    if (mj & 3u) bwd_pair<HAS_INV>(st[0], pfx, py0, pos, xy, f, co, col, o);
-                    if (mj & 12u) bwd_pair<HAS_INV>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
+                    // both halves in one straight-line block (two independent dependency chains
+                    // for the scheduler to interleave), or the one the entry reaches
+                    if ((mj & 3u) && (mj & 12u)) {
+                        bwd_pair<HAS_INV, true>(st[0], pfx, py0, pos, xy, f, co, col, o);
+                        bwd_pair<HAS_INV, false>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
+                    } else if (mj & 3u) {
+                        bwd_pair<HAS_INV, true>(st[0], pfx, py0, pos, xy, f, co, col, o);
+                    } else {
+                        bwd_pair<HAS_INV, true>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
+                    }
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
                     if (jj + 1 < G) {
