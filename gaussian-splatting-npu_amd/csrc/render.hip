@@ -50,7 +50,8 @@ __device__ __forceinline__ float box_min_quadform(float a, float b, float c, flo
                                                   float dy1)
 {
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return 0.f;
-    const float ia = 1.0f / a, ic = 1.0f / c;
+    // v_rcp_f32 (1 ulp): the test is conservative by the cullK margin, far above that
+    const float ia = __builtin_amdgcn_rcpf(a), ic = __builtin_amdgcn_rcpf(c);
     float m = 3.0e38f;
     {  // vertical edges dx = dx0, dx1
         float dy = fminf(fmaxf(-b * dx0 * ic, dy0), dy1);
