@@ -270,17 +270,18 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
             const int jr = r * 64 + lane;
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
-            int j = r * 64 + (int)__builtin_ctzll(rem);
-            rem &= rem - 1;
-            float4 xy = s_rec[j], co = s_rec[BATCH + j], col = s_rec[2 * BATCH + j];
-            while (true) {
-                const int jn = rem ? r * 64 + (int)__builtin_ctzll(rem) : j;
-                const float4 nxy = s_rec[jn], nco = s_rec[BATCH + jn], ncol = s_rec[2 * BATCH + jn];
+            // two entries per iteration with ping-pong record registers (no rotation copies)
+            auto take = [&]() -> int {
+                const int jj = rem ? r * 64 + (int)__builtin_ctzll(rem) : -1;
+                rem &= rem - 1;
+                return jj;
+            };
+            auto blend = [&](int j, const float4 xy, const float4 co, const float4 col) {
                 const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
                 const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
                 bool contrib = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 const float test_T = T * (1 - alpha);
-                if (contrib && test_T < 0.0001f) {
+                if (contrib && test_T < 0.0001f) {  // forward.cu:366-370
                     done = true;
                     contrib = false;
                 }
@@ -292,12 +293,22 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
                     T = test_T;
                     last_contributor = (uint32_t)(base + j + 1);
                 }
-                if (rem == 0 || __all(done)) break;
-                j = jn;
-                rem &= rem - 1;
-                xy = nxy;
-                co = nco;
-                col = ncol;
+            };
+            int j = take();
+            float4 axy = s_rec[j], aco = s_rec[BATCH + j], acol = s_rec[2 * BATCH + j];
+            while (true) {
+                const int jb = take();
+                const int lb = jb >= 0 ? jb : j;
+                const float4 bxy = s_rec[lb], bco = s_rec[BATCH + lb], bcol = s_rec[2 * BATCH + lb];
+                blend(j, axy, aco, acol);
+                if (jb < 0 || __all(done)) break;
+                j = take();
+                const int la = j >= 0 ? j : jb;
+                axy = s_rec[la];
+                aco = s_rec[BATCH + la];
+                acol = s_rec[2 * BATCH + la];
+                blend(jb, bxy, bco, bcol);
+                if (j < 0 || __all(done)) break;
             }
         }
     }
