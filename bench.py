@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--no-aux", action="store_true", help="skip the §8f side measurements (distCUDA2)")
     return ap.parse_args()
 
 
@@ -181,6 +182,10 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(args, scene, cams[0], grads[0])
 
+    aux = None
+    if not args.no_aux and world == 1:
+        aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args)}
+
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
         "value": round(value, 2),
@@ -200,10 +205,43 @@ def main():
                    "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "aux": aux,
     }
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def aux_knn(points, args, reps=5):
+    """simple_knn.distCUDA2 on the scene's P means: mean time per call
+    (it synchronises once inside, to size its grid), plus the brute-force C oracle on a
+    bounded sample as the CPU baseline."""
+    from simple_knn._C import distCUDA2
+    for _ in range(2):
+        distCUDA2(points)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        distCUDA2(points)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / reps * 1e3
+    P = points.shape[0]
+    out = {"points": P, "ms": round(ms, 3), "Mpoints_per_s": round(P / ms / 1e3, 1), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            n = 20000
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            sample = points[:n].cpu().numpy()
+            t = time.perf_counter()
+            oracle.knn_dist2(sample, nthreads=threads)
+            dt = time.perf_counter() - t
+            out["cpu_baseline"] = {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads,
+                                   "kind": "port", "sample": f"brute-force oracle on the first {n} points"}
+        except Exception as e:
+            out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
+    return out
 
 
 def cpu_baseline(args, scene, s, grad):

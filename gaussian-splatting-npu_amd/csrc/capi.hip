@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "gsr.h"
+#include "simple_knn.h"
 #include "gsr_common.h"
 #include "gsr_kernels.h"
 
@@ -478,6 +479,21 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         HIP_TRY(launch_preprocess_bwd(p, s));
     }
     DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+// ---- simple_knn.h ----
+size_t gsr_knn_workspace_size(int P) { return knn_workspace_bytes(P); }
+
+int gsr_knn_dist2(int P, const float* points, float* dist2_out, void* workspace, void* stream)
+{
+    if (P < 0) return fail(GSR_ERR_INVALID, "P must be >= 0");
+    if (P == 0) return GSR_OK;
+    if (!points || !dist2_out || !workspace) return fail(GSR_ERR_INVALID, "null pointer");
+    uint32_t* h;
+    int rc = pinned(&h);
+    if (rc) return rc;
+    HIP_TRY(knn_dist2(P, points, dist2_out, static_cast<char*>(workspace), h + 8, (hipStream_t)stream));
     return GSR_OK;
 }
 

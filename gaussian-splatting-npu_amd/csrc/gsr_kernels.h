@@ -149,4 +149,8 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 
+// distCUDA2 (knn.hip); host_bounds: 6 words of pinned host memory
+size_t knn_workspace_bytes(int P);
+hipError_t knn_dist2(int P, const float* pts, float* dist2, char* workspace, uint32_t* host_bounds, hipStream_t s);
+
 }  // namespace gsr

@@ -140,5 +140,15 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     return out.astype(bool)
 
 
+def knn_dist2(points, nthreads=8):
+    """simple-knn distCUDA2 restated (knn_oracle.c): mean squared distance to the 3 nearest others."""
+    p = _np(points).reshape(-1, 3)
+    out = np.zeros((p.shape[0],), np.float32)
+    if p.shape[0]:
+        lib().gsr_oracle_knn_dist2(ctypes.c_int(p.shape[0]), _p(p), out.ctypes.data_as(ctypes.c_void_p),
+                                   ctypes.c_int(nthreads))
+    return out
+
+
 def higher_msb(n):
     return int(lib().gsr_oracle_higher_msb(ctypes.c_uint32(n)))

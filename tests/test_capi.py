@@ -15,12 +15,12 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "gsr.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "simple_knn.h")]
 LIB = os.path.join(ROOT, "gaussian-splatting-npu_amd", "diff_gaussian_rasterization", "libgsr_hip.so")
 
 
 def _declared():
-    text = open(HEADER).read()
+    text = "\n".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     text = re.sub(r"//[^\n]*", "", text)
     names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(gsr_[a-z_0-9]+)\s*\(", text, flags=re.M)
@@ -42,13 +42,13 @@ def lib():
 def test_header_declares_the_boundary():
     names = _declared()
     for must in ["gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_last_error", "gsr_geometry_buffer_size",
-                 "gsr_image_buffer_size", "gsr_binning_buffer_size"]:
+                 "gsr_image_buffer_size", "gsr_binning_buffer_size", "gsr_knn_dist2", "gsr_knn_workspace_size"]:
         assert must in names, must
 
 
 def test_library_exports_every_declared_symbol(lib):
     missing = [n for n in _declared() if not hasattr(lib, n)]
-    assert not missing, f"declared in include/gsr.h but not exported: {missing}"
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
 
 
 def test_version_and_error_string(lib):
