@@ -11,6 +11,7 @@
 
 #include "gsr.h"
 #include "simple_knn.h"
+#include "fused_ssim.h"
 #include "gsr_common.h"
 #include "gsr_kernels.h"
 
@@ -479,6 +480,34 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         HIP_TRY(launch_preprocess_bwd(p, s));
     }
     DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+// ---- fused_ssim.h ----
+int gsr_ssim_forward(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                     float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, void* stream)
+{
+    if (planes < 0 || H < 0 || W < 0) return fail(GSR_ERR_INVALID, "negative image size");
+    if ((size_t)planes * H * W == 0) return GSR_OK;
+    if (!img1 || !img2 || !ssim_map) return fail(GSR_ERR_INVALID, "null pointer");
+    const bool train = dm_dmu1 && dm_dsigma1_sq && dm_dsigma12;
+    HIP_TRY(launch_ssim_fwd(planes, H, W, C1, C2, img1, img2, ssim_map, train ? dm_dmu1 : nullptr,
+                            train ? dm_dsigma1_sq : nullptr, train ? dm_dsigma12 : nullptr, (hipStream_t)stream));
+    return GSR_OK;
+}
+
+int gsr_ssim_backward(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                      const float* dL_dmap, const float* dm_dmu1, const float* dm_dsigma1_sq,
+                      const float* dm_dsigma12, float* dL_dimg1, void* stream)
+{
+    (void)C1;
+    (void)C2;  // folded into the forward's partial derivatives
+    if (planes < 0 || H < 0 || W < 0) return fail(GSR_ERR_INVALID, "negative image size");
+    if ((size_t)planes * H * W == 0) return GSR_OK;
+    if (!img1 || !img2 || !dL_dmap || !dm_dmu1 || !dm_dsigma1_sq || !dm_dsigma12 || !dL_dimg1)
+        return fail(GSR_ERR_INVALID, "null pointer");
+    HIP_TRY(launch_ssim_bwd(planes, H, W, img1, img2, dL_dmap, dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1,
+                            (hipStream_t)stream));
     return GSR_OK;
 }
 

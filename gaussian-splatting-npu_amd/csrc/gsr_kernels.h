@@ -149,6 +149,12 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 
+// fused SSIM (ssim.hip); dA/dB/dC null: map only
+hipError_t launch_ssim_fwd(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,
+                           float* map, float* dA, float* dB, float* dC, hipStream_t s);
+hipError_t launch_ssim_bwd(int planes, int H, int W, const float* img1, const float* img2, const float* dmap,
+                           const float* dA, const float* dB, const float* dC, float* dimg1, hipStream_t s);
+
 // distCUDA2 (knn.hip); host_bounds: 6 words of pinned host memory
 size_t knn_workspace_bytes(int P);
 hipError_t knn_dist2(int P, const float* pts, float* dist2, char* workspace, uint32_t* host_bounds, hipStream_t s);

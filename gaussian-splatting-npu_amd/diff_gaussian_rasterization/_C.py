@@ -240,3 +240,16 @@ def sorted_keys(geomBuffer, binningBuffer, imgBuffer, P, L, W, H):
                                      imgBuffer.data_ptr(), P, L, W, H, keys.data_ptr() if L else None,
                                      vals.data_ptr() if L else None, ranges.data_ptr(), _stream(dev)))
     return keys, vals, ranges
+
+
+def fusedssim(C1, C2, img1, img2):
+    """The dr_aa extension's SSIM-map op that utils/loss_utils.py:17-30 imports: ssim_map."""
+    import fused_ssim
+    return fused_ssim.fusedssim(C1, C2, img1, img2, train=False)[0]
+
+
+def fusedssim_backward(C1, C2, img1, img2, opt_grad):
+    """dL/dimg1 of the SSIM map for upstream opt_grad (utils/loss_utils.py:32-37)."""
+    import fused_ssim
+    _, a, b, c = fused_ssim.fusedssim(C1, C2, img1, img2, train=True)
+    return fused_ssim.fusedssim_backward(C1, C2, img1, img2, opt_grad, a, b, c)

@@ -15,7 +15,7 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "simple_knn.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("gsr.h", "simple_knn.h", "fused_ssim.h")]
 LIB = os.path.join(ROOT, "gaussian-splatting-npu_amd", "diff_gaussian_rasterization", "libgsr_hip.so")
 
 
@@ -42,7 +42,8 @@ def lib():
 def test_header_declares_the_boundary():
     names = _declared()
     for must in ["gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_last_error", "gsr_geometry_buffer_size",
-                 "gsr_image_buffer_size", "gsr_binning_buffer_size", "gsr_knn_dist2", "gsr_knn_workspace_size"]:
+                 "gsr_image_buffer_size", "gsr_binning_buffer_size", "gsr_knn_dist2", "gsr_knn_workspace_size", "gsr_ssim_forward",
+                 "gsr_ssim_backward"]:
         assert must in names, must
 
 
