@@ -184,7 +184,7 @@ def main():
 
     aux = None
     if not args.no_aux and world == 1:
-        aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args)}
+        aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args), "fused_ssim": aux_ssim(H, W, dev, args)}
 
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
@@ -239,6 +239,50 @@ def aux_knn(points, args, reps=5):
             dt = time.perf_counter() - t
             out["cpu_baseline"] = {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads,
                                    "kind": "port", "sample": f"brute-force oracle on the first {n} points"}
+        except Exception as e:
+            out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
+    return out
+
+
+def aux_ssim(H, W, dev, args, reps=20):
+    """fused_ssim on one (1, 3, H, W) image pair: forward (map + partials) and
+    backward, timed with events on the current stream; HBM-bound, so priced in algorithmic bytes
+    (forward: 2 images in, map + 3 partial planes out; backward: 2 images + dL/dmap + 3 partial
+    planes in, dL/dimg1 out: 13 planes of 4 B per pixel and channel)."""
+    from fused_ssim import fusedssim, fusedssim_backward
+    g = torch.Generator(device=dev).manual_seed(0)
+    a = torch.rand((1, 3, H, W), device=dev, generator=g)
+    b = (a + 0.1 * torch.randn(a.shape, device=dev, generator=g)).clamp(0, 1)
+    up = torch.randn(a.shape, device=dev, generator=g)
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+
+    def once():
+        m, dA, dB, dC = fusedssim(C1, C2, a, b, True)
+        return fusedssim_backward(C1, C2, a, b, up, dA, dB, dC)
+    for _ in range(3):
+        once()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        once()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = 13 * 4 * a.numel()
+    out = {"shape": list(a.shape), "ms_fwd_bwd": round(ms, 4), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+           "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import ssim_oracle
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            torch.set_num_threads(threads)
+            ac, bc, uc = a.cpu(), b.cpu(), up.cpu()
+            t = time.perf_counter()
+            ssim_oracle.ssim_and_grad(ac, bc, dtype=torch.float32, upstream=uc)
+            dt = time.perf_counter() - t
+            out["cpu_baseline"] = {"value": round(dt * 1e3, 1), "unit": "ms (fwd+bwd)", "cores": threads,
+                                   "kind": "port", "sample": "the same image pair, float32 torch-CPU restatement"}
         except Exception as e:
             out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
     return out

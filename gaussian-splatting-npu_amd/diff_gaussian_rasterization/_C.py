@@ -156,21 +156,26 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
     M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
-    # Render-pass gradients (one allocation): mean2D 3 | colors 3 | conic 4 | opacity 1 | invdepth 1.
+    # Render-pass gradients (one allocation): mean2D 3 | colors 3 | conic 4 | invdepth 1.
     # The HIP backward writes every element (no atomics, no pre-zeroing needed).
-    acc = torch.empty((P * 12,), dtype=torch.float32, device=dev)
+    acc = torch.empty((P * 11,), dtype=torch.float32, device=dev)
     dL_dmeans2D = acc[0:3 * P].view(P, 3)
     dL_dcolors = acc[3 * P:6 * P].view(P, 3)
     dL_dconic = acc[6 * P:10 * P].view(P, 2, 2)
-    dL_dopacity = acc[10 * P:11 * P].view(P, 1)
     has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
-    dL_dinvdepths = acc[11 * P:12 * P].view(P, 1)
-    # Fully written by the HIP kernel (zeros for culled Gaussians)
-    dL_dmeans3D = torch.empty((P, 3), dtype=torch.float32, device=dev)
-    dL_dcov3D = torch.empty((P, 6), dtype=torch.float32, device=dev)
-    dL_dsh = (torch.empty if M else torch.zeros)((P, M, 3), dtype=torch.float32, device=dev)
-    dL_dscales = torch.empty((P, 3), dtype=torch.float32, device=dev)
-    dL_drotations = torch.empty((P, 4), dtype=torch.float32, device=dev)
+    dL_dinvdepths = acc[10 * P:11 * P].view(P, 1)
+    # Parameter gradients, fully written by the HIP kernel (zeros for culled Gaussians), in ONE
+    # buffer laid out as multiview.PARAM_ORDER (means3D | sh | opacity | scales | rotations) then
+    # cov3D: autograd keeps these views as the leaves' .grad, so a multi-GPU step all-reduces the
+    # buffer in place instead of gathering and scattering 236 B per Gaussian around the collective.
+    sizes = [3 * P, 3 * M * P, P, 3 * P, 4 * P, 6 * P]
+    parts = torch.split(torch.empty((sum(sizes),), dtype=torch.float32, device=dev), sizes)
+    dL_dmeans3D = parts[0].view(P, 3)
+    dL_dsh = parts[1].view(P, M, 3)
+    dL_dopacity = parts[2].view(P, 1)
+    dL_dscales = parts[3].view(P, 3)
+    dL_drotations = parts[4].view(P, 4)
+    dL_dcov3D = parts[5].view(P, 6)
     if P == 0:
         return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
 

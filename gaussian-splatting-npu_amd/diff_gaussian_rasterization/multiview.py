@@ -28,11 +28,35 @@ def grad_bucket(params, order=PARAM_ORDER):
     return torch.cat([params[k].grad.reshape(-1) for k in order])
 
 
+def flat_grad_view(params, order=PARAM_ORDER):
+    """The one buffer holding every parameter gradient, if the .grad tensors are consecutive
+    views of a single storage in `order` (as the HIP backward allocates them and autograd hands
+    them to the leaves); otherwise None."""
+    gs = [params[k].grad for k in order]
+    g0 = gs[0]
+    if any(g is None for g in gs):
+        return None
+    if any(not g.is_contiguous() or g.dtype != g0.dtype or g.device != g0.device for g in gs):
+        return None
+    base = g0.untyped_storage().data_ptr()
+    off = g0.storage_offset()
+    for g in gs:
+        if g.untyped_storage().data_ptr() != base or g.storage_offset() != off:
+            return None
+        off += g.numel()
+    return g0.as_strided((off - g0.storage_offset(),), (1,), g0.storage_offset())
+
+
 def allreduce_grads(params, order=PARAM_ORDER, group=None):
-    """SUM every parameter gradient across ranks with one collective on a flat bucket, and
-    write the result back into .grad.  Returns the number of bytes reduced per rank."""
+    """SUM every parameter gradient across ranks with one collective on a flat bucket.  When the
+    gradients already live in one buffer (flat_grad_view) it is reduced in place; otherwise they
+    are gathered into a bucket and scattered back.  Returns the number of bytes reduced per rank."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return 0
+    flat = flat_grad_view(params, order)
+    if flat is not None:
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+        return flat.numel() * flat.element_size()
     flat = grad_bucket(params, order)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     off = 0

@@ -324,3 +324,21 @@ def test_callback_forward_matches_split_forward():
     assert bufs[1].numel() >= lib.gsr_binning_buffer_size(L2)
     assert torch.equal(radii, radii2)
     assert torch.equal(color, color2) and torch.equal(inv, inv2)
+
+
+def test_parameter_gradients_share_one_buffer():
+    """The backward's parameter gradients arrive as consecutive views of one buffer (multiview
+    PARAM_ORDER), so the multi-GPU step can all-reduce them in place (multiview.flat_grad_view)."""
+    from diff_gaussian_rasterization import multiview
+    case = common.make_case()
+    t, kw = _inputs(case, "sh_scales")
+    color, radii, inv = _dgr().GaussianRasterizer(_settings(case))(
+        means2D=torch.zeros_like(t["means3D"], requires_grad=True), **kw)
+    torch.autograd.backward([color, inv], [case["grad_color"].to(DEV), case["grad_invdepth"].to(DEV)])
+    params = {"means3D": t["means3D"], "shs": t["shs"], "opacities": t["opacities"], "scales": t["scales"],
+              "rotations": t["rotations"]}
+    flat = multiview.flat_grad_view(params)
+    assert flat is not None
+    assert flat.numel() == sum(p.numel() for p in params.values())
+    torch.testing.assert_close(flat, multiview.grad_bucket(params), rtol=0, atol=0)
+

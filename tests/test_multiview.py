@@ -40,7 +40,20 @@ def _fake_params(P, M, view):
     return out
 
 
-def _worker(rank, world, port, P, M, views_per_rank, q):
+def _fake_params_flat(P, M, view):
+    """As _fake_params, with the gradients as consecutive views of one buffer (the layout the
+    HIP backward produces)."""
+    p = _fake_params(P, M, view)
+    flat = torch.cat([p[k].grad.reshape(-1) for k in multiview.PARAM_ORDER])
+    off = 0
+    for k in multiview.PARAM_ORDER:
+        n = p[k].grad.numel()
+        p[k].grad = flat[off:off + n].view_as(p[k])
+        off += n
+    return p
+
+
+def _worker(rank, world, port, P, M, views_per_rank, q, flat=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -48,12 +61,13 @@ def _worker(rank, world, port, P, M, views_per_rank, q):
         views = multiview.views_for_rank(rank, world, views_per_rank)
         params = None
         for v in views:  # local accumulation over this rank's views
-            p = _fake_params(P, M, v)
+            p = (_fake_params_flat if flat else _fake_params)(P, M, v)
             if params is None:
                 params = p
             else:
                 for k in params:
                     params[k].grad += p[k].grad
+        assert (multiview.flat_grad_view(params) is not None) == flat
         nbytes = multiview.allreduce_grads(params)
         t = multiview.max_over_ranks(0.5 + rank)
         q.put((rank, views, {k: v.grad.numpy().copy() for k, v in params.items()}, nbytes, t))  # by value
@@ -61,13 +75,15 @@ def _worker(rank, world, port, P, M, views_per_rank, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("flat", [False, True], ids=["bucketed", "in-place"])
 @pytest.mark.parametrize("views_per_rank", [1, 4])
-def test_allreduce_sums_all_views_world2(views_per_rank):
+def test_allreduce_sums_all_views_world2(views_per_rank, flat):
     world, P, M = 2, 257, 16
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, P, M, views_per_rank, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, P, M, views_per_rank, q, flat))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]

@@ -11,13 +11,15 @@ import json
 import os
 import sys
 
-SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_reduce_kernel": "scan", "scan_apply_kernel": "scan",
-         "scan_blocksums_kernel": "scan", "emit_instances_kernel": "emit_instances",
-         "tile_ranges_kernel": "tile_ranges", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
+SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_lookback_kernel": "scan",
+         "emit_instances_kernel": "emit_instances", "tile_ranges_kernel": "tile_ranges",
+         "tile_order_kernel": "tile_order", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
          "preprocess_bwd_kernel": "preprocess_bwd",
          # the depth sort and the tile sort share these kernels: reported together, per step
-         "radix_histogram_kernel": "radix_sorts", "radix_digit_scan_kernel": "radix_sorts",
-         "onesweep_kernel": "radix_sorts"}
+         "radix_count_kernel": "radix_sorts", "radix_rowscan_kernel": "radix_sorts",
+         "radix_scatter_kernel": "radix_sorts",
+         # SURVEY §8f side paths (bench.py aux leg)
+         "knn_": "distCUDA2", "ssim_fwd_kernel": "ssim_fwd", "ssim_bwd_kernel": "ssim_bwd"}
 
 
 def short_name(k):
