@@ -48,18 +48,21 @@ def parse():
 
 
 def algorithmic_bytes(P, M, L, N, T, P_vis):
-    """Compulsory HBM bytes per launch of each kernel (SURVEY.md §8d, split per kernel; see DESIGN.md)."""
+    """Compulsory HBM bytes per launch of each kernel (SURVEY.md §8d, split per kernel; DESIGN.md §4)."""
     params = 4 * (11 + 3 * M)  # means 12 + scales 12 + rot 16 + opacity 4 + SH 12M
     return {
-        "preprocess_fwd": P * params + P_vis * 44 + P * 8,     # params in; 44 B splat record + count + key out
-        "depth_sort": P * 8,                                   # depth key in, sorted id out
-        "scan": P * 12,                                        # sorted id + gathered count in, offset out
-        "emit_instances": P * 24 + L * 8,                      # per-Gaussian rect inputs; (tile, id) per instance
-        "tile_sort": L * 20,                                   # (tile, id) in; id + tile + inverse slot out
+        # params in; key, radius, tile count, rect out per Gaussian; splat record 48 + conic 16 +
+        # means2D 8 + rgb 12 + depth 4 + clamped 1 per visible Gaussian
+        "preprocess_fwd": P * (params + 20) + P_vis * 89,
+        # depth keys in, sorted ids out; rects gathered and laid out in depth order, tile counts out
+        "depth_sort": P * 28,
+        "scan": P * 8,                                          # depth-ordered tile counts in, offsets out
+        "emit_instances": P * 20 + L * 9,                       # ids, offsets, rects, emit_start; (tile, id, flag)
+        "tile_sort": L * 24,                                    # (tile, slot, id) in and out
         "tile_ranges": L * 4 + T * 8,
-        "tile_order": T * 12,                                  # per-tile work in, launch order out
-        "render_fwd": L * 44 + N * 24 + T * 8,                 # id + 40 B record per instance; 24 B/pixel out
-        "render_bwd": L * 44 + N * 24 + T * 8,                 # id + record per instance; 24 B/pixel in
+        "tile_order": T * 12,                                   # per-tile work in, launch order out
+        "render_fwd": L * 44 + N * 24 + T * 8,                  # id + 40 B record per instance; 24 B/pixel out
+        "render_bwd": L * 44 + N * 24 + T * 8,                  # id + record per instance; 24 B/pixel in
         "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in
     }
 
