@@ -252,27 +252,42 @@ def aux_ssim(H, W, dev, args, reps=20):
     backward, timed with events on the current stream; HBM-bound, so priced in algorithmic bytes
     (forward: 2 images in, map + 3 partial planes out; backward: 2 images + dL/dmap + 3 partial
     planes in, dL/dimg1 out: 13 planes of 4 B per pixel and channel)."""
-    from fused_ssim import fusedssim, fusedssim_backward
+    import fused_ssim
+    lib = fused_ssim._lib
     g = torch.Generator(device=dev).manual_seed(0)
     a = torch.rand((1, 3, H, W), device=dev, generator=g)
     b = (a + 0.1 * torch.randn(a.shape, device=dev, generator=g)).clamp(0, 1)
     up = torch.randn(a.shape, device=dev, generator=g)
     C1, C2 = 0.01 ** 2, 0.03 ** 2
+    m, dA, dB, dC, grad = (torch.empty_like(a) for _ in range(5))
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    n = a.numel() // (H * W)
 
-    def once():
-        m, dA, dB, dC = fusedssim(C1, C2, a, b, True)
-        return fusedssim_backward(C1, C2, a, b, up, dA, dB, dC)
+    # the C ABI directly on preallocated planes, so the events see kernel time, not Python
+    def fwd():
+        return lib.gsr_ssim_forward(n, H, W, C1, C2, a.data_ptr(), b.data_ptr(), m.data_ptr(), dA.data_ptr(),
+                             dB.data_ptr(), dC.data_ptr(), stream)
+
+    def bwd():
+        return lib.gsr_ssim_backward(n, H, W, C1, C2, a.data_ptr(), b.data_ptr(), up.data_ptr(), dA.data_ptr(),
+                              dB.data_ptr(), dC.data_ptr(), grad.data_ptr(), stream)
+
+    def timed(fn):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps
     for _ in range(3):
-        once()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        once()
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+        if fwd() or bwd():
+            raise RuntimeError(lib.gsr_last_error().decode())
+    ms_f, ms_b = timed(fwd), timed(bwd)
+    ms = ms_f + ms_b
     nbytes = 13 * 4 * a.numel()
-    out = {"shape": list(a.shape), "ms_fwd_bwd": round(ms, 4), "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+    out = {"shape": list(a.shape), "ms_fwd_bwd": round(ms, 4), "ms_fwd": round(ms_f, 4), "ms_bwd": round(ms_b, 4),
+           "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
            "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "cpu_baseline": None}
     if not args.no_cpu_baseline:
         try:

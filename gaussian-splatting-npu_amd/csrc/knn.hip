@@ -2,7 +2,8 @@
 // scene/gaussian_model.py:159-160) for gfx950: per point, the mean squared distance to its
 // 3 nearest other points.  Exact 3-NN over a uniform grid instead of simple-knn's Morton
 // boxes of 1024 points scanned by every query:
-//   1. bounds (one pass, ordered-int atomics), read back to size the grid (~2 points/cell);
+//   1. bounds (per-workgroup partials folded by one workgroup into mapped host words), read on
+//      the host to size the grid (~2 points/cell);
 //   2. cell id per point; stable radix sort of (cell, index) with the rasterizer's own sort;
 //   3. points gathered into cell order (16-B rows), cell ranges;
 //   4. one thread per point (in cell order, so a wave's queries share cells in L1/L2) visits
@@ -28,8 +29,14 @@ __device__ __forceinline__ uint32_t f2ord(float f)
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-__global__ void __launch_bounds__(256) knn_bounds_kernel(int P, const float* pts, uint32_t* bounds)
+constexpr int KNN_BOUNDS_BLOCKS = 256;
+
+// Per-workgroup min/max of the three coordinates (no atomics: 24k same-address atomics from every
+// wave cost ~0.28 ms at P = 1M), then one workgroup folds the partials and stores the six
+// ordered words straight into the caller's mapped host page (no memset, no D2H copy).
+__global__ void __launch_bounds__(256) knn_bounds_kernel(int P, const float* pts, float* partial)
 {
+    __shared__ float red[6][4];
     float mn[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, mx[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
     for (int i = blockIdx.x * 256 + (int)threadIdx.x; i < P; i += gridDim.x * 256) {
 #pragma unroll
@@ -47,17 +54,44 @@ __global__ void __launch_bounds__(256) knn_bounds_kernel(int P, const float* pts
             mx[a] = fmaxf(mx[a], __shfl_xor(mx[a], d, 64));
         }
     }
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-            atomicMin(&bounds[a], f2ord(mn[a]));
-            atomicMax(&bounds[3 + a], f2ord(mx[a]));
+            red[a][w] = mn[a];
+            red[3 + a][w] = mx[a];
         }
     }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const int k = threadIdx.x;
+        float v = red[k][0];
+        for (int j = 1; j < 4; j++) v = k < 3 ? fminf(v, red[k][j]) : fmaxf(v, red[k][j]);
+        partial[blockIdx.x * 8 + k] = v;
+    }
+}
+
+__global__ void __launch_bounds__(64) knn_bounds_final_kernel(int nblocks, const float* partial, uint32_t* host_out)
+{
+    const int k = threadIdx.x & 7;
+    if (k >= 6) return;
+    float v = k < 3 ? FLT_MAX : -FLT_MAX;
+    for (int b = threadIdx.x >> 3; b < nblocks; b += 8) {
+        const float x = partial[b * 8 + k];
+        v = k < 3 ? fminf(v, x) : fmaxf(v, x);
+    }
+#pragma unroll
+    for (int d = 8; d <= 32; d <<= 1) {
+        const float o = __shfl_xor(v, d, 64);
+        v = k < 3 ? fminf(v, o) : fmaxf(v, o);
+    }
+    if (threadIdx.x < 6)
+        __hip_atomic_store(host_out + k, f2ord(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 struct KnnGrid {
     float ox, oy, oz, inv_h, h;
+    float tol;  // absolute slack for rounding of cell coordinates (a few ulps of the coordinates)
     int nx, ny, nz;
 };
 
@@ -113,7 +147,19 @@ __global__ void __launch_bounds__(256) knn_query_kernel(int P, const float4* spt
     const int cx = (int)(c % (uint32_t)g.nx), cy = (int)((c / (uint32_t)g.nx) % (uint32_t)g.ny),
               cz = (int)(c / ((uint32_t)g.nx * (uint32_t)g.ny));
     float b[3] = {FLT_MAX, FLT_MAX, FLT_MAX};
+    // q's offsets inside its own cell, for the squared distance from q to another cell's box
+    const float fx = q.x - (g.ox + (float)cx * g.h), fy = q.y - (g.oy + (float)cy * g.h),
+                fz = q.z - (g.oz + (float)cz * g.h);
+    auto axis_gap = [&](int d, float f) {  // distance along one axis to a cell d cells away
+        return d > 0 ? fmaxf(0.f, (float)d * g.h - f - g.tol)
+                     : (d < 0 ? fmaxf(0.f, f - (float)(d + 1) * g.h - g.tol) : 0.f);
+    };
     auto scan_cell = [&](int x, int y, int z) {
+        // Skip a cell whose box lies farther than the current third-best.  The gaps are shrunk by
+        // tol (rounding of q's offset and of the box corners); clamped boundary cells only ever
+        // make a box nearer than it is.
+        const float gx = axis_gap(x - cx, fx), gy = axis_gap(y - cy, fy), gz = axis_gap(z - cz, fz);
+        if ((gx * gx + gy * gy + gz * gz) * (1.0f - 1e-5f) > b[2]) return;
         const uint2 r = cell_range[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
         for (uint32_t j = r.x; j < r.y; j++) {
             if ((int)j == k) continue;
@@ -140,8 +186,8 @@ __global__ void __launch_bounds__(256) knn_query_kernel(int P, const float4* spt
         }
         // Every unvisited point lies in a cell at Chebyshev distance > r, hence farther than
         // r * h from q (q lies in its own cell; a small margin covers rounding and clamping).
-        const float lb = fmaxf(0.f, (float)r * g.h * (1.0f - 1e-5f) - 1e-6f * g.h);
-        if (b[2] <= lb * lb) break;
+        const float lb = fmaxf(0.f, (float)r * g.h - g.tol);
+        if (b[2] <= lb * lb * (1.0f - 1e-5f)) break;
     }
     dist2[sorted_idx[k]] = (b[0] + b[1] + b[2]) / 3.0f;
 }
@@ -170,7 +216,7 @@ KnnLayout knn_layout(int P)
 size_t knn_workspace_bytes(int P)
 {
     const KnnLayout l = knn_layout(P);
-    return l.off[9] + align_up(radix_status_bytes(P, 4), 256) + 256;
+    return l.off[9] + align_up(radix_status_bytes(P, 4), 256) + 32 * KNN_BOUNDS_BLOCKS;
 }
 
 // Host: bounds -> grid of ~P/2 cells (at most 2P + 64), then sort, gather, query.
@@ -179,13 +225,13 @@ hipError_t knn_dist2(int P, const float* pts, float* dist2, char* ws, uint32_t* 
     if (P <= 0) return hipSuccess;
     const KnnLayout l = knn_layout(P);
     auto at32 = [&](int i) { return reinterpret_cast<uint32_t*>(ws + l.off[i]); };
-    uint32_t* bounds = reinterpret_cast<uint32_t*>(ws + l.off[9] + align_up(radix_status_bytes(P, 4), 256));
+    float* partial = reinterpret_cast<float*>(ws + l.off[9] + align_up(radix_status_bytes(P, 4), 256));
+    uint32_t* bounds_dev = nullptr;
     hipError_t e;
-    if ((e = hipMemsetD32Async(bounds, 0xFFFFFFFFu, 3, s)) != hipSuccess) return e;
-    if ((e = hipMemsetD32Async(bounds + 3, 0u, 3, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(knn_bounds_kernel, dim3(min((P + 255) / 256, 1024)), dim3(256), 0, s, P, pts, bounds);
-    if ((e = hipMemcpyAsync(host_bounds, bounds, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return e;
+    if ((e = hipHostGetDevicePointer((void**)&bounds_dev, host_bounds, 0)) != hipSuccess) return e;
+    const int nb = min((P + 255) / 256, KNN_BOUNDS_BLOCKS);
+    hipLaunchKernelGGL(knn_bounds_kernel, dim3(nb), dim3(256), 0, s, P, pts, partial);
+    hipLaunchKernelGGL(knn_bounds_final_kernel, dim3(1), dim3(64), 0, s, nb, partial, bounds_dev);
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     float lo[3], hi[3];
     for (int a = 0; a < 3; a++) {
@@ -225,6 +271,9 @@ hipError_t knn_dist2(int P, const float* pts, float* dist2, char* ws, uint32_t* 
     g.ox = lo[0]; g.oy = lo[1]; g.oz = lo[2];
     g.h = (float)h;
     g.inv_h = (float)(1.0 / h);
+    double amax = 0.0;
+    for (int a = 0; a < 3; a++) amax = fmax(amax, fmax(fabs((double)lo[a]), fabs((double)hi[a])));
+    g.tol = (float)(16.0 * FLT_EPSILON * (amax + h));
     g.nx = n[0]; g.ny = n[1]; g.nz = n[2];
     const uint32_t ncells = (uint32_t)n[0] * (uint32_t)n[1] * (uint32_t)n[2];
 
