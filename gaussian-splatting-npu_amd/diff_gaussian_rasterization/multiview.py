@@ -4,7 +4,8 @@ One process per GPU; the Gaussian parameters are replicated, camera views are de
 round-robin (view v goes to rank v mod world), every rank runs forward+backward of its own
 views and accumulates the parameter gradients locally, and ONE all_reduce(SUM) of a flat
 fp32 bucket holding every parameter gradient (236 B per Gaussian at SH degree 3) makes the
-replicas agree.  The reference trains on one view per step on one GPU (train.py:97-111);
+replicas agree.  The densification statistics (screen-space gradient norms and visit counts:
+SUM; max screen radius: MAX) are accumulated per view and reduced the same way.  The reference trains on one view per step on one GPU (train.py:97-111);
 this is the multi-view form of that step, the only exchange the path has.
 
 Backend-agnostic: "nccl" (RCCL over xGMI) on the GPU box, "gloo" in the CPU tests.
@@ -66,6 +67,41 @@ def allreduce_grads(params, order=PARAM_ORDER, group=None):
         g.copy_(flat[off:off + n].view_as(g))
         off += n
     return flat.numel() * flat.element_size()
+
+
+def densification_stats(P, device=None):
+    """Per-rank densification accumulators, shaped as GaussianModel keeps them
+    (scene/gaussian_model.py: xyz_gradient_accum (P,1), denom (P,1), max_radii2D (P,)).
+    accum and denom are two columns of ONE (P,2) buffer so their SUM is one collective."""
+    sums = torch.zeros((P, 2), dtype=torch.float32, device=device)
+    return {"xyz_gradient_accum": sums[:, 0:1], "denom": sums[:, 1:2], "_sums": sums,
+            "max_radii2D": torch.zeros((P,), dtype=torch.float32, device=device)}
+
+
+@torch.no_grad()
+def add_view_stats(stats, viewspace_grad, radii):
+    """One view's contribution, before any reduction: train.py:166 (running max of radii over
+    the visible Gaussians) and gaussian_model.py:471-473 (the norm of that view's screen-space
+    gradient, taken per view, and a visit count).  viewspace_grad is the view's means2D.grad
+    (P,3); radii the view's int32 radii (P,)."""
+    vis = radii > 0
+    mr = stats["max_radii2D"]
+    mr[vis] = torch.max(mr[vis], radii[vis].to(mr.dtype))
+    stats["xyz_gradient_accum"][vis] += torch.norm(viewspace_grad[vis, :2], dim=-1, keepdim=True)
+    stats["denom"][vis] += 1
+
+
+def allreduce_densification_stats(stats, group=None):
+    """SUM of (xyz_gradient_accum, denom) in one collective on their shared (P,2) buffer, MAX of
+    max_radii2D in a second: afterwards every replica holds the statistics of all
+    views of the step, so densify_and_prune makes the same decision on every rank.  Returns the
+    bytes reduced per rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return 0
+    sums, mr = stats["_sums"], stats["max_radii2D"]
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(mr, op=dist.ReduceOp.MAX, group=group)
+    return sums.numel() * sums.element_size() + mr.numel() * mr.element_size()
 
 
 def max_over_ranks(seconds, device=None, group=None):

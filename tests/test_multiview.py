@@ -108,6 +108,80 @@ def test_allreduce_sums_all_views_world2(views_per_rank, flat):
         assert (res[0][2][k] == res[1][2][k]).all()
 
 
+def _fake_view(P, view):
+    """A view's screen-space gradient (P,3) and int32 radii (about a third culled)."""
+    g = torch.Generator().manual_seed(500 + view)
+    grad = torch.randn((P, 3), generator=g)
+    radii = torch.randint(0, 40, (P,), generator=g, dtype=torch.int32)
+    radii[torch.rand((P,), generator=g) < 0.3] = 0
+    return grad, radii
+
+
+def _stats_worker(rank, world, port, P, views_per_rank, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        stats = multiview.densification_stats(P)
+        for v in multiview.views_for_rank(rank, world, views_per_rank):
+            multiview.add_view_stats(stats, *_fake_view(P, v))
+        nbytes = multiview.allreduce_densification_stats(stats)
+        q.put((rank, {k: stats[k].numpy().copy() for k in ("xyz_gradient_accum", "denom", "max_radii2D")},
+               nbytes))
+    finally:
+        dist.destroy_process_group()
+
+
+def _serial_stats(P, views):
+    """train.py:166 + gaussian_model.py:471-473 applied view after view on one process."""
+    accum = torch.zeros((P, 1))
+    denom = torch.zeros((P, 1))
+    max_radii2D = torch.zeros((P,))
+    for v in views:
+        grad, radii = _fake_view(P, v)
+        visibility_filter = (radii > 0).nonzero()  # gaussian_renderer/__init__.py:123
+        max_radii2D[visibility_filter] = torch.max(max_radii2D[visibility_filter], radii[visibility_filter])
+        accum[visibility_filter] += torch.norm(grad[visibility_filter, :2], dim=-1, keepdim=True)
+        denom[visibility_filter] += 1
+    return {"xyz_gradient_accum": accum, "denom": denom, "max_radii2D": max_radii2D}
+
+
+@pytest.mark.parametrize("views_per_rank", [1, 4])
+def test_densification_stats_reduce_world2(views_per_rank):
+    world, P = 2, 301
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, world, port, P, views_per_rank, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    views = sorted(v for r in range(world) for v in multiview.views_for_rank(r, world, views_per_rank))
+    expect = _serial_stats(P, views)
+    for rank, got, nbytes in res:
+        assert nbytes == P * 2 * 4 + P * 4
+        torch.testing.assert_close(torch.from_numpy(got["xyz_gradient_accum"]), expect["xyz_gradient_accum"],
+                                   rtol=1e-6, atol=1e-6)
+        assert torch.equal(torch.from_numpy(got["denom"]), expect["denom"])
+        assert torch.equal(torch.from_numpy(got["max_radii2D"]), expect["max_radii2D"])
+    for k in ("xyz_gradient_accum", "denom", "max_radii2D"):
+        assert (res[0][1][k] == res[1][1][k]).all()
+
+
+def test_view_stats_match_training_loop_single_process():
+    P = 97
+    stats = multiview.densification_stats(P)
+    for v in (0, 3):
+        multiview.add_view_stats(stats, *_fake_view(P, v))
+    assert multiview.allreduce_densification_stats(stats) == 0
+    expect = _serial_stats(P, (0, 3))
+    for k in expect:
+        torch.testing.assert_close(stats[k], expect[k], rtol=1e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_views_cover_the_ring(world):
     views = [v for r in range(world) for v in multiview.views_for_rank(r, world, 8 // world)]
