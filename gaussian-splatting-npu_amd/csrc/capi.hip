@@ -323,7 +323,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
                                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                                           at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx, tile_keys, gids, emit_start,
-                                          at<uint8_t>(bb, b.off[BIN_VALID]),
+                                          at<uint32_t>(bb, b.off[BIN_VALID]),
                                           at<uint2>(ib, im.off[IMG_RANGES]), T, s));
         }
         DEBUG_SYNC(s);
@@ -437,7 +437,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
     r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
-    r.valid = R > 0 ? at<uint8_t>(bb, b.off[BIN_VALID]) : nullptr;
+    r.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
     if (R > 0) {
         {
             ProfScope ps_(PK_TILE_ORDER, s);
@@ -465,7 +465,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     p.campos = campos;
     p.antialiasing = antialiasing;
     p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
-    p.valid = R > 0 ? at<uint8_t>(bb, b.off[BIN_VALID]) : nullptr;
+    p.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
     p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     p.has_invdepth = dL_invdepths != nullptr;

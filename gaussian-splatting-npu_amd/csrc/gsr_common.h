@@ -195,7 +195,7 @@ enum BinArray {
     BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
                           // it hosts the emission arrays and sort ping-pong buffers (32 B/instance)
     BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
-    BIN_VALID,            // u8[L] 1 <=> the gradient record at this emission slot was written (backward)
+    BIN_VALID,            // u32[ceil(L/32)] bit per emission slot: its gradient record was written (backward)
     BIN_COUNT
 };
 
@@ -236,7 +236,7 @@ inline ImageLayout image_layout(int W, int H)
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, 4), n};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, 4), 4 * ((n + 31) / 32)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

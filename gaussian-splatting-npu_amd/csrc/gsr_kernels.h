@@ -67,7 +67,7 @@ struct RenderBwdArgs {
     const float* dL_dpixels;
     const float* dL_invdepths;  // (1,H,W) or null
     const uint32_t* slot;       // emission slot of each sorted position
-    uint8_t* valid;             // valid[slot] = 1 for every record written (zeroed by the caller)
+    uint32_t* valid;            // bit (slot & 31) of valid[slot >> 5] set for every record written (cleared by emit)
     float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
 };
 
@@ -100,7 +100,7 @@ struct PreprocessBwdArgs {
     int antialiasing;
     // per-instance gradient records and the gather map
     const float* grad_inst;         // f32x12[L], emission order
-    const uint8_t* valid;           // records not flagged were never written (no contribution)
+    const uint32_t* valid;          // one bit per slot: records not flagged were never written (no contribution)
     // (records are stored at emission slots: Gaussian i's are [emit_start[i], +tiles_touched[i]))
     const uint32_t* emit_start;     // first emission slot of Gaussian i
     const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
@@ -133,10 +133,10 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
                       uint32_t* sorted_counts = nullptr);
-// Also clears valid[slot] (the backward's record flags) and ranges[0..T) for tile_ranges.
+// Also clears the valid bit mask (the backward's record flags) and ranges[0..T) for tile_ranges.
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
                                  uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s);
+                                 uint32_t* emit_start, uint32_t* valid, uint2* ranges, int T, hipStream_t s);
 // ranges must be zero on entry unless L == 0 (emit_instances clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,

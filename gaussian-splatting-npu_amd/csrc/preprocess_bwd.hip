@@ -28,6 +28,8 @@ struct BwdIn {
     uint8_t clamped;
 };
 
+constexpr int REC_BATCH = 4;  // record flags / records in flight per step
+
 __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in)
 {
     const size_t i = (size_t)idx;
@@ -48,27 +50,37 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) in.g[q] = 0.f;
     // This Gaussian's records are contiguous (emission order); entries that contributed to no
-    // pixel were never written (valid = 0) and are not read (most slots: records are sparse).
-    // Eight flags per step in flight together, then the flagged records; the sum order stays
-    // the slot order (bitwise reproducible).
+    // pixel were never written (their bit in the valid mask is 0) and are not read (most slots:
+    // records are sparse).  The mask has one bit per slot (L/8 bytes: it stays in L2), so a
+    // Gaussian's flags are one or two words; its flagged records are then read REC_BATCH at a time
+    // in slot order (bitwise reproducible sums).
     const uint32_t e0 = a.emit_start[idx];
     const uint32_t e1 = e0 + a.tiles_touched[idx];  // 0 tiles for culled Gaussians
-    for (uint32_t e = e0; e < e1; e += 8) {
-        bool v[8];
+    for (uint32_t w0 = e0 & ~31u; w0 < e1; w0 += 32) {
+        uint32_t bits = a.valid[w0 >> 5];
+        if (w0 < e0) bits &= ~0u << (e0 - w0);
+        if (e1 - w0 < 32u) bits &= (1u << (e1 - w0)) - 1u;
+        while (bits) {
+        bool v[REC_BATCH];
+        uint32_t sl[REC_BATCH];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = a.valid[min(e + k, e1 - 1)] != 0 && e + k < e1;
-        float4 r[8][3];
+        for (int k = 0; k < REC_BATCH; k++) {
+            v[k] = bits != 0u;
+            sl[k] = w0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
+            bits &= bits - 1u;
+        }
+        float4 r[REC_BATCH][3];
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < REC_BATCH; k++) {
             if (v[k]) {
-                const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)(e + k) * GRAD_REC);
+                const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)sl[k] * GRAD_REC);
                 r[k][0] = rec[0];
                 r[k][1] = rec[1];
                 r[k][2] = rec[2];
             }
         }
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < REC_BATCH; k++) {
             if (v[k]) {
                 float* g = in.g;
                 g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
@@ -76,17 +88,116 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
                 g[8] += r[k][2].x; g[9] += r[k][2].y;
             }
         }
+        }
     }
 }
 
-// One Gaussian.  `sh` / `dsh` point at this Gaussian's SH coefficients and SH gradient,
-// either in global memory or in the workgroup's LDS staging slot (the same slot for both).
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in,
-                                                   const float* sh, float* dsh)
+// Per-Gaussian state carried from the non-SH part into the SH halves and the final dL/dmean3D.
+struct BwdState {
+    bool visible;
+    int ncoef;            // SH coefficients in use: (D + 1)^2, at most M (0: colors_precomp / culled)
+    f3 dir_orig;          // mean - campos (backward.cu:31)
+    float x, y, z;        // its normalisation
+    float dRGB[3];        // dL/dcolor, zeroed for clamped channels (backward.cu:41-44)
+    float dmx, dmy, dmz;  // dL/dmean3D without the view-direction term
+    float ddir[3];        // dL/d(normalised direction), summed over the SH coefficients
+};
+
+// Coefficient k's factor dRGB/dsh_k (backward.cu:51-100, same expressions: dL/dsh is
+// bit-identical) and its derivatives along the normalised view direction (the per-coefficient
+// terms of dRGBdx / dRGBdy / dRGBdz, backward.cu:60-127).  k is a compile-time constant after
+// unrolling, so the switch folds away.
+__device__ __forceinline__ void sh_term(int k, float x, float y, float z, float& b, float& gx, float& gy, float& gz)
+{
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    gx = gy = gz = 0.f;
+    switch (k) {
+    case 0: b = SH_C0; break;
+    case 1: b = -SH_C1 * y; gy = -SH_C1; break;
+    case 2: b = SH_C1 * z; gz = SH_C1; break;
+    case 3: b = -SH_C1 * x; gx = -SH_C1; break;
+    case 4: b = SH_C2_0 * xy; gx = SH_C2_0 * y; gy = SH_C2_0 * x; break;
+    case 5: b = SH_C2_1 * yz; gy = SH_C2_1 * z; gz = SH_C2_1 * y; break;
+    case 6:
+        b = SH_C2_2 * (2.f * zz - xx - yy);
+        gx = SH_C2_2 * 2.f * -x; gy = SH_C2_2 * 2.f * -y; gz = SH_C2_2 * 2.f * 2.f * z;
+        break;
+    case 7: b = SH_C2_3 * xz; gx = SH_C2_3 * z; gz = SH_C2_3 * x; break;
+    case 8: b = SH_C2_4 * (xx - yy); gx = SH_C2_4 * 2.f * x; gy = SH_C2_4 * 2.f * -y; break;
+    case 9: b = SH_C3_0 * y * (3.f * xx - yy); gx = SH_C3_0 * 3.f * 2.f * xy; gy = SH_C3_0 * 3.f * (xx - yy); break;
+    case 10: b = SH_C3_1 * xy * z; gx = SH_C3_1 * yz; gy = SH_C3_1 * xz; gz = SH_C3_1 * xy; break;
+    case 11:
+        b = SH_C3_2 * y * (4.f * zz - xx - yy);
+        gx = SH_C3_2 * -2.f * xy; gy = SH_C3_2 * (-3.f * yy + 4.f * zz - xx); gz = SH_C3_2 * 4.f * 2.f * yz;
+        break;
+    case 12:
+        b = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+        gx = SH_C3_3 * -3.f * 2.f * xz; gy = SH_C3_3 * -3.f * 2.f * yz; gz = SH_C3_3 * 3.f * (2.f * zz - xx - yy);
+        break;
+    case 13:
+        b = SH_C3_4 * x * (4.f * zz - xx - yy);
+        gx = SH_C3_4 * (-3.f * xx + 4.f * zz - yy); gy = SH_C3_4 * -2.f * xy; gz = SH_C3_4 * 4.f * 2.f * xz;
+        break;
+    case 14: b = SH_C3_5 * z * (xx - yy); gx = SH_C3_5 * 2.f * xz; gy = SH_C3_5 * -2.f * yz; gz = SH_C3_5 * (xx - yy); break;
+    default: b = SH_C3_6 * x * (xx - 3.f * yy); gx = SH_C3_6 * 3.f * (xx - yy); gy = SH_C3_6 * -3.f * 2.f * xy; break;
+    }
+}
+
+// SH backward over coefficients [K0, K1) (computeColorFromSH backward, backward.cu:23-142):
+// dL/dsh_k = b_k * dRGB, and the view-direction gradient accumulated into st.ddir.  `sh` / `dsh`
+// point at coefficient K0 of this Gaussian (global memory or its LDS staging row; they may be
+// the same row: every coefficient is read before it is overwritten).
+template <int K0, int K1>
+__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh)
+{
+#pragma unroll
+    for (int k = K0; k < K1; k++) {
+        if (k < st.ncoef) {
+            float b, gx, gy, gz;
+            sh_term(k, st.x, st.y, st.z, b, gx, gy, gz);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float v = sh[(k - K0) * 3 + c];
+                const float t = v * st.dRGB[c];
+                dsh[(k - K0) * 3 + c] = b * st.dRGB[c];
+                st.ddir[0] += t * gx;
+                st.ddir[1] += t * gy;
+                st.ddir[2] += t * gz;
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; c++) dsh[(k - K0) * 3 + c] = 0.f;
+        }
+    }
+}
+
+// dL/dmean3D with the view-direction term (backward.cu:130-141, 423-440), written.
+__device__ __forceinline__ void bwd_finish(const PreprocessBwdArgs& a, int idx, const BwdState& st)
+{
+    float* dmean = a.dL_dmean3D + 3 * (size_t)idx;
+    float dmx = st.dmx, dmy = st.dmy, dmz = st.dmz;
+    if (st.visible && st.ncoef > 1) {  // degree 0 has no direction dependence
+        const f3 dn = dnormvdv(st.dir_orig, {st.ddir[0], st.ddir[1], st.ddir[2]});
+        dmx += dn.x;
+        dmy += dn.y;
+        dmz += dn.z;
+    }
+    dmean[0] = dmx;
+    dmean[1] = dmy;
+    dmean[2] = dmz;
+}
+
+// Everything of one Gaussian except the SH coefficients: the reduced render gradients,
+// computeCov2DCUDA (backward.cu:147-326), the projection part of preprocessCUDA
+// (backward.cu:423-440), computeCov3D backward (backward.cu:330-393); sets up the SH state.
+__device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, const BwdIn& in, BwdState& st)
 {
     const size_t i = (size_t)idx;
-    float* dmean = a.dL_dmean3D + 3 * i;
-    float* dcov = a.dL_dcov3D + 6 * i;
+    st.visible = in.visible;
+    st.ncoef = 0;
+    st.dmx = st.dmy = st.dmz = 0.f;
+    st.ddir[0] = st.ddir[1] = st.ddir[2] = 0.f;
+    float* dcov_out = a.dL_dcov3D + 6 * i;
 
     if (!in.visible) {
         a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
@@ -95,11 +206,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         a.dL_dopacity[i] = 0.f;
         a.dL_dcolor[3 * i] = 0.f; a.dL_dcolor[3 * i + 1] = 0.f; a.dL_dcolor[3 * i + 2] = 0.f;
         if (a.dL_dinvdepth) a.dL_dinvdepth[i] = 0.f;
-        dmean[0] = 0.f; dmean[1] = 0.f; dmean[2] = 0.f;
 #pragma unroll
-        for (int k = 0; k < 6; k++) dcov[k] = 0.f;
-        if (dsh)
-            for (int k = 0; k < a.M * 3; k++) dsh[k] = 0.f;
+        for (int k = 0; k < 6; k++) dcov_out[k] = 0.f;
         if (a.dL_dscale) { a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f; }
         if (a.dL_drot) { float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f; }
         return;
@@ -186,6 +294,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     const float denom = c_xx * c_yy - c_xy * c_xy;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     const float(*Tm)[3] = T.m;
+    float dcov[6];
     if (denom2inv != 0) {
         dL_dc_xx += denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
                                  (denom - c_xx * c_yy) * dL_dconic.z);
@@ -206,6 +315,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 #pragma unroll
         for (int k = 0; k < 6; k++) dcov[k] = 0;
     }
+#pragma unroll
+    for (int k = 0; k < 6; k++) dcov_out[k] = dcov[k];
     const float(*V)[3] = Vrk.m;
     const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
                           (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
@@ -248,111 +359,26 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         dmy += (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
         dmz += (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
     }
+    st.dmx = dmx;
+    st.dmy = dmy;
+    st.dmz = dmz;
 
-    // ---------------- computeColorFromSH backward (backward.cu:23-142) ----------------
+    // ---------------- computeColorFromSH backward: set-up (backward.cu:28-49) ----------------
     if (a.shs) {
         const int deg = a.D;
-        const f3 dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
-        const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+        int nc = (deg + 1) * (deg + 1);
+        nc = nc < a.M ? nc : a.M;
+        st.ncoef = nc < 16 ? nc : 16;
+        st.dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
+        const f3 d = st.dir_orig;
+        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+        st.x = d.x / len;
+        st.y = d.y / len;
+        st.z = d.z / len;
         const uint8_t cl = in.clamped;
-        float dRGB[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            dRGB[c] = g[GF_COLOR_R + c];
-            dRGB[c] *= (cl >> c) & 1 ? 0 : 1;
-        }
-        float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
-        // dRGB/dsh_k coefficients; dL_dsh is written after every read of sh (sh and dsh may
-        // share an LDS slot), coefficient k * dRGB exactly as backward.cu:51-100.
-        float coef[16];
-        int ncoef = 0;
-#define SETSH(k, cf)      \
-    do {                  \
-        coef[k] = (cf);   \
-        ncoef = (k) + 1;  \
-    } while (0)
-        const float dRGBdsh0 = SH_C0;
-        SETSH(0, dRGBdsh0);
-        if (deg > 0) {
-            const float dRGBdsh1 = -SH_C1 * y;
-            const float dRGBdsh2 = SH_C1 * z;
-            const float dRGBdsh3 = -SH_C1 * x;
-            SETSH(1, dRGBdsh1);
-            SETSH(2, dRGBdsh2);
-            SETSH(3, dRGBdsh3);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                ddx[c] = -SH_C1 * sh[3 * 3 + c];
-                ddy[c] = -SH_C1 * sh[1 * 3 + c];
-                ddz[c] = SH_C1 * sh[2 * 3 + c];
-            }
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                SETSH(4, SH_C2_0 * xy);
-                SETSH(5, SH_C2_1 * yz);
-                SETSH(6, SH_C2_2 * (2.f * zz - xx - yy));
-                SETSH(7, SH_C2_3 * xz);
-                SETSH(8, SH_C2_4 * (xx - yy));
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    const float* s = sh + c;
-                    ddx[c] += SH_C2_0 * y * s[4 * 3] + SH_C2_2 * 2.f * -x * s[6 * 3] + SH_C2_3 * z * s[7 * 3] +
-                              SH_C2_4 * 2.f * x * s[8 * 3];
-                    ddy[c] += SH_C2_0 * x * s[4 * 3] + SH_C2_1 * z * s[5 * 3] + SH_C2_2 * 2.f * -y * s[6 * 3] +
-                              SH_C2_4 * 2.f * -y * s[8 * 3];
-                    ddz[c] += SH_C2_1 * y * s[5 * 3] + SH_C2_2 * 2.f * 2.f * z * s[6 * 3] + SH_C2_3 * x * s[7 * 3];
-                }
-                if (deg > 2) {
-                    SETSH(9, SH_C3_0 * y * (3.f * xx - yy));
-                    SETSH(10, SH_C3_1 * xy * z);
-                    SETSH(11, SH_C3_2 * y * (4.f * zz - xx - yy));
-                    SETSH(12, SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy));
-                    SETSH(13, SH_C3_4 * x * (4.f * zz - xx - yy));
-                    SETSH(14, SH_C3_5 * z * (xx - yy));
-                    SETSH(15, SH_C3_6 * x * (xx - 3.f * yy));
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        const float* s = sh + c;
-                        ddx[c] += (SH_C3_0 * s[9 * 3] * 3.f * 2.f * xy + SH_C3_1 * s[10 * 3] * yz +
-                                   SH_C3_2 * s[11 * 3] * -2.f * xy + SH_C3_3 * s[12 * 3] * -3.f * 2.f * xz +
-                                   SH_C3_4 * s[13 * 3] * (-3.f * xx + 4.f * zz - yy) +
-                                   SH_C3_5 * s[14 * 3] * 2.f * xz + SH_C3_6 * s[15 * 3] * 3.f * (xx - yy));
-                        ddy[c] += (SH_C3_0 * s[9 * 3] * 3.f * (xx - yy) + SH_C3_1 * s[10 * 3] * xz +
-                                   SH_C3_2 * s[11 * 3] * (-3.f * yy + 4.f * zz - xx) +
-                                   SH_C3_3 * s[12 * 3] * -3.f * 2.f * yz + SH_C3_4 * s[13 * 3] * -2.f * xy +
-                                   SH_C3_5 * s[14 * 3] * -2.f * yz + SH_C3_6 * s[15 * 3] * -3.f * 2.f * xy);
-                        ddz[c] += (SH_C3_1 * s[10 * 3] * xy + SH_C3_2 * s[11 * 3] * 4.f * 2.f * yz +
-                                   SH_C3_3 * s[12 * 3] * 3.f * (2.f * zz - xx - yy) +
-                                   SH_C3_4 * s[13 * 3] * 4.f * 2.f * xz + SH_C3_5 * s[14 * 3] * (xx - yy));
-                    }
-                }
-            }
-        }
-#undef SETSH
-        {
-            const int kmax = a.M < 16 ? a.M : 16;
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (k < kmax) {
-#pragma unroll
-                    for (int c = 0; c < 3; c++) dsh[k * 3 + c] = k < ncoef ? coef[k] * dRGB[c] : 0.f;
-                }
-            }
-            for (int k = 48; k < a.M * 3; k++) dsh[k] = 0.f;
-        }
-        const f3 dL_ddir = {ddx[0] * dRGB[0] + ddx[1] * dRGB[1] + ddx[2] * dRGB[2],
-                            ddy[0] * dRGB[0] + ddy[1] * dRGB[1] + ddy[2] * dRGB[2],
-                            ddz[0] * dRGB[0] + ddz[1] * dRGB[1] + ddz[2] * dRGB[2]};
-        const f3 dn = dnormvdv(dir_orig, dL_ddir);
-        dmx += dn.x;
-        dmy += dn.y;
-        dmz += dn.z;
+        for (int c = 0; c < 3; c++) st.dRGB[c] = g[GF_COLOR_R + c] * ((cl >> c) & 1 ? 0 : 1);
     }
-    dmean[0] = dmx;
-    dmean[1] = dmy;
-    dmean[2] = dmz;
 
     // ---------------- computeCov3D backward (backward.cu:330-393) ----------------
     if (a.scales) {
@@ -401,63 +427,84 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 }
 
 // SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's
-// traffic.  STAGED: the workgroup's 256 x 3M floats are read with coalesced 16-byte loads
-// into LDS (row stride padded to an odd number of dwords, so the 64 lanes walking their own
-// rows hit 64 different banks), each thread works on its row in place, and the SH gradients leave the same way -- instead
-// of every lane striding 192 B through global memory.
-template <bool STAGED>
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a, int lds_stride)
+// traffic.  STAGED (M = 16): the workgroup's SH rows pass through LDS in two halves of 24
+// floats (coefficients 0-7, then 8-15): coalesced 16-byte loads into rows padded to 25 dwords
+// (an odd stride: the 64 lanes walking their own rows hit 64 different banks), each thread
+// works on its row in place, and the SH gradients leave the same way.  Half rows keep the LDS
+// at 25 KB per workgroup, so LDS no longer caps the occupancy below the register limit.
+constexpr int SH_STRIDE = 25;    // LDS dwords per half row
+
+__device__ __forceinline__ void stage_half_in(const float* shs, int base, int n, int half, float* s_sh)
 {
-    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const float4* src = reinterpret_cast<const float4*>(shs + (size_t)base * 48);
+    for (int f = threadIdx.x; f < n * 6; f += 256) {
+        const int g = f / 6, j = f - g * 6;
+        const float4 v = src[g * 12 + half * 6 + j];
+        float* d = &s_sh[g * SH_STRIDE + 4 * j];
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+}
+
+__device__ __forceinline__ void stage_half_out(float* dsh, int base, int n, int half, const float* s_sh)
+{
+    float4* dst = reinterpret_cast<float4*>(dsh + (size_t)base * 48);
+    for (int f = threadIdx.x; f < n * 6; f += 256) {
+        const int g = f / 6, j = f - g * 6;
+        const float* q = &s_sh[g * SH_STRIDE + 4 * j];
+        dst[g * 12 + half * 6 + j] = make_float4(q[0], q[1], q[2], q[3]);
+    }
+}
+
+template <bool STAGED>
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a)
+{
+    __shared__ float s_sh[STAGED ? 256 * SH_STRIDE : 1];
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
     BwdIn in;
+    BwdState st;
     if (idx < a.P) bwd_gather(a, idx, in);  // in flight during the SH staging below
     if (!STAGED) {
         if (idx < a.P) {
-            const size_t w3 = (size_t)a.M * 3;
-            preprocess_bwd_one(a, idx, in, a.shs ? a.shs + idx * w3 : nullptr,
-                               a.dL_dsh ? a.dL_dsh + idx * w3 : nullptr);
+            bwd_core(a, idx, in, st);
+            if (a.dL_dsh) {
+                const size_t w3 = (size_t)a.M * 3;
+                float* dsh = a.dL_dsh + idx * w3;
+                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh);  // ncoef <= M: no read past the row
+                for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
+            }
+            bwd_finish(a, idx, st);
         }
         return;
     }
-    const int W3 = a.M * 3;  // multiple of 4 on this path
     const int n = min(256, a.P - base);
-    const int nv4 = n * (W3 / 4);
-    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
-    for (int f = threadIdx.x; f < nv4; f += 256) {
-        const int g = (f * 4) / W3, w = (f * 4) - g * W3;
-        const float4 v = src[f];
-        float* d = &s_sh[g * lds_stride + w];
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    stage_half_in(a.shs, base, n, 0, s_sh);
+    __syncthreads();
+    float* row = s_sh + threadIdx.x * SH_STRIDE;
+    if (idx < a.P) {
+        bwd_core(a, idx, in, st);
+        sh_bwd_range<0, 8>(st, row, row);
     }
+    __syncthreads();
+    stage_half_out(a.dL_dsh, base, n, 0, s_sh);
+    __syncthreads();
+    stage_half_in(a.shs, base, n, 1, s_sh);
     __syncthreads();
     if (idx < a.P) {
-        float* row = s_sh + threadIdx.x * lds_stride;
-        preprocess_bwd_one(a, idx, in, row, row);
+        sh_bwd_range<8, 16>(st, row, row);
+        bwd_finish(a, idx, st);
     }
     __syncthreads();
-    float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * W3);
-    for (int f = threadIdx.x; f < nv4; f += 256) {
-        const int g = (f * 4) / W3, w = (f * 4) - g * W3;
-        const float* q = &s_sh[g * lds_stride + w];
-        dst[f] = make_float4(q[0], q[1], q[2], q[3]);
-    }
+    stage_half_out(a.dL_dsh, base, n, 1, s_sh);
 }
 
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
 {
     if (a.P <= 0) return hipSuccess;
-    const int W3 = a.M * 3;
-    const bool staged = a.shs && a.dL_dsh && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
-                        ((uintptr_t)a.shs % 16) == 0 && ((uintptr_t)a.dL_dsh % 16) == 0;
-    if (staged) {
-        const int stride = W3 | 1;  // odd number of dwords per row: the per-thread row walks are conflict-free
-        hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
-                           256 * stride * sizeof(float), s, a, stride);
-    } else {
-        hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, 0);
-    }
+    const bool staged = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
+                        ((uintptr_t)a.dL_dsh % 16) == 0;
+    if (staged) hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -245,7 +245,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
                                                              const uint32_t* offsets_d, const uint2* sorted_rects,
                                                              uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                                             uint32_t* emit_start, uint8_t* valid, uint2* ranges,
+                                                             uint32_t* emit_start, uint32_t* valid, uint2* ranges,
                                                              int T)
 {
     __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64];
@@ -288,7 +288,7 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
         const uint32_t yy = local / wj, xx = local - yy * wj;
         tile_keys[sl] = (s_y0[w][j] + yy) * gx + (s_x0[w][j] + xx);
         gids[sl] = s_g[w][j];
-        valid[sl] = 0;  // the backward flags the records it writes
+        if ((sl & 31u) == 0u) valid[sl >> 5] = 0u;  // the backward flags the records it writes
     }
 }
 
@@ -394,7 +394,7 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
 
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
                                  uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, uint8_t* valid, uint2* ranges, int T, hipStream_t s)
+                                 uint32_t* emit_start, uint32_t* valid, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,

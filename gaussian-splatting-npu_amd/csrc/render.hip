@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
             const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // emission slot of entry jl
             if ((lane & 1) == 0 && k < G * GF_NUM && g0 + jj < cnt) {
                 a.grad_inst[(size_t)dst * GRAD_REC + (k - jj * GF_NUM)] = r;
-                if (k == jj * GF_NUM) a.valid[dst] = 1;
+                if (k == jj * GF_NUM) atomicOr(&a.valid[dst >> 5], 1u << (dst & 31u));
             }
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
