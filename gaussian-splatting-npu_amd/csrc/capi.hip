@@ -21,6 +21,7 @@ namespace {
 
 thread_local std::string g_err;
 thread_local uint32_t* g_pinned = nullptr;
+constexpr uint32_t L_PENDING = 0xFFFFFFFFu;  // h[2] before the scan stores num_rendered (< 2^31)
 
 int fail(int code, const char* msg)
 {
@@ -214,7 +215,7 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     int rc = pinned(&h);
     if (rc) return rc;
     h[0] = 0;
-    h[2] = 0;
+    __atomic_store_n(&h[2], L_PENDING, __ATOMIC_RELEASE);
     uint32_t* h_dev = nullptr;
     HIP_TRY(hipHostGetDevicePointer((void**)&h_dev, h, 0));
 
@@ -276,8 +277,18 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     DEBUG_SYNC(s);
 
     // 4. the one device->host hand-off of the forward: num_rendered (rasterizer_impl.cu:283-284),
-    //    stored by the scan into pinned memory, plus the error flag
-    HIP_TRY(hipStreamSynchronize(s));
+    //    stored by the scan into pinned memory, plus the error flag.  The host polls the word
+    //    itself (no driver wake-up on the critical path); hipStreamQuery now and then notices a
+    //    stream that failed, or finished without storing it.
+    for (uint32_t spin = 1;; spin++) {
+        if (__atomic_load_n(&h[2], __ATOMIC_ACQUIRE) != L_PENDING) break;
+        if ((spin & 1023u) == 0u) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) break;
+            if (q != hipErrorNotReady) return fail_hip(q, __LINE__);
+        }
+    }
+    if (__atomic_load_n(&h[2], __ATOMIC_ACQUIRE) == L_PENDING) return fail(GSR_ERR_HIP, "scan did not publish num_rendered");
     if (h[0] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (h[2] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
@@ -393,6 +404,30 @@ int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn 
                             debug, stream);
     if (rc) return rc;
     *num_rendered = L;
+    return GSR_OK;
+}
+
+int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binning_buffer, size_t binning_capacity,
+                         int P, int D, int M, const float* background, int width, int height, const float* means3D,
+                         const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                         float tan_fovy, bool prefiltered, bool antialiasing, float* out_color, float* depth,
+                         int* radii, bool debug, gsr_stream_t stream, int* num_rendered, int* rendered)
+{
+    *rendered = 0;
+    int L = 0;
+    int rc = gsr_forward_geometry(geometry_buffer, image_buffer, P, D, M, width, height, means3D, shs, colors_precomp,
+                                  opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                                  cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing, radii, debug, stream, &L);
+    *num_rendered = L;
+    if (rc) return rc;
+    if (P <= 0) return GSR_OK;  // nothing to render: the caller's gsr_forward_render returns at once
+    if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity) return GSR_OK;  // caller allocates
+    rc = gsr_forward_render(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
+                            colors_precomp, out_color, depth, radii, debug, stream);
+    if (rc) return rc;
+    *rendered = 1;
     return GSR_OK;
 }
 

@@ -35,6 +35,9 @@ def _load():
     lib.gsr_forward_geometry.argtypes = [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                          _vp, _vp, _f, _f, _b, _b, _vp, _b, _vp, ctypes.POINTER(_i)]
     lib.gsr_forward_render.argtypes = [_vp, _vp, _vp, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _b, _vp]
+    lib.gsr_forward_prealloc.argtypes = [_vp, _vp, _vp, _sz, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp,
+                                         _vp, _vp, _vp, _vp, _f, _f, _b, _b, _vp, _vp, _vp, _b, _vp,
+                                         ctypes.POINTER(_i), ctypes.POINTER(_i)]
     lib.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
                                  _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp, _b, _b, _vp]
@@ -54,6 +57,11 @@ def _check(rc):
 
 
 _contig_cache = {}  # small non-contiguous inputs (the transposed view matrices) -> contiguous copy
+# Per device: the last forward's num_rendered.  The next forward pre-allocates its binning buffer
+# from it (+25 % and 64K instances of headroom), so the native forward can run emission, sorts and
+# render straight after the num_rendered read-back instead of returning to Python to allocate
+# (the reference's binningBuffer resize lambda, rasterize_points.cu:27-33, rasterizer_impl.cu:286).
+_binning_hint = {}
 
 
 def _contiguous(t):
@@ -129,20 +137,30 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     img = torch.empty((lib.gsr_image_buffer_size(W, H),), dtype=torch.uint8, device=dev)
     stream = _stream(dev)
     nr = ctypes.c_int(0)
+    rendered = ctypes.c_int(0)
+    hint = _binning_hint.get(dev)
+    cap = lib.gsr_binning_buffer_size(min(int(hint * 1.25) + 65536, 0x7FFFFFFF)) if hint is not None else 0
+    binning = torch.empty((cap,), dtype=torch.uint8, device=dev) if cap else None
     bg_p, means_p = p(background, "bg"), p(means3D, "means3D")
     colors_p, op_p = p(colors, "colors_precomp"), p(opacity, "opacities")
     sc_p, rot_p, cov_p = p(scales, "scales"), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp")
     vm_p, pm_p = p(viewmatrix, "viewmatrix"), p(projmatrix, "projmatrix")
     sh_p, cam_p = p(sh, "sh"), p(campos, "campos")
-    _check(lib.gsr_forward_geometry(
-        geom.data_ptr(), img.data_ptr(), P, int(degree), M, W, H, means_p, sh_p, colors_p, op_p, sc_p,
-        float(scale_modifier), rot_p, cov_p, vm_p, pm_p, cam_p, float(tan_fovx), float(tan_fovy),
-        bool(prefiltered), bool(antialiasing), radii.data_ptr(), bool(debug), stream, ctypes.byref(nr)))
+    _check(lib.gsr_forward_prealloc(
+        geom.data_ptr(), img.data_ptr(), binning.data_ptr() if cap else None, cap, P, int(degree), M, bg_p, W, H,
+        means_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p, cov_p, vm_p, pm_p, cam_p,
+        float(tan_fovx), float(tan_fovy), bool(prefiltered), bool(antialiasing), out_color.data_ptr(),
+        out_invdepth.data_ptr(), radii.data_ptr(), bool(debug), stream, ctypes.byref(nr), ctypes.byref(rendered)))
     L = nr.value
-    binning = torch.empty((lib.gsr_binning_buffer_size(L),), dtype=torch.uint8, device=dev)
-    _check(lib.gsr_forward_render(geom.data_ptr(), binning.data_ptr(), img.data_ptr(), P, L, bg_p, W, H, colors_p,
-                                  out_color.data_ptr(), out_invdepth.data_ptr(), radii.data_ptr(), bool(debug),
-                                  stream))
+    _binning_hint[dev] = L
+    need = lib.gsr_binning_buffer_size(L)
+    if rendered.value:
+        binning = binning[:need]  # a view: the backward re-derives the layout from num_rendered
+    else:  # first call on this device, or the scene grew past the headroom
+        binning = torch.empty((need,), dtype=torch.uint8, device=dev)
+        _check(lib.gsr_forward_render(geom.data_ptr(), binning.data_ptr(), img.data_ptr(), P, L, bg_p, W, H,
+                                      colors_p, out_color.data_ptr(), out_invdepth.data_ptr(), radii.data_ptr(),
+                                      bool(debug), stream))
     return L, out_color, radii, geom, binning, img, out_invdepth
 
 

@@ -110,6 +110,24 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
                        const float* colors_precomp, float* out_color, float* depth, int* radii,
                        bool debug, gsr_stream_t stream);
 
+/* Both phases in one call when the caller's binning buffer is already big enough:
+ * gsr_forward_geometry, then, if gsr_binning_buffer_size(*num_rendered) <=
+ * binning_capacity, gsr_forward_render into binning_buffer and *rendered = 1;
+ * otherwise *rendered = 0 and the caller allocates the exact size and calls
+ * gsr_forward_render itself.  Replaces the allocator round trip between the
+ * reference's two halves (binningBuffer resize lambda, rasterizer_impl.cu:286-288)
+ * when the host can guess the size, so the GPU does not idle while the host
+ * allocates. */
+int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binning_buffer,
+                         size_t binning_capacity, int P, int D, int M, const float* background,
+                         int width, int height, const float* means3D, const float* shs,
+                         const float* colors_precomp, const float* opacities, const float* scales,
+                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                         float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing,
+                         float* out_color, float* depth, int* radii, bool debug,
+                         gsr_stream_t stream, int* num_rendered, int* rendered);
+
 /* Replaces Rasterizer::backward (rasterizer.h:57-90; rasterizer_impl.cu:345-450).
  * dL_dinvdepths / dL_dinvdepth may both be NULL (rasterize_points.cu:174-182).
  * Every output is fully written (zeros for culled Gaussians), so unlike the
