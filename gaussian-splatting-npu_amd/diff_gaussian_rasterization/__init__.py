@@ -55,6 +55,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             s.campos, s.prefiltered, s.antialiasing, s.debug)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        # outputs without a gradient (always radii; invdepth when the loss ignores it) arrive as None
+        # instead of zero tensors that autograd would fill with a kernel of its own; backward treats
+        # None as zero
+        ctx.set_materialize_grads(False)
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities,
                               geomBuffer, binningBuffer, imgBuffer)
         return color, radii, invdepths
@@ -64,6 +68,11 @@ class _RasterizeGaussians(torch.autograd.Function):
         s = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geomBuffer,
          binningBuffer, imgBuffer) = ctx.saved_tensors
+        if grad_out_color is None:
+            grad_out_color = torch.zeros((3, s.image_height, s.image_width), dtype=torch.float32,
+                                         device=means3D.device)
+        if grad_out_depth is None:
+            grad_out_depth = torch.Tensor([])  # no invdepth term (rasterize_points.cu:174-182 with zeros)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
          grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(
             s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,

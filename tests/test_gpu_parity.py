@@ -139,6 +139,42 @@ def test_forward_backward_parity(mode, antialiasing):
         assert ok_, f"{mode} aa={antialiasing}: grad {hk} rel err {rel:.3e}"
 
 
+def test_loss_without_invdepth_matches_zero_invdepth_gradient():
+    """A loss that ignores the invdepth output (train.py without a depth prior): autograd hands the
+    backward None for it (no materialised zeros), which must equal the reference's zero dL/dinvdepth."""
+    case = common.make_case()
+    case["grad_invdepth"] = torch.zeros_like(case["grad_invdepth"])
+    o, og = common.run_oracle(case)
+    dgr = _dgr()
+    t, kw = _inputs(case, "sh_scales")
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    color, radii, inv = dgr.GaussianRasterizer(_settings(case))(means2D=means2D, **kw)
+    (color * case["grad_color"].to(DEV)).sum().backward()
+    torch.cuda.synchronize()
+    for hk, ok in {"means3D": "dL_dmeans3D", "shs": "dL_dsh", "opacities": "dL_dopacity", "scales": "dL_dscales",
+                   "rotations": "dL_drotations"}.items():
+        ok_, rel = common.allclose_rel(t[hk].grad.cpu().numpy(), og[ok].reshape(t[hk].shape))
+        assert ok_, f"grad {hk} rel err {rel:.3e}"
+    ok_, rel = common.allclose_rel(means2D.grad.cpu().numpy(), og["dL_dmean2D"])
+    assert ok_, f"grad means2D rel err {rel:.3e}"
+
+
+def test_forward_with_and_without_preallocated_binning():
+    """The forward pre-sizes its binning buffer from the previous call: a first call, a call that
+    outgrows the guess (falls back to an exact allocation) and a call that fits must agree."""
+    dgr = _dgr()
+    small, big = common.make_case(P=300), common.make_case(P=3000)
+    dgr._C._binning_hint.clear()
+    outs = []
+    for case in (big, small, big, big):
+        t, kw = _inputs(case, "sh_scales")
+        with torch.no_grad():
+            color, radii, inv = dgr.GaussianRasterizer(_settings(case))(
+                means2D=torch.zeros_like(t["means3D"]), **kw)
+        outs.append(color.cpu().numpy())
+    assert np.array_equal(outs[0], outs[2]) and np.array_equal(outs[2], outs[3])
+
+
 def test_1080p_view_properties():
     """Full-size view: image/grad parity on a 50k-Gaussian 1080p frame (oracle multi-threaded)."""
     case = common.make_case(P=50000, H=1080, W=1920)
