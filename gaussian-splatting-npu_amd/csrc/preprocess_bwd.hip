@@ -426,39 +426,18 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
     }
 }
 
-// SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's
-// traffic.  STAGED (M = 16): the workgroup's SH rows pass through LDS in two halves of 24
-// floats (coefficients 0-7, then 8-15): coalesced 16-byte loads into rows padded to 25 dwords
-// (an odd stride: the 64 lanes walking their own rows hit 64 different banks), each thread
-// works on its row in place, and the SH gradients leave the same way.  Half rows keep the LDS
-// at 25 KB per workgroup, so LDS no longer caps the occupancy below the register limit.
-constexpr int SH_STRIDE = 25;    // LDS dwords per half row
-
-__device__ __forceinline__ void stage_half_in(const float* shs, int base, int n, int half, float* s_sh)
-{
-    const float4* src = reinterpret_cast<const float4*>(shs + (size_t)base * 48);
-    for (int f = threadIdx.x; f < n * 6; f += 256) {
-        const int g = f / 6, j = f - g * 6;
-        const float4 v = src[g * 12 + half * 6 + j];
-        float* d = &s_sh[g * SH_STRIDE + 4 * j];
-        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-    }
-}
-
-__device__ __forceinline__ void stage_half_out(float* dsh, int base, int n, int half, const float* s_sh)
-{
-    float4* dst = reinterpret_cast<float4*>(dsh + (size_t)base * 48);
-    for (int f = threadIdx.x; f < n * 6; f += 256) {
-        const int g = f / 6, j = f - g * 6;
-        const float* q = &s_sh[g * SH_STRIDE + 4 * j];
-        dst[g * 12 + half * 6 + j] = make_float4(q[0], q[1], q[2], q[3]);
-    }
-}
+// SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's traffic.
+// STAGED (M = 16): the workgroup's 256 rows are read with coalesced 16-byte loads into LDS rows
+// padded to 49 dwords (an odd stride: the 64 lanes walking their own rows hit 64 different
+// banks), each thread works on its row in place, and the SH gradients leave the same way.
+// (Staging in two 24-float halves halves the LDS and raises occupancy, but measured 3 % slower:
+// most 128-B lines of a row are then fetched in both halves.)
+constexpr int SH_STRIDE = 49;  // LDS dwords per row (odd)
 
 template <bool STAGED>
 __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a)
 {
-    __shared__ float s_sh[STAGED ? 256 * SH_STRIDE : 1];
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
     BwdIn in;
@@ -478,24 +457,27 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         return;
     }
     const int n = min(256, a.P - base);
-    stage_half_in(a.shs, base, n, 0, s_sh);
+    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
+    for (int f = threadIdx.x; f < n * 12; f += 256) {
+        const int g = f / 12, j = f - g * 12;
+        const float4 v = src[f];
+        float* d = &s_sh[g * SH_STRIDE + 4 * j];
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
     __syncthreads();
     float* row = s_sh + threadIdx.x * SH_STRIDE;
     if (idx < a.P) {
         bwd_core(a, idx, in, st);
-        sh_bwd_range<0, 8>(st, row, row);
-    }
-    __syncthreads();
-    stage_half_out(a.dL_dsh, base, n, 0, s_sh);
-    __syncthreads();
-    stage_half_in(a.shs, base, n, 1, s_sh);
-    __syncthreads();
-    if (idx < a.P) {
-        sh_bwd_range<8, 16>(st, row, row);
+        sh_bwd_range<0, 16>(st, row, row);
         bwd_finish(a, idx, st);
     }
     __syncthreads();
-    stage_half_out(a.dL_dsh, base, n, 1, s_sh);
+    float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48);
+    for (int f = threadIdx.x; f < n * 12; f += 256) {
+        const int g = f / 12, j = f - g * 12;
+        const float* q = &s_sh[g * SH_STRIDE + 4 * j];
+        dst[f] = make_float4(q[0], q[1], q[2], q[3]);
+    }
 }
 
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
@@ -503,7 +485,8 @@ hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
     if (a.P <= 0) return hipSuccess;
     const bool staged = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
                         ((uintptr_t)a.dL_dsh % 16) == 0;
-    if (staged) hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    if (staged)
+        hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 256 * SH_STRIDE * 4, s, a);
     else hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
