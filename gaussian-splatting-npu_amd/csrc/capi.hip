@@ -188,8 +188,8 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 }
 
 
-int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
-                         const float* means3D, const float* shs, const float* colors_precomp,
+int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
+                         const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                          const float* opacities, const float* scales, float scale_modifier,
                          const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                          const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
@@ -200,8 +200,10 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
     *num_rendered = 0;
     if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
     if (width <= 0 || height <= 0) return fail(GSR_ERR_INVALID, "image size must be positive");
-    if (!colors_precomp && (!shs || M <= 0))
+    if (!colors_precomp && !dc && (!shs || M <= 0))
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
+    if (dc && M < 0) return fail(GSR_ERR_INVALID, "M (rest SH coefficients) must be >= 0");
+    if (dc && M > 0 && !shs) return fail(GSR_ERR_INVALID, "dc given with M > 0 rest coefficients but shs is NULL");
     if (!cov3D_precomp && (!scales || !rotations))
         return fail(GSR_ERR_INVALID,
                     "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
@@ -221,7 +223,8 @@ int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D
 
     // 1. preprocess (forward.cu:154-272)
     PreprocessArgs a;
-    a.P = P; a.D = D; a.M = M; a.W = width; a.H = height;
+    a.P = P; a.D = D; a.M = dc ? M + 1 : M; a.W = width; a.H = height;  // kernels count the dc coefficient
+    a.dc = dc;
     a.means3D = means3D; a.scales = scales; a.scale_modifier = scale_modifier; a.rotations = rotations;
     a.opacities = opacities; a.shs = shs; a.cov3D_precomp = cov3D_precomp; a.colors_precomp = colors_precomp;
     a.view = viewmatrix; a.proj = projmatrix; a.campos = cam_pos;
@@ -380,9 +383,9 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     return GSR_OK;
 }
 
-int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn binningBuffer, void* binning_ctx,
+int gsr_forward_dc(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn binningBuffer, void* binning_ctx,
                 gsr_resize_fn imageBuffer, void* image_ctx, int P, int D, int M, const float* background, int width,
-                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                int height, const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                 const float* opacities, const float* scales, float scale_modifier, const float* rotations,
                 const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
                 float tan_fovx, float tan_fovy, bool prefiltered, float* out_color, float* depth, bool antialiasing,
@@ -394,7 +397,7 @@ int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn 
     char* ib = imageBuffer(image_ctx, gsr_image_buffer_size(width, height));
     if (!gb || !ib) return fail(GSR_ERR_ALLOC, "resize callback returned NULL");
     int L = 0;
-    int rc = gsr_forward_geometry(gb, ib, P, D, M, width, height, means3D, shs, colors_precomp, opacities, scales,
+    int rc = gsr_forward_geometry_dc(gb, ib, P, D, M, width, height, means3D, dc, shs, colors_precomp, opacities, scales,
                                   scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx,
                                   tan_fovy, prefiltered, antialiasing, radii, debug, stream, &L);
     if (rc) return rc;
@@ -407,9 +410,9 @@ int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn 
     return GSR_OK;
 }
 
-int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binning_buffer, size_t binning_capacity,
+int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* binning_buffer, size_t binning_capacity,
                          int P, int D, int M, const float* background, int width, int height, const float* means3D,
-                         const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                         const float* dc, const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
                          const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
                          float tan_fovy, bool prefiltered, bool antialiasing, float* out_color, float* depth,
@@ -417,7 +420,7 @@ int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binnin
 {
     *rendered = 0;
     int L = 0;
-    int rc = gsr_forward_geometry(geometry_buffer, image_buffer, P, D, M, width, height, means3D, shs, colors_precomp,
+    int rc = gsr_forward_geometry_dc(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs, colors_precomp,
                                   opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
                                   cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing, radii, debug, stream, &L);
     *num_rendered = L;
@@ -431,15 +434,17 @@ int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binnin
     return GSR_OK;
 }
 
-int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
-                 const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+int gsr_backward_dc(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* dc, const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
                  float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                  const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
                  char* geom_buffer, char* binning_buffer, char* image_buffer, const float* dL_dpix,
                  const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
-                 float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale,
                  float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
 {
+    if (dc && !dL_ddc) return fail(GSR_ERR_INVALID, "dc given without dL_ddc");
+    if (dc && M > 0 && (!shs || !dL_dsh)) return fail(GSR_ERR_INVALID, "dc given with M > 0 but shs/dL_dsh NULL");
     (void)colors_precomp;
     hipStream_t s = (hipStream_t)stream;
     if (P <= 0) return GSR_OK;
@@ -488,8 +493,8 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
 
     // BACKWARD::preprocess (rasterizer_impl.cu:423-449), with the per-Gaussian gather of the records
     PreprocessBwdArgs p;
-    p.P = P; p.D = D; p.M = M;
-    p.means3D = means3D; p.radii = rad; p.shs = shs;
+    p.P = P; p.D = D; p.M = dc ? M + 1 : M;
+    p.means3D = means3D; p.radii = rad; p.shs = shs; p.dc = dc; p.dL_ddc = dc ? dL_ddc : nullptr;
     p.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
     p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
     p.cov3D_precomp = cov3D_precomp;
@@ -515,6 +520,82 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         HIP_TRY(launch_preprocess_bwd(p, s));
     }
     DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+// ---- the non-dc entry points: the reference's Rasterizer API (rasterizer.h:31-90) ----
+int gsr_forward_geometry(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
+                         const float* means3D, const float* shs, const float* colors_precomp,
+                         const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                         bool prefiltered, bool antialiasing, int* radii, bool debug, gsr_stream_t stream,
+                         int* num_rendered)
+{
+    return gsr_forward_geometry_dc(geometry_buffer, image_buffer, P, D, M, width, height, means3D, nullptr, shs,
+                                   colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                   viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                   radii, debug, stream, num_rendered);
+}
+
+int gsr_forward(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_fn binningBuffer, void* binning_ctx,
+                gsr_resize_fn imageBuffer, void* image_ctx, int P, int D, int M, const float* background, int width,
+                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                float tan_fovx, float tan_fovy, bool prefiltered, float* out_color, float* depth, bool antialiasing,
+                int* radii, bool debug, gsr_stream_t stream, int* num_rendered)
+{
+    return gsr_forward_dc(geometryBuffer, geometry_ctx, binningBuffer, binning_ctx, imageBuffer, image_ctx, P, D, M,
+                          background, width, height, means3D, nullptr, shs, colors_precomp, opacities, scales,
+                          scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx,
+                          tan_fovy, prefiltered, out_color, depth, antialiasing, radii, debug, stream, num_rendered);
+}
+
+int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binning_buffer, size_t binning_capacity,
+                         int P, int D, int M, const float* background, int width, int height, const float* means3D,
+                         const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                         float tan_fovy, bool prefiltered, bool antialiasing, float* out_color, float* depth,
+                         int* radii, bool debug, gsr_stream_t stream, int* num_rendered, int* rendered)
+{
+    return gsr_forward_prealloc_dc(geometry_buffer, image_buffer, binning_buffer, binning_capacity, P, D, M,
+                                   background, width, height, means3D, nullptr, shs, colors_precomp, opacities,
+                                   scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos,
+                                   tan_fovx, tan_fovy, prefiltered, antialiasing, out_color, depth, radii, debug,
+                                   stream, num_rendered, rendered);
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
+                 float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                 char* geom_buffer, char* binning_buffer, char* image_buffer, const float* dL_dpix,
+                 const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                 float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
+{
+    return gsr_backward_dc(P, D, M, R, background, width, height, means3D, nullptr, shs, colors_precomp, opacities,
+                           scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx,
+                           tan_fovy, radii, geom_buffer, binning_buffer, image_buffer, dL_dpix, dL_invdepths,
+                           dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D, dL_dcov3D, nullptr,
+                           dL_dsh, dL_dscale, dL_drot, antialiasing, debug, stream);
+}
+
+// ---- sparse Adam (adam.hip) ----
+int gsr_adam_update(float* param, const float* param_grad, float* exp_avg, float* exp_avg_sq, const bool* visible,
+                    float lr, float b1, float b2, float eps, int N, int M, gsr_stream_t stream)
+{
+    if (N < 0 || M < 0) return fail(GSR_ERR_INVALID, "N and M must be >= 0");
+    if ((size_t)N * M == 0) return GSR_OK;
+    if ((size_t)N * M >= 0xFFFFFFF0ull) return fail(GSR_ERR_INVALID, "N*M must be < 2^32");
+    if (!param || !param_grad || !exp_avg || !exp_avg_sq || !visible) return fail(GSR_ERR_INVALID, "null pointer");
+    AdamArgs a;
+    a.param = param; a.grad = param_grad; a.exp_avg = exp_avg; a.exp_avg_sq = exp_avg_sq;
+    a.visible = reinterpret_cast<const uint8_t*>(visible);
+    a.lr = lr; a.b1 = b1; a.b2 = b2; a.eps = eps; a.N = N; a.M = M;
+    HIP_TRY(launch_adam_update(a, (hipStream_t)stream));
     return GSR_OK;
 }
 

@@ -244,6 +244,68 @@ inline BinLayout bin_layout(int L)
     return l;
 }
 
+// ---------------------------------------------------------------------------
+// Separate-DC SH layout (the `dc=` input of the accelerated upstream rasterizer that
+// train.py selects with SparseGaussianAdam, train.py:37-41, gaussian_renderer/__init__.py:82-100):
+// coefficient 0 lives in dc (P,1,3), coefficients 1.. in a (P,M-1,3) "rest" array.  Both
+// preprocess kernels stage a workgroup's 256 SH rows through LDS; these helpers move a block
+// of rows of `w` floats between a global array and LDS columns [col0, col0 + w) of rows of
+// `stride` dwords, coalesced (16-byte accesses when the array is 16-byte aligned -- a block
+// of 256 rows starts at a multiple of 1 KB, so alignment of the array is alignment of the
+// block), dropping (in) / zero-filling (out) columns at or beyond `ncols`.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, int ncols, const float* src, int w,
+                                            int n)
+{
+    const int total = n * w;
+    int e0 = 0;
+    if (((uintptr_t)src & 15) == 0) {
+        const int nv4 = total >> 2;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        for (int f = threadIdx.x; f < nv4; f += blockDim.x) {
+            const float4 v = s4[f];
+            const float vv[4] = {v.x, v.y, v.z, v.w};
+            int g = (4 * f) / w, j = 4 * f - g * w;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (col0 + j < ncols) lds[g * stride + col0 + j] = vv[q];
+                if (++j == w) { j = 0; g++; }
+            }
+        }
+        e0 = nv4 << 2;
+    }
+    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) {
+        const int g = e / w, j = e - g * w;
+        if (col0 + j < ncols) lds[g * stride + col0 + j] = src[e];
+    }
+}
+
+__device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const float* lds, int stride, int col0,
+                                             int ncols)
+{
+    const int total = n * w;
+    int e0 = 0;
+    if (((uintptr_t)dst & 15) == 0) {
+        const int nv4 = total >> 2;
+        float4* d4 = reinterpret_cast<float4*>(dst);
+        for (int f = threadIdx.x; f < nv4; f += blockDim.x) {
+            float vv[4];
+            int g = (4 * f) / w, j = 4 * f - g * w;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                vv[q] = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
+                if (++j == w) { j = 0; g++; }
+            }
+            d4[f] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+        e0 = nv4 << 2;
+    }
+    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) {
+        const int g = e / w, j = e - g * w;
+        dst[e] = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
+    }
+}
+
 // Reference getHigherMsb (rasterizer_impl.cu:35-50)
 inline uint32_t higher_msb(uint32_t n)
 {

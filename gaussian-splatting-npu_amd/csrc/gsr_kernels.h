@@ -12,7 +12,8 @@ struct PreprocessArgs {
     float scale_modifier;
     const float* rotations;
     const float* opacities;
-    const float* shs;
+    const float* shs;  // (P,M,3); with dc: the (P,M-1,3) rest coefficients (M counts the dc one)
+    const float* dc;   // separate coefficient 0 (P,1,3), or null
     const float* cov3D_precomp;
     const float* colors_precomp;
     const float* view;
@@ -86,7 +87,8 @@ struct PreprocessBwdArgs {
     int P, D, M;
     const float* means3D;
     const int* radii;
-    const float* shs;
+    const float* shs;  // as PreprocessArgs: with dc, the rest coefficients and M counts dc
+    const float* dc;
     const uint8_t* clamped;
     const float* opacities;
     const float* scales;
@@ -116,9 +118,21 @@ struct PreprocessBwdArgs {
     float* dL_dmean3D;
     float* dL_dcov3D;
     float* dL_dsh;
+    float* dL_ddc;  // (P,1,3) when dc is given
     float* dL_dscale;
     float* dL_drot;
 };
+
+struct AdamArgs {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    const uint8_t* visible;  // one flag per Gaussian (bool)
+    float lr, b1, b2, eps;
+    int N, M;  // N Gaussians of M elements each
+};
+hipError_t launch_adam_update(const AdamArgs& a, hipStream_t s);
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);

@@ -201,6 +201,15 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
         if (idx < a.P) preprocess_one(a, idx, a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr);
         return;
     }
+    if (a.dc) {  // separate dc: coefficient 0 into columns 0-2, the rest after it (at most 16 used)
+        const int n = min(256, a.P - base), ncols = min(a.M, 16) * 3;
+        lds_rows_in(s_sh, lds_stride, 0, ncols, a.dc + (size_t)base * 3, 3, n);
+        if (a.shs && a.M > 1) lds_rows_in(s_sh, lds_stride, 3, ncols, a.shs + (size_t)base * (a.M - 1) * 3,
+                                          (a.M - 1) * 3, n);
+        __syncthreads();
+        if (idx < a.P) preprocess_one(a, idx, s_sh + threadIdx.x * lds_stride);
+        return;
+    }
     const int W3 = a.M * 3;  // multiple of 4 on this path
     const int nv4 = min(256, a.P - base) * (W3 / 4);
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
@@ -342,7 +351,11 @@ hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
     const int W3 = a.M * 3;
     const bool staged = a.shs && !a.colors_precomp && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
                         ((uintptr_t)a.shs % 16) == 0;
-    if (staged) {
+    if (a.dc && !a.colors_precomp) {  // separate dc: always staged (any M, any alignment)
+        const int stride = (min(a.M, 16) * 3) | 1;
+        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
+                           256 * stride * sizeof(float), s, a, stride);
+    } else if (staged) {
         const int stride = W3 | 1;
         hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
                            256 * stride * sizeof(float), s, a, stride);

@@ -147,8 +147,9 @@ __device__ __forceinline__ void sh_term(int k, float x, float y, float z, float&
 // dL/dsh_k = b_k * dRGB, and the view-direction gradient accumulated into st.ddir.  `sh` / `dsh`
 // point at coefficient K0 of this Gaussian (global memory or its LDS staging row; they may be
 // the same row: every coefficient is read before it is overwritten).
+// Coefficients at or beyond `kw` (the row width in coefficients) are not written.
 template <int K0, int K1>
-__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh)
+__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh, int kw = K1)
 {
 #pragma unroll
     for (int k = K0; k < K1; k++) {
@@ -164,7 +165,7 @@ __device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, floa
                 st.ddir[1] += t * gy;
                 st.ddir[2] += t * gz;
             }
-        } else {
+        } else if (k < kw) {
 #pragma unroll
             for (int c = 0; c < 3; c++) dsh[(k - K0) * 3 + c] = 0.f;
         }
@@ -364,7 +365,7 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
     st.dmz = dmz;
 
     // ---------------- computeColorFromSH backward: set-up (backward.cu:28-49) ----------------
-    if (a.shs) {
+    if (a.shs || a.dc) {
         const int deg = a.D;
         int nc = (deg + 1) * (deg + 1);
         nc = nc < a.M ? nc : a.M;
@@ -449,7 +450,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             if (a.dL_dsh) {
                 const size_t w3 = (size_t)a.M * 3;
                 float* dsh = a.dL_dsh + idx * w3;
-                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh);  // ncoef <= M: no read past the row
+                // ncoef <= M: no read past the row; no write past it either (M < 16)
+                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M);
                 for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
             }
             bwd_finish(a, idx, st);
@@ -457,6 +459,22 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         return;
     }
     const int n = min(256, a.P - base);
+    if (a.dc) {  // separate dc (train.py's sparse-Adam layout): dc -> columns 0-2, rest -> 3..47
+        const int wr = (a.M - 1) * 3;
+        lds_rows_in(s_sh, SH_STRIDE, 0, 48, a.dc + (size_t)base * 3, 3, n);
+        if (a.shs && wr > 0) lds_rows_in(s_sh, SH_STRIDE, 3, 48, a.shs + (size_t)base * wr, wr, n);
+        __syncthreads();
+        float* row = s_sh + threadIdx.x * SH_STRIDE;
+        if (idx < a.P) {
+            bwd_core(a, idx, in, st);
+            sh_bwd_range<0, 16>(st, row, row);
+            bwd_finish(a, idx, st);
+        }
+        __syncthreads();
+        lds_rows_out(a.dL_ddc + (size_t)base * 3, 3, n, s_sh, SH_STRIDE, 0, 48);
+        if (a.dL_dsh && wr > 0) lds_rows_out(a.dL_dsh + (size_t)base * wr, wr, n, s_sh, SH_STRIDE, 3, 48);
+        return;
+    }
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
     for (int f = threadIdx.x; f < n * 12; f += 256) {
         const int g = f / 12, j = f - g * 12;
@@ -485,7 +503,7 @@ hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
     if (a.P <= 0) return hipSuccess;
     const bool staged = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
                         ((uintptr_t)a.dL_dsh % 16) == 0;
-    if (staged)
+    if (staged || (a.dc && a.dL_ddc))
         hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 256 * SH_STRIDE * 4, s, a);
     else hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();

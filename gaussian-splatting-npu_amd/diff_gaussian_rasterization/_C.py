@@ -41,6 +41,13 @@ def _load():
     lib.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp,
                                  _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                  _vp, _b, _b, _vp]
+    lib.gsr_forward_prealloc_dc.argtypes = [_vp, _vp, _vp, _sz, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _b, _b, _vp, _vp, _vp, _b, _vp,
+                                            ctypes.POINTER(_i), ctypes.POINTER(_i)]
+    lib.gsr_backward_dc.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
+                                    _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp, _b, _b, _vp]
+    lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
     for n in ("gsr_geometry_layout", "gsr_binning_layout"):
         getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
@@ -105,10 +112,19 @@ def _require_gpu(t):
                            f"{t.device}. There is no CPU path.")
 
 
+def _sh_split(sh, dc):
+    """(M, has_dc): M = sh.size(1) -- with dc, the number of REST coefficients (0 if sh is empty)."""
+    M = sh.size(1) if sh is not None and sh.numel() != 0 and sh.size(0) != 0 else 0
+    has_dc = dc is not None and dc.numel() != 0
+    return M, has_dc
+
+
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, antialiasing, debug):
-    """RasterizeGaussiansNPU (rasterize_points.cu:35-124)."""
+                        prefiltered, antialiasing, debug, dc=None):
+    """RasterizeGaussiansNPU (rasterize_points.cu:35-124).  `dc` (P,1,3): the separate-DC form of
+    the accelerated upstream op (coefficient 0 apart from the rest in `sh`), selected by train.py
+    together with SparseGaussianAdam (train.py:37-41, gaussian_renderer/__init__.py:82-100)."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     _require_gpu(means3D)
@@ -125,7 +141,9 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     radii = torch.empty((P,), dtype=torch.int32, device=dev)
     out_invdepth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
     out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
-    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    M, has_dc = _sh_split(sh, dc)
+    if has_dc and (dc.dim() != 3 or dc.size(0) != P or dc.size(1) != 1 or dc.size(2) != 3):
+        raise RuntimeError("dc must have dimensions (num_points, 1, 3)")
     keep = []
 
     def p(t, name):
@@ -146,9 +164,10 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     sc_p, rot_p, cov_p = p(scales, "scales"), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp")
     vm_p, pm_p = p(viewmatrix, "viewmatrix"), p(projmatrix, "projmatrix")
     sh_p, cam_p = p(sh, "sh"), p(campos, "campos")
-    _check(lib.gsr_forward_prealloc(
+    dc_p = p(dc, "dc") if has_dc else None
+    _check(lib.gsr_forward_prealloc_dc(
         geom.data_ptr(), img.data_ptr(), binning.data_ptr() if cap else None, cap, P, int(degree), M, bg_p, W, H,
-        means_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p, cov_p, vm_p, pm_p, cam_p,
+        means_p, dc_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p, cov_p, vm_p, pm_p, cam_p,
         float(tan_fovx), float(tan_fovy), bool(prefiltered), bool(antialiasing), out_color.data_ptr(),
         out_invdepth.data_ptr(), radii.data_ptr(), bool(debug), stream, ctypes.byref(nr), ctypes.byref(rendered)))
     L = nr.value
@@ -167,13 +186,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                  dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                 antialiasing, debug):
-    """RasterizeGaussiansBackwardNPU (rasterize_points.cu:126-223)."""
+                                 antialiasing, debug, dc=None):
+    """RasterizeGaussiansBackwardNPU (rasterize_points.cu:126-223).  With `dc` (the separate-DC
+    form) the result carries dL_ddc (P,1,3) before dL_dsh, as the accelerated upstream op returns
+    it: (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
+    dL_drotations)."""
     _require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
-    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    M, has_dc = _sh_split(sh, dc)
     # Render-pass gradients (one allocation): mean2D 3 | colors 3 | conic 4 | invdepth 1.
     # The HIP backward writes every element (no atomics, no pre-zeroing needed).
     acc = torch.empty((P * 11,), dtype=torch.float32, device=dev)
@@ -186,16 +208,25 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     # buffer laid out as multiview.PARAM_ORDER (means3D | sh | opacity | scales | rotations) then
     # cov3D: autograd keeps these views as the leaves' .grad, so a multi-GPU step all-reduces the
     # buffer in place instead of gathering and scattering 236 B per Gaussian around the collective.
-    sizes = [3 * P, 3 * M * P, P, 3 * P, 4 * P, 6 * P]
+    # With dc, its gradient sits between means3D and the rest (multiview.PARAM_ORDER_DC).
+    sizes = [3 * P, 3 * P if has_dc else 0, 3 * M * P, P, 3 * P, 4 * P, 6 * P]
     parts = torch.split(torch.empty((sum(sizes),), dtype=torch.float32, device=dev), sizes)
     dL_dmeans3D = parts[0].view(P, 3)
-    dL_dsh = parts[1].view(P, M, 3)
-    dL_dopacity = parts[2].view(P, 1)
-    dL_dscales = parts[3].view(P, 3)
-    dL_drotations = parts[4].view(P, 4)
-    dL_dcov3D = parts[5].view(P, 6)
-    if P == 0:
+    dL_ddc = parts[1].view(P, 1, 3) if has_dc else None
+    dL_dsh = parts[2].view(P, M, 3)
+    dL_dopacity = parts[3].view(P, 1)
+    dL_dscales = parts[4].view(P, 3)
+    dL_drotations = parts[5].view(P, 4)
+    dL_dcov3D = parts[6].view(P, 6)
+
+    def result():
+        if has_dc:
+            return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
+                    dL_drotations)
         return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+    if P == 0:
+        return result()
 
     keep = []
 
@@ -206,17 +237,36 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
 
     dpix = p(dL_dout_color, "dL_dout_color")
     dinv = p(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None
-    _check(lib.gsr_backward(
-        P, int(degree), M, int(R), p(background, "bg"), W, H, p(means3D, "means3D"), p(sh, "sh"),
+    _check(lib.gsr_backward_dc(
+        P, int(degree), M, int(R), p(background, "bg"), W, H, p(means3D, "means3D"),
+        p(dc, "dc") if has_dc else None, p(sh, "sh"),
         p(colors, "colors_precomp"), p(opacities, "opacities"), p(scales, "scales"), float(scale_modifier),
         p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp"), p(viewmatrix, "viewmatrix"),
         p(projmatrix, "projmatrix"), p(campos, "campos"), float(tan_fovx), float(tan_fovy), radii.data_ptr(),
         geomBuffer.data_ptr(), binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
         dpix, dinv, dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(), dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
         dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
-        dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(), bool(antialiasing),
-        bool(debug), _stream(dev)))
-    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+        dL_ddc.data_ptr() if has_dc else None, dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(),
+        dL_drotations.data_ptr(), bool(antialiasing), bool(debug), _stream(dev)))
+    return result()
+
+
+def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M):
+    """The accelerated upstream's `_C.adamUpdate` (called by SparseGaussianAdam.step): Adam on the
+    rows of the N Gaussians with visible[i] set (M elements each), in place; no bias correction."""
+    _require_gpu(param)
+    dev = param.device
+    for name, t in (("param", param), ("param_grad", param_grad), ("exp_avg", exp_avg), ("exp_avg_sq", exp_avg_sq)):
+        if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
+            raise RuntimeError(f"adamUpdate: {name} must be a contiguous float32 tensor on {dev}")
+        if t.numel() != int(N) * int(M):
+            raise RuntimeError(f"adamUpdate: {name} has {t.numel()} elements, expected N*M = {int(N) * int(M)}")
+    if visible.device != dev or visible.dtype != torch.bool or visible.numel() != int(N):
+        raise RuntimeError(f"adamUpdate: visible must be a bool tensor of N = {int(N)} flags on {dev}")
+    visible = visible.contiguous()
+    _check(lib.gsr_adam_update(param.data_ptr(), param_grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                               visible.data_ptr(), float(lr), float(b1), float(b2), float(eps), int(N), int(M),
+                               _stream(dev)))
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

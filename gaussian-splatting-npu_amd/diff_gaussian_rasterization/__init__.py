@@ -4,9 +4,12 @@ Public surface kept verbatim from diff-gaussian-rasterization-npu/diff_gaussian_
 __init__.py: ``GaussianRasterizationSettings`` (:143-156), ``GaussianRasterizer`` (:158-207),
 ``rasterize_gaussians`` (:21-42) and the autograd function ``_RasterizeGaussians`` (:44-141), so
 ``gaussian_renderer/__init__.py`` (and therefore train.py / render.py) import and call it
-unchanged.  ``SparseGaussianAdam`` is deliberately not exported (the caller would
-then pass a ``dc=`` argument this surface does not take).  All compute is the HIP library
-behind ``_C`` (gfx950); there is no CPU path.
+unchanged.  It also carries the accelerated upstream surface that train.py switches to when the
+package exports ``SparseGaussianAdam`` (train.py:37-41, 180-183): ``GaussianRasterizer.forward``
+takes ``dc=`` (SH coefficient 0 apart from the rest, gaussian_renderer/__init__.py:82-100) and
+``SparseGaussianAdam.step(visibility, N)`` updates only visible Gaussians
+(scene/gaussian_model.py:194-196).  All compute is the HIP library behind ``_C`` (gfx950); there is
+no CPU path.
 """
 from typing import NamedTuple
 
@@ -15,7 +18,7 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam"]
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -35,24 +38,25 @@ class GaussianRasterizationSettings(NamedTuple):
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                        raster_settings):
+                        raster_settings, dc=None):
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                                     cov3Ds_precomp, raster_settings)
+                                     cov3Ds_precomp, raster_settings, dc)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     """Forward returns (color (3,H,W), radii int32 (P), invdepth (1,H,W)); backward returns the
-    nine input gradients in input order, with d(means2D) = the screen-space gradient (P,3)
-    that the caller's densification statistics read (scene/gaussian_model.py:471-473)."""
+    input gradients in input order, with d(means2D) = the screen-space gradient (P,3)
+    that the caller's densification statistics read (scene/gaussian_model.py:471-473).  The last
+    input, ``dc`` (None unless the separate-DC surface is used), gets its own gradient."""
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings):
+                raster_settings, dc=None):
         s = raster_settings
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepths = _C.rasterize_gaussians(
             s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
-            s.campos, s.prefiltered, s.antialiasing, s.debug)
+            s.campos, s.prefiltered, s.antialiasing, s.debug, dc=dc)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
         # outputs without a gradient (always radii; invdepth when the loss ignores it) arrive as None
@@ -60,26 +64,32 @@ class _RasterizeGaussians(torch.autograd.Function):
         # None as zero
         ctx.set_materialize_grads(False)
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities,
-                              geomBuffer, binningBuffer, imgBuffer)
+                              geomBuffer, binningBuffer, imgBuffer, dc)
         return color, radii, invdepths
 
     @staticmethod
     def backward(ctx, grad_out_color, _grad_radii, grad_out_depth):
         s = ctx.raster_settings
         (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, geomBuffer,
-         binningBuffer, imgBuffer) = ctx.saved_tensors
+         binningBuffer, imgBuffer, dc) = ctx.saved_tensors
         if grad_out_color is None:
             grad_out_color = torch.zeros((3, s.image_height, s.image_width), dtype=torch.float32,
                                          device=means3D.device)
         if grad_out_depth is None:
             grad_out_depth = torch.Tensor([])  # no invdepth term (rasterize_points.cu:174-182 with zeros)
-        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
-         grad_scales, grad_rotations) = _C.rasterize_gaussians_backward(
+        grads = _C.rasterize_gaussians_backward(
             s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth, sh, s.sh_degree,
-            s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug)
+            s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug, dc=dc)
+        if len(grads) == 9:
+            (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
+             grad_scales, grad_rotations) = grads
+        else:
+            (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+             grad_scales, grad_rotations) = grads
+            grad_dc = None
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                grad_rotations, grad_cov3Ds_precomp, None)
+                grad_rotations, grad_cov3Ds_precomp, None, grad_dc)
 
 
 class GaussianRasterizer(nn.Module):
@@ -94,7 +104,9 @@ class GaussianRasterizer(nn.Module):
             return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
 
     def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-                cov3D_precomp=None):
+                cov3D_precomp=None, dc=None):
+        """``dc`` (P,1,3), keyword only in practice (gaussian_renderer/__init__.py:91-100): SH
+        coefficient 0, with ``shs`` then holding coefficients 1.. (features_rest)."""
         s = self.raster_settings
         if (shs is None) == (colors_precomp is None):
             raise Exception('Please provide excatly one of either SHs or precomputed colors!')
@@ -110,4 +122,37 @@ class GaussianRasterizer(nn.Module):
             absent if scales is None else scales,
             absent if rotations is None else rotations,
             absent if cov3D_precomp is None else cov3D_precomp,
-            s)
+            s, dc)
+
+
+class SparseGaussianAdam(torch.optim.Adam):
+    """Adam that updates only the rows of visible Gaussians (train.py:180-183:
+    ``optimizer.step(radii > 0, radii.shape[0])``; constructed as ``SparseGaussianAdam(l, lr=0.0,
+    eps=1e-15)``, scene/gaussian_model.py:194-196).  One parameter tensor per group, as the
+    caller's per-attribute groups are; state keeps torch.optim.Adam's keys (``exp_avg``,
+    ``exp_avg_sq``, ``step``), so GaussianModel's densification surgery on ``optimizer.state``
+    (gaussian_model.py:316-400) works unchanged.  The update is the published upstream one:
+    betas fixed at (0.9, 0.999), no bias correction; each group is one HIP launch
+    (``_C.adamUpdate``)."""
+
+    def __init__(self, params, lr, eps):
+        super().__init__(params=params, lr=lr, eps=eps)
+
+    @torch.no_grad()
+    def step(self, visibility, N):
+        for group in self.param_groups:
+            lr = group["lr"]
+            eps = group["eps"]
+            if len(group["params"]) != 1:
+                raise AssertionError("more than one tensor in group")
+            param = group["params"][0]
+            if param.grad is None:
+                continue
+            state = self.state[param]
+            if len(state) == 0:
+                state["step"] = torch.tensor(0.0, dtype=torch.float32)
+                state["exp_avg"] = torch.zeros_like(param, memory_format=torch.preserve_format)
+                state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
+            M = param.numel() // N
+            _C.adamUpdate(param, param.grad, state["exp_avg"], state["exp_avg_sq"], visibility, lr, 0.9, 0.999,
+                          eps, N, M)

@@ -15,6 +15,8 @@ import torch.distributed as dist
 
 # parameter order of the bucket (xyz, features, opacity, scaling, rotation)
 PARAM_ORDER = ("means3D", "shs", "opacities", "scales", "rotations")
+# the same with the separate-DC surface (features_dc apart from features_rest)
+PARAM_ORDER_DC = ("means3D", "dc", "shs", "opacities", "scales", "rotations")
 
 
 def views_for_rank(rank, world, views_per_rank=1, n_views=8):

@@ -171,6 +171,68 @@ int gsr_backward(int P, int D, int M, int R,
                  bool debug,
                  gsr_stream_t stream);
 
+/* Separate-DC ("dc=") forms of the four entry points above: the accelerated
+ * upstream rasterizer's Rasterizer::forward/backward, which take `dc` (P,1,3,
+ * SH coefficient 0) and `shs` (P,M,3, coefficients 1..M) as two arrays and
+ * return dL_ddc / dL_dsh separately.  train.py picks that surface whenever the
+ * package exports SparseGaussianAdam (train.py:37-41 -> gaussian_renderer/
+ * __init__.py:82-100, rasterizer(dc=features_dc, shs=features_rest)), which
+ * saves the caller's torch.cat of the two parameter tensors (192 B/Gaussian
+ * written and read again) and the split of its gradient.  Here M counts the
+ * rest coefficients only (sh.size(1) of features_rest; 15 at degree 3) and may
+ * be 0 with shs NULL; dc NULL makes each call identical to its non-dc form. */
+int gsr_forward_dc(gsr_resize_fn geometryBuffer, void* geometry_ctx,
+                   gsr_resize_fn binningBuffer, void* binning_ctx,
+                   gsr_resize_fn imageBuffer, void* image_ctx,
+                   int P, int D, int M, const float* background, int width, int height,
+                   const float* means3D, const float* dc, const float* shs,
+                   const float* colors_precomp, const float* opacities, const float* scales,
+                   float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                   const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                   float tan_fovx, float tan_fovy, bool prefiltered, float* out_color, float* depth,
+                   bool antialiasing, int* radii, bool debug, gsr_stream_t stream, int* num_rendered);
+
+int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer,
+                            int P, int D, int M, int width, int height,
+                            const float* means3D, const float* dc, const float* shs,
+                            const float* colors_precomp, const float* opacities, const float* scales,
+                            float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                            const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                            float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing,
+                            int* radii, bool debug, gsr_stream_t stream, int* num_rendered);
+
+int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* binning_buffer,
+                            size_t binning_capacity, int P, int D, int M, const float* background,
+                            int width, int height, const float* means3D, const float* dc,
+                            const float* shs, const float* colors_precomp, const float* opacities,
+                            const float* scales, float scale_modifier, const float* rotations,
+                            const float* cov3D_precomp, const float* viewmatrix,
+                            const float* projmatrix, const float* cam_pos, float tan_fovx,
+                            float tan_fovy, bool prefiltered, bool antialiasing, float* out_color,
+                            float* depth, int* radii, bool debug, gsr_stream_t stream,
+                            int* num_rendered, int* rendered);
+
+int gsr_backward_dc(int P, int D, int M, int R, const float* background, int width, int height,
+                    const float* means3D, const float* dc, const float* shs,
+                    const float* colors_precomp, const float* opacities, const float* scales,
+                    float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                    const float* viewmatrix, const float* projmatrix, const float* campos,
+                    float tan_fovx, float tan_fovy, const int* radii, char* geom_buffer,
+                    char* binning_buffer, char* image_buffer, const float* dL_dpix,
+                    const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic,
+                    float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                    float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                    bool antialiasing, bool debug, gsr_stream_t stream);
+
+/* Visibility-masked Adam step (the accelerated upstream's `_C.adamUpdate`, called
+ * by SparseGaussianAdam.step(visibility, N) from train.py:180-183): for each of the
+ * N Gaussians with visible[i] set, its M consecutive elements of param are updated
+ *   m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;  param -= lr m / (sqrt(v) + eps)
+ * (no bias correction); other rows are left untouched.  N*M < 2^32. */
+int gsr_adam_update(float* param, const float* param_grad, float* exp_avg, float* exp_avg_sq,
+                    const bool* visible, float lr, float b1, float b2, float eps, int N, int M,
+                    gsr_stream_t stream);
+
 /* Debug / parity helper: writes the sorted 64-bit tile|depth keys
  * (rasterizer_impl.cu:102-104 layout, after the sort of :306-311) and the
  * sorted Gaussian ids of the last forward held in these buffers. */

@@ -5,8 +5,9 @@
   reference's GeometryState/ImageState/BinningState::required + obtain do
   (rasterizer_impl.h:21-73, rasterizer_impl.cu:155-194): every chunk 128-byte aligned,
   in bounds, and sizes monotone in P / pixels / L;
-* the Python surface exposes the reference's names and nothing else of note
-  (diff_gaussian_rasterization/__init__.py:143-207; no SparseGaussianAdam).
+* the Python surface exposes the reference's names (diff_gaussian_rasterization/__init__.py:143-207)
+  plus the accelerated upstream's SparseGaussianAdam, which train.py may only find together with
+  the `dc=` argument of GaussianRasterizer.forward.
 """
 import ctypes
 import os
@@ -43,7 +44,8 @@ def test_header_declares_the_boundary():
     names = _declared()
     for must in ["gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_last_error", "gsr_geometry_buffer_size",
                  "gsr_image_buffer_size", "gsr_binning_buffer_size", "gsr_knn_dist2", "gsr_knn_workspace_size", "gsr_ssim_forward",
-                 "gsr_ssim_backward"]:
+                 "gsr_ssim_backward", "gsr_forward_dc", "gsr_forward_geometry_dc", "gsr_forward_prealloc_dc",
+                 "gsr_backward_dc", "gsr_adam_update"]:
         assert must in names, must
 
 
@@ -102,9 +104,13 @@ def test_python_surface():
     import diff_gaussian_rasterization as dgr
     for name in ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians"]:
         assert hasattr(dgr, name), name
-    assert not hasattr(dgr, "SparseGaussianAdam")
+    # SparseGaussianAdam makes train.py pass dc= (train.py:37-41 -> gaussian_renderer/__init__.py:90-100)
+    import inspect
+    assert issubclass(dgr.SparseGaussianAdam, __import__("torch").optim.Adam)
+    assert "dc" in inspect.signature(dgr.GaussianRasterizer.forward).parameters
+    assert list(inspect.signature(dgr.SparseGaussianAdam.step).parameters) == ["self", "visibility", "N"]
     assert dgr.GaussianRasterizationSettings._fields == (
         "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
         "sh_degree", "campos", "prefiltered", "debug", "antialiasing")
-    for name in ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible"]:
+    for name in ["rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "adamUpdate"]:
         assert callable(getattr(dgr._C, name)), name
