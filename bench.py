@@ -187,7 +187,9 @@ def main():
 
     aux = None
     if not args.no_aux and world == 1:
-        aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args), "fused_ssim": aux_ssim(H, W, dev, args)}
+        aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args), "fused_ssim": aux_ssim(H, W, dev, args),
+               "separate_sh": aux_separate_sh(dgr, params, cams[0], grads[0], H * W),
+               "sparse_adam": aux_sparse_adam(dgr, params, cams[0], grads[0], args)}
 
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
@@ -242,6 +244,88 @@ def aux_knn(points, args, reps=5):
             dt = time.perf_counter() - t
             out["cpu_baseline"] = {"value": round(n / dt / 1e6, 4), "unit": "Mpoints/s", "cores": threads,
                                    "kind": "port", "sample": f"brute-force oracle on the first {n} points"}
+        except Exception as e:
+            out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
+    return out
+
+
+def aux_separate_sh(dgr, params, s, grad, npix, reps=10):
+    """The headline step through the separate-DC surface train.py uses once SparseGaussianAdam is
+    exported (rasterizer(dc=features_dc, shs=features_rest), gaussian_renderer/__init__.py:90-100):
+    same view, same scene, SH coefficient 0 and the rest as two parameter tensors."""
+    dc = params["shs"].detach()[:, :1].contiguous().requires_grad_(True)
+    rest = params["shs"].detach()[:, 1:].contiguous().requires_grad_(True)
+    gc, gi = grad
+    rast = dgr.GaussianRasterizer(raster_settings=s)
+
+    def step():
+        for p in (*params.values(), dc, rest):
+            p.grad = None  # as the headline step: no gradient accumulation kernels
+        means2D = torch.zeros_like(params["means3D"], requires_grad=True)
+        color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, dc=dc, shs=rest,
+                                 opacities=params["opacities"], scales=params["scales"], rotations=params["rotations"])
+        torch.autograd.backward([color, inv], [gc, gi])
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / reps * 1e3
+    return {"ms_per_step": round(ms, 4), "Mpix_per_s": round(npix / ms / 1e3, 2)}
+
+
+def aux_sparse_adam(dgr, params, s, grad, args, reps=10):
+    """SparseGaussianAdam.step(radii > 0, P) (train.py:180-183) over the six parameter groups of a
+    degree-3 model (xyz 3, f_dc 3, f_rest 45, opacity 1, scaling 3, rotation 4 floats per Gaussian)
+    with the bench view's gradients and visibility.  HBM-bound: 28 B per visible element (p, g, m, v
+    read; p, m, v written) + 1 B of flags per Gaussian and group.  CPU baseline: the numpy
+    restatement (oracle/adam_oracle.py) on the same arrays."""
+    gc, gi = grad
+    P = params["means3D"].shape[0]
+    rast = dgr.GaussianRasterizer(raster_settings=s)
+    sh = params["shs"].detach()
+    groups = {"xyz": params["means3D"].detach().clone(), "f_dc": sh[:, :1].contiguous(),
+              "f_rest": sh[:, 1:].contiguous(), "opacity": params["opacities"].detach().clone(),
+              "scaling": params["scales"].detach().clone(), "rotation": params["rotations"].detach().clone()}
+    groups = {k: torch.nn.Parameter(v) for k, v in groups.items()}
+    means2D = torch.zeros_like(groups["xyz"], requires_grad=True)
+    color, radii, inv = rast(means3D=groups["xyz"], means2D=means2D, dc=groups["f_dc"], shs=groups["f_rest"],
+                             opacities=groups["opacity"], scales=groups["scaling"], rotations=groups["rotation"])
+    torch.autograd.backward([color, inv], [gc, gi])
+    visible = radii > 0
+    opt = dgr.SparseGaussianAdam([{"params": [p], "lr": 1e-4, "name": k} for k, p in groups.items()], lr=0.0,
+                                 eps=1e-15)
+    for _ in range(2):
+        opt.step(visible, P)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        opt.step(visible, P)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    n_vis = int(visible.sum())
+    per_g = sum(p.numel() for p in groups.values()) // P
+    nbytes = 28 * n_vis * per_g + len(groups) * P
+    out = {"gaussians": P, "visible": n_vis, "floats_per_gaussian": per_g, "ms_step": round(ms, 4),
+           "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "hbm_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3),
+           "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        try:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import adam_oracle
+            host = {k: (p.detach().cpu().numpy(), p.grad.cpu().numpy(), opt.state[p]["exp_avg"].cpu().numpy(),
+                        opt.state[p]["exp_avg_sq"].cpu().numpy()) for k, p in groups.items()}
+            vis = visible.cpu().numpy()
+            t = time.perf_counter()
+            for pa, ga, ma, va in host.values():
+                adam_oracle.adam_update(pa, ga, ma, va, vis, 1e-4, 0.9, 0.999, 1e-15, P, pa.size // P)
+            dt = time.perf_counter() - t
+            out["cpu_baseline"] = {"value": round(dt * 1e3, 1), "unit": "ms per step", "cores": 1, "kind": "port",
+                                   "sample": "one step of all six groups, numpy restatement (single thread)"}
         except Exception as e:
             out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
     return out

@@ -306,6 +306,34 @@ __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const flo
     }
 }
 
+// Verbatim block copies between a global array and LDS (the separate-DC staging with rows of
+// <= 16 coefficients keeps the global row layout in LDS: the dc rows have a stride of 3 dwords and
+// degree-3 rest rows 45, both odd, so per-thread row walks are bank-conflict-free without
+// padding, and the copy needs no index arithmetic).  16-byte accesses when both sides allow it.
+__device__ __forceinline__ void lds_copy_in(float* lds, const float* src, int total)
+{
+    int e0 = 0;
+    if (((uintptr_t)src & 15) == 0 && ((uintptr_t)lds & 15) == 0) {
+        const int nv4 = total >> 2;
+        for (int f = threadIdx.x; f < nv4; f += blockDim.x)
+            reinterpret_cast<float4*>(lds)[f] = reinterpret_cast<const float4*>(src)[f];
+        e0 = nv4 << 2;
+    }
+    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) lds[e] = src[e];
+}
+
+__device__ __forceinline__ void lds_copy_out(float* dst, const float* lds, int total)
+{
+    int e0 = 0;
+    if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)lds & 15) == 0) {
+        const int nv4 = total >> 2;
+        for (int f = threadIdx.x; f < nv4; f += blockDim.x)
+            reinterpret_cast<float4*>(dst)[f] = reinterpret_cast<const float4*>(lds)[f];
+        e0 = nv4 << 2;
+    }
+    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) dst[e] = lds[e];
+}
+
 // Reference getHigherMsb (rasterizer_impl.cu:35-50)
 inline uint32_t higher_msb(uint32_t n)
 {

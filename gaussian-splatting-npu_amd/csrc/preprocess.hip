@@ -37,15 +37,17 @@ __device__ __forceinline__ f3 computeCov2D(const f3 mean, float focal_x, float f
 }
 
 // forward.cu:20-71
-__device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const float* sh, const float* campos,
-                                                 uint8_t& clamped)
+// `sh0` holds coefficient 0 and sh[3k..3k+2] coefficient k >= 1 (sh0 == sh for one (P,M,3) row;
+// with a separate dc row, sh = rest row - 3, never dereferenced below index 3).
+__device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const float* sh0, const float* sh,
+                                                 const float* campos, uint8_t& clamped)
 {
     f3 dir = {pos.x - campos[0], pos.y - campos[1], pos.z - campos[2]};
     const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
     dir.x = dir.x / len; dir.y = dir.y / len; dir.z = dir.z / len;
     float res[3];
 #pragma unroll
-    for (int c = 0; c < 3; c++) res[c] = SH_C0 * sh[0 * 3 + c];
+    for (int c = 0; c < 3; c++) res[c] = SH_C0 * sh0[c];
     if (deg > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
 #pragma unroll
@@ -84,7 +86,7 @@ __device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const fl
 }
 
 // One Gaussian; `sh` points at its SH coefficients (global memory or its LDS staging row).
-__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const float* sh)
+__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const float* sh0, const float* sh)
 {
 
     a.radii[idx] = 0;
@@ -148,7 +150,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     f3 rgb;
     if (!a.colors_precomp) {
         uint8_t cl;
-        rgb = computeColorFromSH(p_orig, a.D, sh, a.campos, cl);
+        rgb = computeColorFromSH(p_orig, a.D, sh0, sh, a.campos, cl);
         a.rgb[3 * (size_t)idx + 0] = rgb.x;
         a.rgb[3 * (size_t)idx + 1] = rgb.y;
         a.rgb[3 * (size_t)idx + 2] = rgb.z;
@@ -198,16 +200,27 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
     const int idx = base + (int)threadIdx.x;
     if (idx < a.scan_status_words) a.scan_status[idx] = 0;  // the scan runs after this kernel
     if (!STAGED) {
-        if (idx < a.P) preprocess_one(a, idx, a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr);
+        const float* row = a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr;
+        if (idx < a.P) preprocess_one(a, idx, row, row);
         return;
     }
-    if (a.dc) {  // separate dc: coefficient 0 into columns 0-2, the rest after it (at most 16 used)
+    if (a.dc && a.M <= 16) {  // separate dc, verbatim: dc rows at 0, rest rows (stride 3(M-1)) at 768
+        const int n = min(256, a.P - base), wr = (a.M - 1) * 3;
+        float* s_rest = s_sh + 768;
+        lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
+        if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
+        __syncthreads();
+        if (idx < a.P) preprocess_one(a, idx, s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x - 3);
+        return;
+    }
+    if (a.dc) {  // separate dc, wide rest rows: coefficient 0 into columns 0-2, the rest after it (16 used)
         const int n = min(256, a.P - base), ncols = min(a.M, 16) * 3;
         lds_rows_in(s_sh, lds_stride, 0, ncols, a.dc + (size_t)base * 3, 3, n);
         if (a.shs && a.M > 1) lds_rows_in(s_sh, lds_stride, 3, ncols, a.shs + (size_t)base * (a.M - 1) * 3,
                                           (a.M - 1) * 3, n);
         __syncthreads();
-        if (idx < a.P) preprocess_one(a, idx, s_sh + threadIdx.x * lds_stride);
+        const float* row = s_sh + threadIdx.x * lds_stride;
+        if (idx < a.P) preprocess_one(a, idx, row, row);
         return;
     }
     const int W3 = a.M * 3;  // multiple of 4 on this path
@@ -220,7 +233,8 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
     __syncthreads();
-    if (idx < a.P) preprocess_one(a, idx, s_sh + threadIdx.x * lds_stride);
+    const float* row = s_sh + threadIdx.x * lds_stride;
+    if (idx < a.P) preprocess_one(a, idx, row, row);
 }
 
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,
@@ -353,8 +367,9 @@ hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
                         ((uintptr_t)a.shs % 16) == 0;
     if (a.dc && !a.colors_precomp) {  // separate dc: always staged (any M, any alignment)
         const int stride = (min(a.M, 16) * 3) | 1;
-        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
-                           256 * stride * sizeof(float), s, a, stride);
+        const size_t lds = a.M <= 16 ? (768 + 256 * (size_t)(a.M - 1) * 3) * sizeof(float)
+                                     : 256 * stride * sizeof(float);
+        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), lds, s, a, stride);
     } else if (staged) {
         const int stride = W3 | 1;
         hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),

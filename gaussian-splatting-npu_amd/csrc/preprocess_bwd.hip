@@ -459,7 +459,26 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         return;
     }
     const int n = min(256, a.P - base);
-    if (a.dc) {  // separate dc (train.py's sparse-Adam layout): dc -> columns 0-2, rest -> 3..47
+    if (a.dc && a.M <= 16) {  // separate dc (train.py's sparse-Adam layout), verbatim rows (see preprocess.hip)
+        const int wr = (a.M - 1) * 3;
+        float* s_rest = s_sh + 768;
+        lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
+        if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
+        __syncthreads();
+        if (idx < a.P) {
+            bwd_core(a, idx, in, st);
+            float* d0 = s_sh + 3 * threadIdx.x;
+            float* r = s_rest + wr * threadIdx.x;
+            sh_bwd_range<0, 1>(st, d0, d0);
+            sh_bwd_range<1, 16>(st, r, r, a.M);
+            bwd_finish(a, idx, st);
+        }
+        __syncthreads();
+        lds_copy_out(a.dL_ddc + (size_t)base * 3, s_sh, n * 3);
+        if (wr > 0) lds_copy_out(a.dL_dsh + (size_t)base * wr, s_rest, n * wr);
+        return;
+    }
+    if (a.dc) {  // separate dc, wide rest rows: dc -> columns 0-2, rest -> 3..47
         const int wr = (a.M - 1) * 3;
         lds_rows_in(s_sh, SH_STRIDE, 0, 48, a.dc + (size_t)base * 3, 3, n);
         if (a.shs && wr > 0) lds_rows_in(s_sh, SH_STRIDE, 3, 48, a.shs + (size_t)base * wr, wr, n);
