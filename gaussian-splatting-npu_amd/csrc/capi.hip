@@ -599,6 +599,29 @@ int gsr_adam_update(float* param, const float* param_grad, float* exp_avg, float
     return GSR_OK;
 }
 
+int gsr_adam_update_multi(int n_groups, float* const* params, const float* const* param_grads,
+                          float* const* exp_avgs, float* const* exp_avg_sqs, const int* Ms, const float* lrs,
+                          const float* epss, const bool* visible, float b1, float b2, int N, gsr_stream_t stream)
+{
+    if (n_groups < 0 || N < 0) return fail(GSR_ERR_INVALID, "n_groups and N must be >= 0");
+    if (n_groups == 0 || N == 0) return GSR_OK;
+    if (!params || !param_grads || !exp_avgs || !exp_avg_sqs || !Ms || !lrs || !epss || !visible)
+        return fail(GSR_ERR_INVALID, "null pointer");
+    std::vector<AdamArgs> g((size_t)n_groups);
+    for (int i = 0; i < n_groups; i++) {
+        if (Ms[i] < 0) return fail(GSR_ERR_INVALID, "M must be >= 0");
+        if ((size_t)N * Ms[i] >= 0xFFFFFFF0ull) return fail(GSR_ERR_INVALID, "N*M must be < 2^32");
+        if (Ms[i] > 0 && (!params[i] || !param_grads[i] || !exp_avgs[i] || !exp_avg_sqs[i]))
+            return fail(GSR_ERR_INVALID, "null group pointer");
+        AdamArgs& a = g[i];
+        a.param = params[i]; a.grad = param_grads[i]; a.exp_avg = exp_avgs[i]; a.exp_avg_sq = exp_avg_sqs[i];
+        a.visible = reinterpret_cast<const uint8_t*>(visible);
+        a.lr = lrs[i]; a.b1 = b1; a.b2 = b2; a.eps = epss[i]; a.N = N; a.M = Ms[i];
+    }
+    HIP_TRY(launch_adam_update_multi(g.data(), n_groups, (hipStream_t)stream));
+    return GSR_OK;
+}
+
 // ---- fused_ssim.h ----
 int gsr_ssim_forward(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,
                      float* ssim_map, float* dm_dmu1, float* dm_dsigma1_sq, float* dm_dsigma12, void* stream)

@@ -132,7 +132,14 @@ struct AdamArgs {
     float lr, b1, b2, eps;
     int N, M;  // N Gaussians of M elements each
 };
+constexpr int ADAM_MAX_GROUPS = 8;
+struct AdamMultiArgs {
+    AdamArgs g[ADAM_MAX_GROUPS];
+    uint32_t block_start[ADAM_MAX_GROUPS];  // first workgroup of each group
+    int n_groups;
+};
 hipError_t launch_adam_update(const AdamArgs& a, hipStream_t s);
+hipError_t launch_adam_update_multi(const AdamArgs* groups, int n_groups, hipStream_t s);
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);

@@ -48,6 +48,7 @@ def _load():
                                     _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _b, _b, _vp]
     lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
+    lib.gsr_adam_update_multi.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
     for n in ("gsr_geometry_layout", "gsr_binning_layout"):
         getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
@@ -251,16 +252,40 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     return result()
 
 
-def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M):
-    """The accelerated upstream's `_C.adamUpdate` (called by SparseGaussianAdam.step): Adam on the
-    rows of the N Gaussians with visible[i] set (M elements each), in place; no bias correction."""
-    _require_gpu(param)
-    dev = param.device
+def _adam_check(param, param_grad, exp_avg, exp_avg_sq, N, M, dev):
     for name, t in (("param", param), ("param_grad", param_grad), ("exp_avg", exp_avg), ("exp_avg_sq", exp_avg_sq)):
         if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous():
             raise RuntimeError(f"adamUpdate: {name} must be a contiguous float32 tensor on {dev}")
         if t.numel() != int(N) * int(M):
             raise RuntimeError(f"adamUpdate: {name} has {t.numel()} elements, expected N*M = {int(N) * int(M)}")
+
+
+def adam_update_groups(groups, visible, b1, b2, N):
+    """One launch for several (param, grad, exp_avg, exp_avg_sq, lr, eps) groups sharing the
+    visibility mask of N Gaussians (SparseGaussianAdam.step); M = param.numel() // N per group."""
+    if not groups:
+        return
+    dev = groups[0][0].device
+    _require_gpu(groups[0][0])
+    if visible.device != dev or visible.dtype != torch.bool or visible.numel() != int(N):
+        raise RuntimeError(f"adamUpdate: visible must be a bool tensor of N = {int(N)} flags on {dev}")
+    visible = visible.contiguous()
+    n = len(groups)
+    Ms = [g[0].numel() // int(N) if int(N) else 0 for g in groups]
+    for (p, gr, m, v, _, _), M in zip(groups, Ms):
+        _adam_check(p, gr, m, v, N, M, dev)
+    ptrs = [(_vp * n)(*[g[k].data_ptr() for g in groups]) for k in range(4)]
+    _check(lib.gsr_adam_update_multi(n, *ptrs, (_i * n)(*Ms), (_f * n)(*[float(g[4]) for g in groups]),
+                                     (_f * n)(*[float(g[5]) for g in groups]), visible.data_ptr(), float(b1),
+                                     float(b2), int(N), _stream(dev)))
+
+
+def adamUpdate(param, param_grad, exp_avg, exp_avg_sq, visible, lr, b1, b2, eps, N, M):
+    """The accelerated upstream's `_C.adamUpdate` (called by SparseGaussianAdam.step): Adam on the
+    rows of the N Gaussians with visible[i] set (M elements each), in place; no bias correction."""
+    _require_gpu(param)
+    dev = param.device
+    _adam_check(param, param_grad, exp_avg, exp_avg_sq, N, M, dev)
     if visible.device != dev or visible.dtype != torch.bool or visible.numel() != int(N):
         raise RuntimeError(f"adamUpdate: visible must be a bool tensor of N = {int(N)} flags on {dev}")
     visible = visible.contiguous()

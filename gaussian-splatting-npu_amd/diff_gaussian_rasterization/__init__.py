@@ -132,14 +132,16 @@ class SparseGaussianAdam(torch.optim.Adam):
     caller's per-attribute groups are; state keeps torch.optim.Adam's keys (``exp_avg``,
     ``exp_avg_sq``, ``step``), so GaussianModel's densification surgery on ``optimizer.state``
     (gaussian_model.py:316-400) works unchanged.  The update is the published upstream one:
-    betas fixed at (0.9, 0.999), no bias correction; each group is one HIP launch
-    (``_C.adamUpdate``)."""
+    betas fixed at (0.9, 0.999), no bias correction.  Where the upstream class launches
+    ``_C.adamUpdate`` once per group, all groups of a step go in ONE HIP launch here
+    (``_C.adam_update_groups``; per group the same update)."""
 
     def __init__(self, params, lr, eps):
         super().__init__(params=params, lr=lr, eps=eps)
 
     @torch.no_grad()
     def step(self, visibility, N):
+        batch = []
         for group in self.param_groups:
             lr = group["lr"]
             eps = group["eps"]
@@ -153,6 +155,7 @@ class SparseGaussianAdam(torch.optim.Adam):
                 state["step"] = torch.tensor(0.0, dtype=torch.float32)
                 state["exp_avg"] = torch.zeros_like(param, memory_format=torch.preserve_format)
                 state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
-            M = param.numel() // N
-            _C.adamUpdate(param, param.grad, state["exp_avg"], state["exp_avg_sq"], visibility, lr, 0.9, 0.999,
-                          eps, N, M)
+            if param.numel() != (param.numel() // N) * N:
+                raise RuntimeError(f"parameter of {param.numel()} elements is not N = {N} rows")
+            batch.append((param, param.grad, state["exp_avg"], state["exp_avg_sq"], lr, eps))
+        _C.adam_update_groups(batch, visibility, 0.9, 0.999, N)

@@ -233,6 +233,15 @@ int gsr_adam_update(float* param, const float* param_grad, float* exp_avg, float
                     const bool* visible, float lr, float b1, float b2, float eps, int N, int M,
                     gsr_stream_t stream);
 
+/* The same step for n_groups parameter tensors sharing one visibility mask (one
+ * SparseGaussianAdam.step over its per-attribute groups, scene/gaussian_model.py:
+ * 181-196) in a single launch: group i has Ms[i] elements per Gaussian, learning
+ * rate lrs[i] and epsilon epss[i].  Per group identical to gsr_adam_update. */
+int gsr_adam_update_multi(int n_groups, float* const* params, const float* const* param_grads,
+                          float* const* exp_avgs, float* const* exp_avg_sqs, const int* Ms,
+                          const float* lrs, const float* epss, const bool* visible, float b1,
+                          float b2, int N, gsr_stream_t stream);
+
 /* Debug / parity helper: writes the sorted 64-bit tile|depth keys
  * (rasterizer_impl.cu:102-104 layout, after the sort of :306-311) and the
  * sorted Gaussian ids of the last forward held in these buffers. */

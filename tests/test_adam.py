@@ -119,7 +119,8 @@ def test_sparse_adam_training_step():
         "xyz": sc["means3D"], "f_dc": sc["shs"][:, :1].contiguous(), "f_rest": sc["shs"][:, 1:].contiguous(),
         "opacity": sc["opacities"], "scaling": sc["scales"], "rotation": sc["rotations"]}
     params = {k: torch.nn.Parameter(v.to(DEV).clone()) for k, v in params.items()}
-    opt = dgr.SparseGaussianAdam([{"params": [p], "lr": 1e-3, "name": k} for k, p in params.items()], lr=0.0,
+    lrs = {k: 1e-3 * (i + 1) for i, k in enumerate(params)}  # per-group rates, as the caller's schedule sets them
+    opt = dgr.SparseGaussianAdam([{"params": [p], "lr": lrs[k], "name": k} for k, p in params.items()], lr=0.0,
                                  eps=1e-15)
     s = dgr.GaussianRasterizationSettings(case["H"], case["W"], cam.tanfovx, cam.tanfovy, case["bg"].to(DEV), 1.0,
                                           cam.world_view_transform.to(DEV), cam.full_proj_transform.to(DEV), 3,
@@ -143,10 +144,42 @@ def test_sparse_adam_training_step():
     for k, p in params.items():
         M = p.numel() // N
         want = before[k].copy()
-        adam_oracle.adam_update(want, grads[k], np.zeros_like(want), np.zeros_like(want), vis, 1e-3, 0.9, 0.999,
+        adam_oracle.adam_update(want, grads[k], np.zeros_like(want), np.zeros_like(want), vis, lrs[k], 0.9, 0.999,
                                 1e-15, N, M)
         got = p.detach().cpu().numpy()
         np.testing.assert_allclose(got, want, rtol=RTOL, atol=1e-30, err_msg=k)
         assert np.array_equal(got.reshape(N, -1)[~vis], before[k].reshape(N, -1)[~vis]), k
         st = opt.state[p]
         assert set(st) == {"step", "exp_avg", "exp_avg_sq"}
+
+
+@pytest.mark.gpu
+def test_adam_update_groups_one_launch_matches_oracle():
+    """Ten groups (more than one launch holds) of mixed widths, rates, epsilons and alignments
+    through the multi-group entry point, against the per-group oracle."""
+    dgr = _dgr()
+    N = 3001
+    r = np.random.default_rng(11)
+    vis = r.random(N) < 0.5
+    tvis = torch.from_numpy(vis).to(DEV)
+    groups, host = [], []
+    for i, M in enumerate([3, 3, 45, 1, 3, 4, 2, 7, 16, 5]):
+        p, g, m, v, _ = _state(N, M, 100 + i)
+        off = i % 3
+        dev = []
+        for a in (p, g, m, v):
+            buf = torch.zeros(a.size + off, dtype=torch.float32, device=DEV)
+            t = buf[off:]
+            t.copy_(torch.from_numpy(a))
+            dev.append(t)
+        lr, eps = 1e-3 * (i + 1), 1e-15 * (i + 1)
+        groups.append((*dev, lr, eps))
+        host.append((p, g, m, v, lr, eps, M))
+    for _ in range(2):
+        dgr._C.adam_update_groups(groups, tvis, 0.9, 0.999, N)
+        for p, g, m, v, lr, eps, M in host:
+            adam_oracle.adam_update(p, g, m, v, vis, lr, 0.9, 0.999, eps, N, M)
+    torch.cuda.synchronize()
+    for (tp, _, tm, tv, _, _), (p, _, m, v, _, _, M) in zip(groups, host):
+        for got, want in ((tp, p), (tm, m), (tv, v)):
+            np.testing.assert_allclose(got.cpu().numpy(), want, rtol=RTOL, atol=1e-30, err_msg=f"M={M}")
