@@ -196,7 +196,8 @@ def main():
     if not args.no_aux and world == 1:
         aux = {"distCUDA2": aux_knn(params["means3D"].detach(), args), "fused_ssim": aux_ssim(H, W, dev, args),
                "separate_sh": aux_separate_sh(dgr, params, cams[0], grads[0], H * W),
-               "sparse_adam": aux_sparse_adam(dgr, params, cams[0], grads[0], args)}
+               "sparse_adam": aux_sparse_adam(dgr, params, cams[0], grads[0], args),
+               "train_iteration": aux_train_iteration(dgr, params, cams[0], H, W)}
 
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
@@ -336,6 +337,50 @@ def aux_sparse_adam(dgr, params, s, grad, args, reps=10):
         except Exception as e:
             out["cpu_baseline"] = {"value": None, "sample": f"failed: {e}"}
     return out
+
+
+def aux_train_iteration(dgr, params, s, H, W, reps=10):
+    """One train.py iteration with --optimizer_type sparse_adam at the bench scale (train.py:97-183):
+    parameter activations (gaussian_model.py:111-135), render with dc= (gaussian_renderer/
+    __init__.py:90-100), loss 0.8 L1 + 0.2 (1 - fused SSIM) (train.py:119-124), backward,
+    SparseGaussianAdam.step(radii > 0, P).  Densification and logging are not part of it.  The
+    target is a perturbed render of the same view (synthetic data)."""
+    from fused_ssim import fused_ssim
+    P = params["means3D"].shape[0]
+    sh = params["shs"].detach()
+    raw = {"xyz": params["means3D"].detach().clone(), "f_dc": sh[:, :1].contiguous(),
+           "f_rest": sh[:, 1:].contiguous(), "opacity": torch.logit(params["opacities"].detach()),
+           "scaling": torch.log(params["scales"].detach()), "rotation": params["rotations"].detach().clone()}
+    raw = {k: torch.nn.Parameter(v) for k, v in raw.items()}
+    lr = {"xyz": 1.6e-4, "f_dc": 2.5e-3, "f_rest": 2.5e-3 / 20, "opacity": 2.5e-2, "scaling": 5e-3, "rotation": 1e-3}
+    opt = dgr.SparseGaussianAdam([{"params": [p], "lr": lr[k], "name": k} for k, p in raw.items()], lr=0.0, eps=1e-15)
+    rast = dgr.GaussianRasterizer(raster_settings=s)
+
+    def render():
+        means2D = torch.zeros_like(raw["xyz"], requires_grad=True)
+        return rast(means3D=raw["xyz"], means2D=means2D, dc=raw["f_dc"], shs=raw["f_rest"],
+                    opacities=torch.sigmoid(raw["opacity"]), scales=torch.exp(raw["scaling"]),
+                    rotations=torch.nn.functional.normalize(raw["rotation"]))
+
+    with torch.no_grad():
+        gt = (render()[0] + 0.05 * torch.randn((3, H, W), device=raw["xyz"].device)).clamp(0, 1)
+
+    def iteration():
+        img, radii, _ = render()
+        loss = 0.8 * (img - gt).abs().mean() + 0.2 * (1.0 - fused_ssim(img[None], gt[None]))
+        loss.backward()
+        opt.step(radii > 0, P)
+        opt.zero_grad(set_to_none=True)
+    for _ in range(3):
+        iteration()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        iteration()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t) / reps * 1e3
+    return {"gaussians": P, "resolution": [W, H], "ms_per_iteration": round(ms, 4),
+            "iterations_per_s": round(1e3 / ms, 1), "Mpix_per_s": round(H * W / ms / 1e3, 1)}
 
 
 def aux_ssim(H, W, dev, args, reps=20):
