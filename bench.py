@@ -28,6 +28,9 @@ import torch.distributed as dist  # noqa: E402
 import synthetic  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMD-32 units, one wave64 VALU instruction per 2 cycles per SIMD
+# (MI355X_MICROARCH.md), at the 2.4 GHz the PMC runs measure (GRBM_GUI_ACTIVE / kernel time)
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1,228.8 G wave-instructions/s
 
 
 def parse():
@@ -182,11 +185,25 @@ def main():
                 traffic = json.load(open(tf)).get(dom)
             except Exception:
                 traffic = None
+        valu = None  # secondary roofline: render kernels are VALU-issue bound, not HBM bound
+        vf = os.path.join(ROOT, "profiles", "pmc_valu.json")
+        if os.path.exists(vf):
+            try:
+                vi = json.load(open(vf))
+                valu = {k: {"winst_per_launch": vi[k],
+                            "achieved_Ginst_s": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
+                            "frac": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
+                        for k in kern if k in vi}
+                valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": "profiles/pmc_valu.json (SQ_INSTS_VALU)",
+                        "kernels": valu}
+            except Exception:
+                valu = None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "algorithmic_bytes": ab[dom],
                     "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
-                                    "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1)} for k, v in kern.items()}}
+                                    "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1)} for k, v in kern.items()},
+                    "valu": valu}
 
     cpu = None
     if not args.no_cpu_baseline and world == 1:
