@@ -5,8 +5,12 @@ One step = for each view this rank owns: forward + backward of the differentiabl
 through the drop-in surface (diff_gaussian_rasterization.GaussianRasterizer + autograd),
 gradients accumulated into the replicated Gaussian parameters; then, with N>1 ranks, one
 RCCL all_reduce(SUM) of the 236 B/Gaussian parameter-gradient bucket.
-Each rank owns `--views-per-rank` views (default 1) of the 8-view ring, so per-GPU work is
-fixed as N grows (weak scaling; N=8 is BASELINE config 4's 8 views).
+A step is one optimizer step's batch.  At N=1 it is ONE view (BASELINE config 2: a single
+1080p view, fwd+bwd; no collective).  At N>1 each rank renders a mini-batch of `--views-per-rank`
+views (default 8: config 4's 8-view batch, per GPU), accumulates their gradients and joins ONE
+all-reduce, so the collective is amortised over the batch as a data-parallel training step would
+do it; the per-view work is the same at every N (weak scaling; the views of all ranks are distinct
+cameras on one ring).
 
 Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
 Prints ONE JSON line on rank 0.
@@ -41,7 +45,8 @@ def parse():
     ap.add_argument("--P", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--views-per-rank", type=int, default=1)
+    ap.add_argument("--views-per-rank", type=int, default=0,
+                    help="views per rank per step; 0 = 1 on one GPU, 8 (one all-reduce per 8-view batch) on N>1")
     ap.add_argument("--antialiasing", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
@@ -99,10 +104,12 @@ def main():
     scene = synthetic.make_scene(P, seed=0)
     params = {k: v.to(dev).requires_grad_(True) for k, v in scene.items()}
     M = params["shs"].shape[1]
-    views = multiview.views_for_rank(rank, world, args.views_per_rank)
+    vpr = args.views_per_rank or (1 if world == 1 else 8)
+    n_ring = max(8, vpr * world)  # distinct cameras for every view of every rank
+    views = multiview.views_for_rank(rank, world, vpr, n_views=n_ring)
     cams, grads = [], []
     for v in views:
-        cam = synthetic.Camera(W, H, view=v)
+        cam = synthetic.Camera(W, H, view=v, n_views=n_ring)
         s = dgr.GaussianRasterizationSettings(
             image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
             bg=torch.zeros(3, device=dev), scale_modifier=1.0, viewmatrix=cam.world_view_transform.to(dev),
@@ -157,13 +164,16 @@ def main():
 
     # geometry of the workload (one extra forward outside the timed region)
     with torch.no_grad():
-        s = cams[0]
-        out = dgr._C.rasterize_gaussians(s.bg, params["means3D"], torch.Tensor([]), params["opacities"],
-                                         params["scales"], params["rotations"], 1.0, torch.Tensor([]), s.viewmatrix,
-                                         s.projmatrix, s.tanfovx, s.tanfovy, H, W, params["shs"], 3, s.campos, False,
-                                         args.antialiasing, False)
-        L = int(out[0])
-        P_vis = int((out[2] > 0).sum().item())
+        Ls, vis = [], []
+        for s in cams:  # per-view geometry, averaged like the per-kernel times are
+            out = dgr._C.rasterize_gaussians(s.bg, params["means3D"], torch.Tensor([]), params["opacities"],
+                                             params["scales"], params["rotations"], 1.0, torch.Tensor([]),
+                                             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, H, W, params["shs"], 3,
+                                             s.campos, False, args.antialiasing, False)
+            Ls.append(int(out[0]))
+            vis.append(int((out[2] > 0).sum().item()))
+        L = round(sum(Ls) / len(Ls))
+        P_vis = round(sum(vis) / len(vis))
     N = H * W
     T = ((W + 15) // 16) * ((H + 15) // 16)
     pix_total = world * len(views) * N * args.steps
