@@ -133,7 +133,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 // radix scatter, so the order is deterministic.  Tiles are independent, so the launch order
 // changes timing only, never a result.
 constexpr int ORDER_BITS = 6;         // 64 work classes; tiles without work join the last one
-constexpr int ORDER_PER_THREAD = 16;  // tiles per thread and pass: 16,384 per pass
+constexpr int ORDER_PER_THREAD = 8;   // tiles per thread and pass: 8,192 per pass (one pass at 1080p)
 
 template <bool FROM_RANGES>
 __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, const uint32_t* work, int T,
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, c
         return t < T ? v : 0u;
     };
     if (tid == 0) s_max = 0;
-    // Above 16,384 tiles the passes order each 16K block separately (longest-first inside it).
+    // Above 8,192 tiles the passes order each 8K block separately (longest-first inside it).
     for (int t0 = 0; t0 < T; t0 += 1024 * ORDER_PER_THREAD) {
         uint32_t w[ORDER_PER_THREAD];  // wave wid, item i: the 64 consecutive tiles t0 + (i * 16 + wid) * 64 + lane
 #pragma unroll
@@ -178,6 +178,9 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, c
 #pragma unroll
         for (int i = 0; i < ORDER_PER_THREAD; i++) {
             const int t = t0 + (i * 16 + wid) * 64 + lane;
+            cls[i] = 0u;
+            rank[i] = 0u;
+            if (t0 + (i * 16 + wid) * 64 >= T) continue;  // the wave's 64 tiles are all past T (uniform)
             const uint32_t c = 63u - min((uint32_t)((float)w[i] * scale), 63u);
             cls[i] = c;
             uint64_t peers = __ballot(t < T);
