@@ -88,6 +88,57 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(uint32_t* cou
     if (tid == 0) totals[blockIdx.x] = s_carry;
 }
 
+// (2') the same for rows of up to RS_ROW_LDS chunks (every sort at <= 4K resolution): the row is
+// staged in LDS with all its loads in flight at once, each thread scans a contiguous segment
+// serially, and one block-wide scan of the segment sums joins them -- one global round trip and
+// two barriers instead of three barriers per 256 chunks.
+constexpr int RS_ROW_LDS = 12288;
+__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(uint32_t* counts, int nchunks,
+                                                                       uint32_t* totals)
+{
+    __shared__ uint32_t s_row[RS_ROW_LDS];
+    __shared__ uint32_t s_wave[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t* row = counts + (size_t)blockIdx.x * nchunks;
+    constexpr int B = 8;
+    for (int c0 = 0; c0 < nchunks; c0 += RS_THREADS * B) {
+        uint32_t v[B];
+#pragma unroll
+        for (int i = 0; i < B; i++) {
+            const int c = c0 + i * RS_THREADS + tid;
+            v[i] = c < nchunks ? row[c] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < B; i++) {
+            const int c = c0 + i * RS_THREADS + tid;
+            if (c < nchunks) s_row[c] = v[i];
+        }
+    }
+    __syncthreads();
+    const int seg = (nchunks + RS_THREADS - 1) / RS_THREADS;
+    const int j0 = min(tid * seg, nchunks), j1 = min(j0 + seg, nchunks);
+    uint32_t sum = 0;
+    for (int j = j0; j < j1; j++) sum += s_row[j];
+    uint32_t x = sum;  // inclusive wave scan of the segment sums
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_wave[w] = x;
+    __syncthreads();
+    uint32_t run = x - sum;
+    for (int q = 0; q < w; q++) run += s_wave[q];
+    if (tid == RS_THREADS - 1) totals[blockIdx.x] = run + sum;
+    for (int j = j0; j < j1; j++) {
+        const uint32_t c = s_row[j];
+        s_row[j] = run;
+        run += c;
+    }
+    __syncthreads();
+    for (int c = tid; c < nchunks; c += RS_THREADS) row[c] = s_row[c];
+}
+
 struct SortPassArgs {
     int n, shift, nbits, nchunks;
     const uint32_t* keys_in;
@@ -358,7 +409,11 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
         else
             hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, kin,
                                n, shift, w, nchunks, counts);
-        hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks, totals);
+        if (nchunks <= RS_ROW_LDS)
+            hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks,
+                               totals);
+        else
+            hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks, totals);
         SortPassArgs a;
         a.n = n;
         a.shift = shift;
