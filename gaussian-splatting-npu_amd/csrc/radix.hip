@@ -159,6 +159,24 @@ struct SortPassArgs {
     const uint32_t* totals;      // (nbins) digit totals
 };
 
+// Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
+// one barrier to add the preceding waves' totals (s4: 4 words, not reused before a later barrier).
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s4[w] = x;
+    __syncthreads();
+    uint32_t pre = x - v;
+    for (int q = 0; q < w; q++) pre += s4[q];
+    return pre;
+}
+
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
 template <int ITEMS, bool PAIR>
 __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs a)
@@ -170,6 +188,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     __shared__ uint32_t s_base[RS_MAXBINS];    // global start of each digit for this chunk
     __shared__ uint32_t s_keys[TILE];
     __shared__ Val s_vals[TILE];
+    __shared__ uint32_t s_w0[4], s_w1[4];      // wave totals of the two block scans
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nb = 1u << a.nbits, mask = nb - 1u;
@@ -178,15 +197,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     // digit offsets: exclusive scan of the totals (in s_base), plus this chunk's row prefix
     const uint32_t tot = (uint32_t)tid < nb ? a.totals[tid] : 0u;
     const uint32_t rowp = (uint32_t)tid < nb ? a.row_prefix[(size_t)tid * a.nchunks + chunk] : 0u;
-    s_base[tid] = tot;
-    __syncthreads();
-    for (int d = 1; d < RS_MAXBINS; d <<= 1) {
-        const uint32_t v = tid >= d ? s_base[tid - d] : 0u;
-        __syncthreads();
-        s_base[tid] += v;
-        __syncthreads();
-    }
-    const uint32_t gbase = s_base[tid] - tot + rowp;
+    const uint32_t gbase = block_excl_scan256(tot, s_w0) + rowp;  // its barrier also publishes s_cnt = 0
 
     const size_t base = (size_t)chunk * TILE;
     const int nvalid = (int)min((size_t)TILE, (size_t)a.n - base);
@@ -232,16 +243,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     s_cnt[1][tid] = c0;
     s_cnt[2][tid] = c0 + c1;
     s_cnt[3][tid] = c0 + c1 + c2;
-    s_blk[tid] = total;
-    __syncthreads();
-    for (int d = 1; d < RS_MAXBINS; d <<= 1) {
-        const uint32_t v = tid >= d ? s_blk[tid - d] : 0u;
-        __syncthreads();
-        s_blk[tid] += v;
-        __syncthreads();
-    }
-    const uint32_t blk_start = s_blk[tid] - total;
-    __syncthreads();
+    const uint32_t blk_start = block_excl_scan256(total, s_w1);
     s_blk[tid] = blk_start;
     s_base[tid] = gbase;
     __syncthreads();
