@@ -188,17 +188,17 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 }
 
 
-int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
-                         const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
-                         const float* opacities, const float* scales, float scale_modifier,
-                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
-                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
-                         bool prefiltered, bool antialiasing, int* radii, bool debug, gsr_stream_t stream,
-                         int* num_rendered)
+// Forward, first half: preprocess, depth sort and the tile-count scan are enqueued; *h_out is the
+// pinned word block the scan publishes num_rendered into (forward_geometry_wait reads it).
+static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width,
+                                   int height, const float* means3D, const float* dc, const float* shs,
+                                   const float* colors_precomp, const float* opacities, const float* scales,
+                                   float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                   const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                                   float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
+                                   bool debug, gsr_stream_t stream, uint32_t** h_out)
 {
     hipStream_t s = (hipStream_t)stream;
-    *num_rendered = 0;
-    if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
     if (width <= 0 || height <= 0) return fail(GSR_ERR_INVALID, "image size must be positive");
     if (!colors_precomp && !dc && (!shs || M <= 0))
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
@@ -279,6 +279,13 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
     }
     DEBUG_SYNC(s);
 
+    *h_out = h;
+    return GSR_OK;
+}
+
+static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rendered)
+{
+    hipStream_t s = (hipStream_t)stream;
     // 4. the one device->host hand-off of the forward: num_rendered (rasterizer_impl.cu:283-284),
     //    stored by the scan into pinned memory, plus the error flag.  The host polls the word
     //    itself (no driver wake-up on the critical path); hipStreamQuery now and then notices a
@@ -299,12 +306,46 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
     return GSR_OK;
 }
 
+int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
+                         const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                         const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                         bool prefiltered, bool antialiasing, int* radii, bool debug, gsr_stream_t stream,
+                         int* num_rendered)
+{
+    *num_rendered = 0;
+    if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
+    uint32_t* h = nullptr;
+    int rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                     colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                     viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                     radii, debug, stream, &h);
+    if (rc) return rc;
+    return forward_geometry_wait(h, stream, num_rendered);
+}
+
+static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
+                               int num_rendered, const float* background, int width, int height, float* out_color,
+                               float* depth, bool debug, gsr_stream_t stream, bool emitted);
+
 int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P, int num_rendered,
                        const float* background, int width, int height, const float* colors_precomp,
                        float* out_color, float* depth, int* radii, bool debug, gsr_stream_t stream)
 {
-    (void)colors_precomp;  // folded into the render record by preprocess
-    hipStream_t s = (hipStream_t)stream;
+    (void)radii;
+    (void)colors_precomp;
+    return forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, num_rendered, background, width,
+                               height, out_color, depth, debug, stream, false);
+}
+
+// Forward, second half.  `emitted`: the early emission (gsr_forward_prealloc_dc) already wrote the
+// instances into this binning buffer.
+static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
+                               int num_rendered, const float* background, int width, int height, float* out_color,
+                               float* depth, bool debug, gsr_stream_t stream, bool emitted)
+{
+    hipStream_t s = (hipStream_t)stream;  // colors_precomp was folded into the render record by preprocess
     if (P <= 0) return GSR_OK;
     const int L = num_rendered;
     const GeomLayout g = geom_layout(P);
@@ -332,7 +373,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
         uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
         uint32_t* v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
         uint32_t* v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
-        {
+        if (!emitted) {
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
                                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
@@ -412,23 +453,49 @@ int gsr_forward_dc(gsr_resize_fn geometryBuffer, void* geometry_ctx, gsr_resize_
 
 int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* binning_buffer, size_t binning_capacity,
                          int P, int D, int M, const float* background, int width, int height, const float* means3D,
-                         const float* dc, const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
-                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                         const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
-                         float tan_fovy, bool prefiltered, bool antialiasing, float* out_color, float* depth,
-                         int* radii, bool debug, gsr_stream_t stream, int* num_rendered, int* rendered)
+                         const float* dc, const float* shs, const float* colors_precomp, const float* opacities,
+                         const float* scales, float scale_modifier, const float* rotations,
+                         const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                         const float* cam_pos, float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing,
+                         float* out_color, float* depth, int* radii, bool debug, gsr_stream_t stream,
+                         int* num_rendered, int* rendered)
 {
+    (void)colors_precomp;
     *rendered = 0;
+    *num_rendered = 0;
+    if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
+    uint32_t* h = nullptr;
+    int rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                     colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                     viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                     radii, debug, stream, &h);
+    if (rc) return rc;
+    // Emission does not need num_rendered on the host: enqueue it now, so the GPU works through
+    // the read-back below instead of idling until the host launches it (it resolves its output
+    // arrays from the device-side total and writes nothing if the buffer is too small).
+    const bool early = binning_buffer != nullptr && binning_capacity > 0;
+    if (early) {
+        hipStream_t s = (hipStream_t)stream;
+        const GeomLayout g = geom_layout(P);
+        const ImageLayout im = image_layout(width, height);
+        const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+        const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+        char* gb = geometry_buffer;
+        ProfScope ps_(PK_EMIT, s);
+        HIP_TRY(launch_emit_instances_early(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
+                                            at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
+                                            at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx,
+                                            at<uint32_t>(gb, g.off[GEOM_EMIT_START]), binning_buffer,
+                                            binning_capacity, at<uint2>(image_buffer, im.off[IMG_RANGES]),
+                                            (int)(gx * gy), s));
+    }
     int L = 0;
-    int rc = gsr_forward_geometry_dc(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs, colors_precomp,
-                                  opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
-                                  cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing, radii, debug, stream, &L);
+    rc = forward_geometry_wait(h, stream, &L);
     *num_rendered = L;
     if (rc) return rc;
-    if (P <= 0) return GSR_OK;  // nothing to render: the caller's gsr_forward_render returns at once
     if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity) return GSR_OK;  // caller allocates
-    rc = gsr_forward_render(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
-                            colors_precomp, out_color, depth, radii, debug, stream);
+    rc = forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
+                             out_color, depth, debug, stream, early && L > 0);
     if (rc) return rc;
     *rendered = 1;
     return GSR_OK;

@@ -155,6 +155,9 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
                       uint32_t* sorted_counts = nullptr);
 // Also clears the valid bit mask (the backward's record flags) and ranges[0..T) for tile_ranges.
+hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
+                                       const uint2* sorted_rects, uint32_t gx, uint32_t* emit_start, char* bb,
+                                       size_t capacity, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
                                  uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
                                  uint32_t* emit_start, uint32_t* valid, uint2* ranges, int T, hipStream_t s);

@@ -295,13 +295,26 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 // the depth sort laid them out, no gathers by Gaussian id) in LDS, then the wave fills its whole
 // slot range 64 consecutive slots at a time (coalesced stores), each lane finding the owner of
 // its slot by a binary search over the 64 rect starts.
+// Early form (bb != null): launched before the host has read num_rendered back, so the output
+// arrays are resolved here from the device-side total (offsets_d[P-1]) with the binning layout
+// the host will use; if that layout does not fit in `capacity` bytes, nothing is written (the
+// host then allocates the exact size and emits again).
 __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
                                                              const uint32_t* offsets_d, const uint2* sorted_rects,
                                                              uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
                                                              uint32_t* emit_start, uint32_t* valid, uint2* ranges,
-                                                             int T)
+                                                             int T, char* bb, size_t capacity)
 {
     __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64];
+    if (bb) {
+        const size_t n = offsets_d[P - 1];
+        const BinLayout b = bin_layout_dev(n);
+        if (n == 0 || b.off[BIN_COUNT] + 256 > capacity) return;  // gsr_binning_buffer_size = total + 256
+        const size_t q = align_up(4 * n, 256);
+        tile_keys = reinterpret_cast<uint32_t*>(bb + b.off[BIN_GRAD_INST]);
+        gids = reinterpret_cast<uint32_t*>(bb + b.off[BIN_GRAD_INST] + q);
+        valid = reinterpret_cast<uint32_t*>(bb + b.off[BIN_VALID]);
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int k0 = (blockIdx.x * 4 + w) * 64;
     // ranges must be zero for tile_ranges (empty tiles keep (0, 0)): cleared here, not by a memset
@@ -382,6 +395,8 @@ size_t radix_status_bytes(int n, int npass)
     (void)npass;
     return align_up(rs_chunks(n) * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
 }
+static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 2048 && RS_MAXBINS == 256,
+              "tile_sort_status_bytes (gsr_common.h) restates radix_status_bytes for 2,048-key chunks");
 
 // Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, and
 // with `gids` also gids[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
@@ -455,7 +470,17 @@ hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       sorted_rects, gx, tile_keys, gids, emit_start, valid, ranges, T);
+                       sorted_rects, gx, tile_keys, gids, emit_start, valid, ranges, T, nullptr, (size_t)0);
+    return hipGetLastError();
+}
+
+hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
+                                       const uint2* sorted_rects, uint32_t gx, uint32_t* emit_start, char* bb,
+                                       size_t capacity, uint2* ranges, int T, hipStream_t s)
+{
+    if (P <= 0 || !bb) return hipSuccess;
+    hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
+                       sorted_rects, gx, nullptr, nullptr, emit_start, nullptr, ranges, T, bb, capacity);
     return hipGetLastError();
 }
 
