@@ -322,13 +322,21 @@ __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, 
     // each thread owns 16 consecutive items; every load issued before the first use
     const size_t base = (size_t)c * SCAN_ITEMS + (size_t)threadIdx.x * 16;
     uint32_t v[16];
+    if (!gather && base + 16 <= (size_t)n && ((uintptr_t)in & 15) == 0) {  // 4 x 16-byte loads
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const size_t i = base + k;
-        v[k] = i < (size_t)n ? (gather ? gather[i] : (uint32_t)i) : 0u;
+        for (int k = 0; k < 4; k++) {
+            const uint4 q = reinterpret_cast<const uint4*>(in + base)[k];
+            v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const size_t i = base + k;
+            v[k] = i < (size_t)n ? (gather ? gather[i] : (uint32_t)i) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) v[k] = base + k < (size_t)n ? in[v[k]] : 0u;
     }
-#pragma unroll
-    for (int k = 0; k < 16; k++) v[k] = base + k < (size_t)n ? in[v[k]] : 0u;
     uint32_t s = 0;
 #pragma unroll
     for (int k = 0; k < 16; k++) s += v[k];
@@ -351,11 +359,23 @@ __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, 
     }
     __syncthreads();
     ex += s_excl;
+    if (base + 16 <= (size_t)n && ((uintptr_t)out & 15) == 0) {  // 4 x 16-byte stores
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        ex += v[k];
-        const size_t i = base + k;
-        if (i < (size_t)n) out[i] = ex;
+        for (int k = 0; k < 4; k++) {
+            uint4 q;
+            q.x = (ex += v[4 * k]);
+            q.y = (ex += v[4 * k + 1]);
+            q.z = (ex += v[4 * k + 2]);
+            q.w = (ex += v[4 * k + 3]);
+            reinterpret_cast<uint4*>(out + base)[k] = q;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            ex += v[k];
+            const size_t i = base + k;
+            if (i < (size_t)n) out[i] = ex;
+        }
     }
 }
 
