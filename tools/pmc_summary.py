@@ -56,20 +56,29 @@ def main(d):
             ent[c] = sum(per.values()) / max(1, len(per))
             ent["dispatches"] = len(per)
         out[k[:120]] = ent
-    traffic = collections.defaultdict(float)
-    counts = collections.defaultdict(int)
-    for k, ent in out.items():
-        s = short_name(k)
-        if s and "FETCH_SIZE" in ent and "WRITE_SIZE" in ent:
-            traffic[s] += (2 * ent["FETCH_SIZE"] + ent["WRITE_SIZE"]) * 1024.0
-            counts[s] += 1
+    # Per-launch figures per short name.  Template variants of one kernel (render_bwd<true/false>,
+    # tile_order<true/false>, ...) are alternatives of ONE launch: dispatch-weighted mean.  The radix
+    # kernels of a sort are consecutive launches: their per-dispatch means are summed.
+    def per_launch(counter_fn):
+        acc_v, acc_n = collections.defaultdict(float), collections.defaultdict(float)
+        for k, ent in out.items():
+            s = short_name(k)
+            v = counter_fn(ent)
+            if not s or v is None:
+                continue
+            if s in ("radix_sorts", "distCUDA2"):  # several different kernels per call
+                acc_v[s] += v
+                acc_n[s] = 1.0
+            else:
+                acc_v[s] += v * ent["dispatches"]
+                acc_n[s] += ent["dispatches"]
+        return {s: acc_v[s] / acc_n[s] for s in acc_v if acc_n[s]}
+
+    traffic = per_launch(lambda e: (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
+                         if "FETCH_SIZE" in e and "WRITE_SIZE" in e else None)
     json.dump({k: round(v) for k, v in traffic.items()}, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
     # VALU wave-instructions per launch (bench.py's secondary, VALU-issue roofline)
-    valu = collections.defaultdict(float)
-    for k, ent in out.items():
-        s = short_name(k)
-        if s and "SQ_INSTS_VALU" in ent:
-            valu[s] += ent["SQ_INSTS_VALU"]
+    valu = per_launch(lambda e: e.get("SQ_INSTS_VALU"))
     json.dump({k: round(v) for k, v in valu.items()}, open(os.path.join(d, "pmc_valu.json"), "w"), indent=1)
     print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
                      indent=1))
