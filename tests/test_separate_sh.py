@@ -130,3 +130,23 @@ def test_dc_backward_tuple_layout():
         dgr._C.rasterize_gaussians(
             s.bg, sc["means3D"], e, sc["opacities"], sc["scales"], sc["rotations"], 1.0, e, s.viewmatrix,
             s.projmatrix, s.tanfovx, s.tanfovy, 64, 64, rest, 3, s.campos, False, False, False, dc=dc[:10])
+
+
+def test_dc_gradients_share_one_buffer():
+    """With dc=, the parameter gradients are consecutive views of one buffer in
+    multiview.PARAM_ORDER_DC (means3D | dc | rest | opacity | scales | rotations), so the
+    multi-GPU step all-reduces them in place as in the single-array layout."""
+    from diff_gaussian_rasterization import multiview
+    dgr = _dgr()
+    case = common.make_case(P=800, H=64, W=80)
+    sc = case["scene"]
+    t = {"means3D": sc["means3D"], "dc": sc["shs"][:, :1].contiguous(), "shs": sc["shs"][:, 1:].contiguous(),
+         "opacities": sc["opacities"], "scales": sc["scales"], "rotations": sc["rotations"]}
+    t = {k: v.to(DEV).clone().requires_grad_(True) for k, v in t.items()}
+    color, radii, inv = dgr.GaussianRasterizer(_settings(case, 3, False))(
+        means2D=torch.zeros_like(t["means3D"], requires_grad=True), **t)
+    torch.autograd.backward([color, inv], [case["grad_color"].to(DEV), case["grad_invdepth"].to(DEV)])
+    flat = multiview.flat_grad_view(t, multiview.PARAM_ORDER_DC)
+    assert flat is not None
+    assert flat.numel() == sum(p.numel() for p in t.values())
+    torch.testing.assert_close(flat, multiview.grad_bucket(t, multiview.PARAM_ORDER_DC), rtol=0, atol=0)
