@@ -203,6 +203,8 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     if (!colors_precomp && !dc && (!shs || M <= 0))
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
     if (dc && M < 0) return fail(GSR_ERR_INVALID, "M (rest SH coefficients) must be >= 0");
+    if (dc && colors_precomp)
+        return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
     if (dc && M > 0 && !shs) return fail(GSR_ERR_INVALID, "dc given with M > 0 rest coefficients but shs is NULL");
     if (!cov3D_precomp && (!scales || !rotations))
         return fail(GSR_ERR_INVALID,
@@ -511,6 +513,8 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
                  float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
 {
     if (dc && !dL_ddc) return fail(GSR_ERR_INVALID, "dc given without dL_ddc");
+    if (dc && colors_precomp)
+        return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
     if (dc && M > 0 && (!shs || !dL_dsh)) return fail(GSR_ERR_INVALID, "dc given with M > 0 but shs/dL_dsh NULL");
     (void)colors_precomp;
     hipStream_t s = (hipStream_t)stream;

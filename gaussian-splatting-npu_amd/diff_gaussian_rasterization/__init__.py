@@ -108,7 +108,7 @@ class GaussianRasterizer(nn.Module):
         """``dc`` (P,1,3), keyword only in practice (gaussian_renderer/__init__.py:91-100): SH
         coefficient 0, with ``shs`` then holding coefficients 1.. (features_rest)."""
         s = self.raster_settings
-        if (shs is None) == (colors_precomp is None):
+        if (shs is None) == (colors_precomp is None) or (dc is not None and colors_precomp is not None):
             raise Exception('Please provide excatly one of either SHs or precomputed colors!')
         if ((scales is None or rotations is None) and cov3D_precomp is None) or \
                 ((scales is not None or rotations is not None) and cov3D_precomp is not None):

@@ -150,3 +150,16 @@ def test_dc_gradients_share_one_buffer():
     assert flat is not None
     assert flat.numel() == sum(p.numel() for p in t.values())
     torch.testing.assert_close(flat, multiview.grad_bucket(t, multiview.PARAM_ORDER_DC), rtol=0, atol=0)
+
+
+def test_dc_with_precomputed_colors_raises():
+    """dc= is SH input: together with colors_precomp it breaks the reference's exactly-one rule
+    (diff_gaussian_rasterization/__init__.py:178-182)."""
+    dgr = _dgr()
+    case = common.make_case(P=100, H=32, W=32)
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    with pytest.raises(Exception, match="exactly one of either SHs or precomputed colors|excatly one"):
+        dgr.GaussianRasterizer(_settings(case, 3, False))(
+            means3D=sc["means3D"], means2D=torch.zeros_like(sc["means3D"]), opacities=sc["opacities"],
+            dc=sc["shs"][:, :1].contiguous(), colors_precomp=torch.rand(100, 3, device=DEV), scales=sc["scales"],
+            rotations=sc["rotations"])
