@@ -119,7 +119,9 @@ def main():
         gc, gi = synthetic.make_grads(H, W, seed=1 + v)
         grads.append((gc.to(dev), gi.to(dev)))
 
-    def step():
+    ar_events = []  # (start, end) around the all-reduce, recorded only in the instrumented pass below
+
+    def step(record_allreduce=False):
         for p in params.values():
             p.grad = None
         for s, (gc, gi) in zip(cams, grads):
@@ -129,7 +131,13 @@ def main():
                                      opacities=params["opacities"], scales=params["scales"],
                                      rotations=params["rotations"])
             torch.autograd.backward([color, inv], [gc, gi])
-        multiview.allreduce_grads(params)
+        if record_allreduce:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        nbytes = multiview.allreduce_grads(params)
+        if record_allreduce:
+            e1.record()
+            ar_events.append((e0, e1, nbytes))
 
     for _ in range(args.warmup):
         step()
@@ -161,6 +169,18 @@ def main():
         for k in range(n):
             if cnt[k]:
                 kern[lib.gsr_profile_kernel_name(k).decode()] = {"avg_ms": tot[k] / cnt[k], "launches": cnt[k]}
+
+    # all-reduce share of the step: events around the collective, separate pass
+    allreduce = None
+    if world > 1:
+        for _ in range(min(args.steps, 5)):
+            step(record_allreduce=True)
+        torch.cuda.synchronize()
+        ar_ms = sum(a.elapsed_time(b) for a, b, _ in ar_events) / len(ar_events)
+        ar_ms = multiview.max_over_ranks(ar_ms / 1e3, dev) * 1e3
+        allreduce = {"ms": round(ar_ms, 4), "bytes_per_rank": ar_events[0][2],
+                     "fraction_of_step": round(ar_ms / (elapsed / args.steps * 1e3), 3),
+                     "algbw_GBps": round(ar_events[0][2] / (ar_ms * 1e-3) / 1e9, 1)}
 
     # geometry of the workload (one extra forward outside the timed region)
     with torch.no_grad():
@@ -246,6 +266,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "aux": aux,
+        "allreduce": allreduce,
     }
     print(json.dumps(res), flush=True)
     if world > 1:
