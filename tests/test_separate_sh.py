@@ -68,10 +68,17 @@ def _run(case, degree, antialiasing, shs=None, dc=None, rest=None):
 
 
 @pytest.mark.parametrize("degree,n_coef,antialiasing,offset", [
-    (3, 16, False, 0), (3, 16, True, 0), (1, 16, False, 0), (2, 9, False, 0), (3, 16, False, 1), (1, 4, True, 3)])
+    (3, 16, False, 0), (3, 16, True, 0), (1, 16, False, 0), (2, 9, False, 0), (3, 16, False, 1), (1, 4, True, 3),
+    (3, 21, False, 0), (3, 21, False, 1)])
 def test_dc_path_equals_full_sh_path(degree, n_coef, antialiasing, offset):
+    """n_coef 21: rows wider than the 16 coefficients degree 3 reads (the padded-row staging
+    path); the extra coefficients get zero gradients on both paths."""
     case = common.make_case(P=3000, H=200, W=232)
-    full = case["scene"]["shs"][:, :n_coef].contiguous().to(DEV)
+    full = case["scene"]["shs"]
+    if n_coef > full.shape[1]:
+        extra = torch.randn((full.shape[0], n_coef - full.shape[1], 3), generator=torch.Generator().manual_seed(3))
+        full = torch.cat([full, 0.05 * extra], dim=1)
+    full = full[:, :n_coef].contiguous().to(DEV)
     a = _run(case, degree, antialiasing, shs=full)
     b = _run(case, degree, antialiasing, dc=_misaligned(full[:, :1].contiguous(), offset),
              rest=_misaligned(full[:, 1:].contiguous(), offset))
