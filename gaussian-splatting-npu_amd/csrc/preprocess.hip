@@ -115,13 +115,15 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     const float p_w = 1.0f / (p_hom.w + 0.0000001f);
     const float ppx = p_hom.x * p_w, ppy = p_hom.y * p_w;
 
-    float cov3D_local[6];
-    const float* cov3D;
+    // One local array filled either way: a pointer choosing between global memory and a local
+    // array forced the local copy into scratch (32 B/lane; 0.099 -> 0.094 ms without it).
+    float cov3D[6];
     if (a.cov3D_precomp) {
-        cov3D = a.cov3D_precomp + (size_t)idx * 6;
+        const float* c = a.cov3D_precomp + (size_t)idx * 6;
+#pragma unroll
+        for (int k = 0; k < 6; k++) cov3D[k] = c[k];
     } else {
-        computeCov3D(scl, a.scale_modifier, rot, cov3D_local);  // recomputed by preprocess_bwd, not stored
-        cov3D = cov3D_local;
+        computeCov3D(scl, a.scale_modifier, rot, cov3D);  // recomputed by preprocess_bwd, not stored
     }
 
     f3 cov = computeCov2D(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3D, a.view);
