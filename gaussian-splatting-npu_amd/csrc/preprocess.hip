@@ -89,10 +89,13 @@ __device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const fl
 __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const float* sh0, const float* sh)
 {
 
-    a.radii[idx] = 0;
-    a.tiles_touched[idx] = 0;
-    a.rect[idx] = make_uint2(0u, 0u);
-    a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
+    // culled: these four are written here and only here (a visible Gaussian writes them once, below)
+    auto cull = [&]() {
+        a.radii[idx] = 0;
+        a.tiles_touched[idx] = 0;
+        a.rect[idx] = make_uint2(0u, 0u);
+        a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
+    };
 
     // Issue every per-Gaussian load up front (one memory round trip instead of one per phase).
     const f3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
@@ -109,6 +112,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     const f3 p_view = transformPoint4x3(p_orig, a.view);
     if (p_view.z <= 0.2f) {
         if (a.prefiltered) __hip_atomic_store(a.host_flags, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        cull();
         return;
     }
     const float4 p_hom = transformPoint4x4(p_orig, a.proj);
@@ -136,7 +140,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     if (a.antialiasing) h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
 
     const float det = det_cov_plus_h_cov;
-    if (det == 0.0f) return;
+    if (det == 0.0f) { cull(); return; }
     const float det_inv = 1.f / det;
     const float conic_x = cov.z * det_inv, conic_y = -cov.y * det_inv, conic_z = cov.x * det_inv;
 
@@ -147,7 +151,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     const float pix_x = ndc2Pix(ppx, a.W), pix_y = ndc2Pix(ppy, a.H);
     uint32_t rminx, rminy, rmaxx, rmaxy;
     getRect(pix_x, pix_y, (int)my_radius, a.grid_x, a.grid_y, rminx, rminy, rmaxx, rmaxy);
-    if ((rmaxx - rminx) * (rmaxy - rminy) == 0) return;
+    if ((rmaxx - rminx) * (rmaxy - rminy) == 0) { cull(); return; }
 
     f3 rgb;
     if (!a.colors_precomp) {
