@@ -358,20 +358,38 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
     }
 }
 
+// identifyTileRanges (rasterizer_impl.cu:116-138): four consecutive instances per thread (one
+// 16-byte load); each element's predecessor comes from the same load or, for the first, from the
+// neighbouring lane (the wave's first lane loads it).
 __global__ void __launch_bounds__(256) tile_ranges_kernel(int L, const uint32_t* sorted_tiles, uint2* ranges)
 {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= L) return;
-    const uint32_t cur = sorted_tiles[idx];
-    if (idx == 0) ranges[cur].x = 0;
-    else {
-        const uint32_t prev = sorted_tiles[idx - 1];
-        if (cur != prev) {
-            ranges[prev].y = idx;
-            ranges[cur].x = idx;
-        }
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int i0 = 4 * t;
+    uint32_t v[4];
+    if (i0 + 4 <= L) {
+        const uint4 q = reinterpret_cast<const uint4*>(sorted_tiles)[t];
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = i0 + k < L ? sorted_tiles[i0 + k] : 0u;
     }
-    if (idx == L - 1) ranges[cur].y = L;
+    uint32_t prev = (uint32_t)__shfl_up((int)v[3], 1, 64);  // every lane, before any exit
+    if (lane == 0 && i0 > 0 && i0 - 1 < L) prev = sorted_tiles[i0 - 1];
+    if (i0 >= L) return;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int i = i0 + k;
+        if (i >= L) break;
+        const uint32_t cur = v[k];
+        const uint32_t p = k == 0 ? prev : v[k - 1];
+        if (i == 0) ranges[cur].x = 0;
+        else if (cur != p) {
+            ranges[p].y = (uint32_t)i;
+            ranges[cur].x = (uint32_t)i;
+        }
+        if (i == L - 1) ranges[cur].y = (uint32_t)L;
+    }
 }
 
 __global__ void __launch_bounds__(256) debug_keys_kernel(int L, const uint32_t* sorted_tiles, const uint32_t* point_list,
@@ -487,7 +505,9 @@ hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const 
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s)
 {
     if (L <= 0) return hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);  // no emit ran to clear them
-    hipLaunchKernelGGL(tile_ranges_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, sorted_tiles, ranges);
+    if ((uintptr_t)sorted_tiles & 15) return hipErrorInvalidValue;  // binning arrays are 256-B aligned
+    const int quads = (L + 3) / 4;
+    hipLaunchKernelGGL(tile_ranges_kernel, dim3((quads + 255) / 256), dim3(256), 0, s, L, sorted_tiles, ranges);
     return hipGetLastError();
 }
 
