@@ -48,11 +48,23 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t*
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * (RS_THREADS * ITEMS);
     uint32_t k[ITEMS];
+    if (base + RS_THREADS * ITEMS <= (size_t)n && ((uintptr_t)keys & 15) == 0 && ITEMS % 4 == 0) {
+        // full chunk: 16-byte loads (a histogram does not care which thread counts which key)
+        const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
-    for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
+        for (int j = 0; j < ITEMS / 4; j++) {
+            const uint4 q = k4[j * RS_THREADS + tid];
+            k[4 * j] = q.x; k[4 * j + 1] = q.y; k[4 * j + 2] = q.z; k[4 * j + 3] = q.w;
+        }
 #pragma unroll
-    for (int i = 0; i < ITEMS; i++)
-        if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+        for (int i = 0; i < ITEMS; i++) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+    } else {
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++)
+            if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+    }
     __syncthreads();
     if ((uint32_t)tid < nb) counts[(size_t)tid * nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
