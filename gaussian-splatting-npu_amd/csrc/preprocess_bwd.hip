@@ -28,7 +28,7 @@ struct BwdIn {
     uint8_t clamped;
 };
 
-constexpr int REC_BATCH = 4;  // record flags / records in flight per step
+constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +3 us, 2: +10 us)
 
 __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in)
 {
