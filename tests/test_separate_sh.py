@@ -170,3 +170,45 @@ def test_dc_with_precomputed_colors_raises():
             means3D=sc["means3D"], means2D=torch.zeros_like(sc["means3D"]), opacities=sc["opacities"],
             dc=sc["shs"][:, :1].contiguous(), colors_precomp=torch.rand(100, 3, device=DEV), scales=sc["scales"],
             rotations=sc["rotations"])
+
+
+def _golden_sh_files():
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    out = []
+    for f in sorted(os.listdir(d)) if os.path.isdir(d) else []:
+        if f.endswith(".npz"):
+            z = np.load(os.path.join(d, f), allow_pickle=False)
+            if z["shs"].size and z["shs"].shape[1] > 1:
+                out.append(os.path.join(d, f))
+    return out
+
+
+@pytest.mark.parametrize("path", _golden_sh_files(), ids=lambda p: p.rsplit("/", 1)[-1])
+def test_dc_gradients_match_oracle_fixture(path):
+    """gsr_backward_dc's dL/ddc and dL/drest against the oracle's dL/dsh (the committed
+    fixtures), split into coefficient 0 and the rest -- a direct oracle check of the dc= path,
+    not only a comparison with the full-SH HIP path (gaussian_renderer/__init__.py:90-100)."""
+    dgr = _dgr()
+    z = np.load(path, allow_pickle=False)
+    H, W = int(z["H"]), int(z["W"])
+    t = lambda k: torch.from_numpy(np.ascontiguousarray(z[k], dtype=np.float32)).to(DEV)  # noqa: E731
+    s = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=float(z["tanfovx"]), tanfovy=float(z["tanfovy"]), bg=t("bg"),
+        scale_modifier=float(z["scale_modifier"]), viewmatrix=t("viewmatrix"), projmatrix=t("projmatrix"),
+        sh_degree=int(z["sh_degree"]), campos=t("campos"), prefiltered=False, debug=False,
+        antialiasing=bool(z["antialiasing"]))
+    kw = {k: t(k).requires_grad_(True) for k in ["means3D", "opacities", "scales", "rotations", "cov3D_precomp"]
+          if z[k].size}
+    sh = t("shs")
+    dc = sh[:, :1].contiguous().requires_grad_(True)
+    rest = sh[:, 1:].contiguous().requires_grad_(True)
+    means2D = torch.zeros_like(kw["means3D"], requires_grad=True)
+    color, radii, inv = dgr.GaussianRasterizer(s)(means2D=means2D, dc=dc, shs=rest, **kw)
+    torch.autograd.backward([color, inv], [t("grad_color"), t("grad_invdepth")])
+    torch.cuda.synchronize()
+    ref = z["dL_dsh"].reshape(sh.shape)
+    for name, hip, r in (("dL_ddc", dc.grad, ref[:, :1]), ("dL_drest", rest.grad, ref[:, 1:]),
+                         ("dL_dmeans3D", kw["means3D"].grad, z["dL_dmeans3D"])):
+        ok, rel = common.allclose_rel(hip.cpu().numpy(), r.reshape(hip.shape))
+        assert ok, f"{path}: {name} rel err {rel:.3e}"
