@@ -15,12 +15,14 @@ GRAD_ATOL = 1e-6
 # 1/255 or 1e-4 thresholds ("flipped": n_contrib differs, or some channel is off by more than
 # IMG_ATOL) is allowed to differ; at most this fraction of pixels may, and even there by at
 # most FLIP_MAX_ABS.  Bound of one flipped decision (forward.cu:364-370): a Gaussian k with
-# alpha_k ~ 1/255 blended or not changes the pixel by alpha_k T_k (c_k - C_behind_k - T bg), and
-# the stop rule moves at most the stopping Gaussian's alpha T c with T (1 - alpha) ~ 1e-4, so
-# |d colour| <= (1/255) (|c| + |C| + |bg|) ~ 1e-2 for rgb, bg <= 1.2 -- the measured maxima sit
-# well below it (parity_stats.json of the GPU run).
-FLIP_FRACTION = 2e-4
-FLIP_MAX_ABS = 1e-2
+# alpha_k ~ 1/255 blended or not changes the pixel by alpha_k T_k (c_k - C_behind_k), and the
+# stop rule moves the stopping Gaussian's alpha T c with T (1 - alpha) ~ 1e-4, so
+# |d colour| <= (1/255) |c_k - C_behind| ~ 5e-3 for the synthetic scenes' rgb (<= 1.2), and
+# |d final_T| <= 1/255.  Measured (GPU round 2, gpurun_out/*/parity_stats.json): config 2
+# (1M, 1080p) 8 of 2.07M pixels flipped, largest 5.9e-4; the 3840x2176 case 2 of 8.4M pixels,
+# 2.05e-3 (a flip at T ~ 1, final_T off by 1/255); every other case none.
+FLIP_FRACTION = 1e-4
+FLIP_MAX_ABS = 5e-3
 # every check_render call appends its statistics here; conftest writes them to
 # gpurun_out/parity_stats.json at the end of a session that has any
 PARITY_LOG = []
