@@ -28,42 +28,127 @@ def _small_case(P=300, H=64, W=96, seed=3):
     return case
 
 
+def _dense_inputs(case, mode, dtype=torch.float64):
+    sc = case["scene"]
+    inp = {"means3D": sc["means3D"].to(dtype).requires_grad_(True),
+           "opacities": sc["opacities"].to(dtype).requires_grad_(True)}
+    if mode.startswith("sh"):
+        inp["shs"] = sc["shs"].to(dtype).requires_grad_(True)
+    else:
+        inp["colors_precomp"] = case["colors_precomp"].to(dtype).requires_grad_(True)
+    if mode.endswith("scales"):
+        inp["scales"] = sc["scales"].to(dtype).requires_grad_(True)
+        inp["rotations"] = sc["rotations"].to(dtype).requires_grad_(True)
+    else:
+        inp["cov3D_precomp"] = case["cov3D_precomp"].to(dtype).requires_grad_(True)
+    return inp
+
+
+PAIRS = {"means3D": "dL_dmeans3D", "opacities": "dL_dopacity", "shs": "dL_dsh", "colors_precomp": "dL_dcolors",
+         "scales": "dL_dscales", "rotations": "dL_drotations", "cov3D_precomp": "dL_dcov3D"}
+
+
+def _decisions_agree(o, out):
+    """The dense restatement's own float64 decisions against the oracle's float32 ones: radii
+    equal, n_contrib equal on every pixel whose decisions are not within float32 reach of a
+    threshold (forward.cu:356-370)."""
+    np.testing.assert_array_equal(out["radii"].numpy(), o.radii)
+    nc = out["n_contrib"].numpy()
+    diff = nc != o.get("n_contrib")
+    tie = out["tie"].numpy()
+    assert not np.any(diff & ~tie), f"n_contrib differs on {int((diff & ~tie).sum())} non-tie pixels"
+    assert tie.mean() < 1e-2
+    return int(diff.sum())
+
+
 @pytest.mark.parametrize("mode", ["sh_scales", "colors_cov"])
 @pytest.mark.parametrize("antialiasing", [False, True])
 def test_oracle_backward_matches_autograd(mode, antialiasing):
+    """Oracle backward vs torch.autograd of the dense float64 restatement, whose blend decisions
+    (tile rects, power > 0, alpha < 1/255, the stop rule excluding the stopping Gaussian) are its
+    own -- not the oracle's."""
     case = _small_case()
     o, og = common.run_oracle(case, mode, antialiasing=antialiasing)
     assert o.num_rendered > 100
-    contrib = dense_ref.frozen_contributors(o)
-    assert sum(len(r) for r in contrib) > 1000
-    cam = case["cam"]
-    sc = case["scene"]
-    d = torch.float64
-    inp = {"means3D": sc["means3D"].to(d).requires_grad_(True), "opacities": sc["opacities"].to(d).requires_grad_(True)}
-    if mode.startswith("sh"):
-        inp["shs"] = sc["shs"].to(d).requires_grad_(True)
-    else:
-        inp["colors_precomp"] = case["colors_precomp"].to(d).requires_grad_(True)
-    if mode.endswith("scales"):
-        inp["scales"] = sc["scales"].to(d).requires_grad_(True)
-        inp["rotations"] = sc["rotations"].to(d).requires_grad_(True)
-    else:
-        inp["cov3D_precomp"] = case["cov3D_precomp"].to(d).requires_grad_(True)
-    camd = {"view": cam.world_view_transform.to(d), "proj": cam.full_proj_transform.to(d),
-            "campos": cam.camera_center.to(d), "tanfovx": cam.tanfovx, "tanfovy": cam.tanfovy}
-    col, inv, alpha = dense_ref.dense_forward(inp, camd, case["H"], case["W"], 3, case["bg"].to(d), contrib,
-                                              antialiasing=antialiasing)
-    assert float(alpha.max()) < 0.99
+    inp = _dense_inputs(case, mode)
+    out = dense_ref.dense_render(inp, dense_ref.ring_cam(case["cam"]), case["H"], case["W"], 3,
+                                 case["bg"].to(torch.float64), antialiasing=antialiasing)
+    _decisions_agree(o, out)
+    assert int((out["n_contrib"] > 0).sum()) > 500
+    assert float(out["alpha_max"]) < 0.99
     # forward agreement (fp32 oracle vs fp64 dense)
-    assert np.abs(col.detach().numpy() - o.color).max() < 1e-4
-    assert np.abs(inv.detach().numpy() - o.invdepth).max() < 1e-4
-    loss = (col * case["grad_color"].to(d)).sum() + (inv * case["grad_invdepth"].to(d)).sum()
-    loss.backward()
-    pairs = {"means3D": "dL_dmeans3D", "opacities": "dL_dopacity", "shs": "dL_dsh", "colors_precomp": "dL_dcolors",
-             "scales": "dL_dscales", "rotations": "dL_drotations", "cov3D_precomp": "dL_dcov3D"}
+    assert np.abs(out["color"].detach().numpy() - o.color).max() < 1e-4
+    assert np.abs(out["invdepth"].detach().numpy() - o.invdepth).max() < 1e-4
+    assert np.abs(out["final_T"].numpy() - o.get("final_T").reshape(-1)).max() < 1e-4
+    dense_ref.loss_of(out, case["grad_color"].to(torch.float64), case["grad_invdepth"].to(torch.float64)).backward()
     for k, t in inp.items():
-        ok, rel = common.allclose_rel(og[pairs[k]].reshape(t.shape), t.grad.numpy(), rtol=2e-4, atol=1e-7)
+        ok, rel = common.allclose_rel(og[PAIRS[k]].reshape(t.shape), t.grad.numpy(), rtol=2e-4, atol=1e-7)
         assert ok, f"{mode} aa={antialiasing}: oracle d{k} vs autograd rel err {rel:.3e}"
+
+
+def _fd_case(seed=5):
+    """<= 16 Gaussians in front of view 0 of the ring, overlapping on a 48x40 image: every one
+    visible, alpha < 0.99 everywhere (no clamp kink), SH colours > 0 (no clamp kink)."""
+    P, H, W = 14, 40, 48
+    case = common.make_case(P=P, H=H, W=W, seed=seed)
+    g = torch.Generator().manual_seed(seed)
+    sc = case["scene"]
+    sc["means3D"] = (torch.rand(P, 3, generator=g) - 0.5) * torch.tensor([1.4, 1.12, 1.4])
+    sc["scales"] = 0.25 + 0.25 * torch.rand(P, 3, generator=g)
+    sc["opacities"] = 0.3 + 0.5 * torch.rand(P, 1, generator=g)
+    sc["shs"][:, 0] = 1.0 + torch.rand(P, 3, generator=g)
+    case["colors_precomp"] = 0.2 + torch.rand(P, 3, generator=g)
+    case["bg"] = torch.tensor([0.1, 0.4, 0.7])
+    o, _ = common.run_oracle(case, backward=False)
+    case["cov3D_precomp"] = torch.from_numpy(o.get("cov3D").copy())
+    return case
+
+
+@pytest.mark.parametrize("mode", ["sh_scales", "colors_cov"])
+@pytest.mark.parametrize("antialiasing", [False, True])
+def test_finite_differences(mode, antialiasing):
+    """central finite differences of the dense float64 forward (its own decisions
+    re-made at every evaluation) on 14 Gaussians, against the oracle's analytic backward.
+    With antialiasing the reference's AA-scale derivative is evaluated at the dilated covariance
+    (backward.cu:213-246, RefAAScale): the finite differences then pin the exact derivative
+    (autograd with aa_quirk=False) and the oracle's opacity / colour / SH gradients, which the
+    quirk does not touch; the oracle's geometry gradients are pinned to the quirk through
+    test_oracle_backward_matches_autograd."""
+    case = _fd_case()
+    o, og = common.run_oracle(case, mode, antialiasing=antialiasing)
+    H, W = case["H"], case["W"]
+    cam = dense_ref.ring_cam(case["cam"])
+    bg = case["bg"].to(torch.float64)
+    gc, gi = case["grad_color"].to(torch.float64), case["grad_invdepth"].to(torch.float64)
+    inp = _dense_inputs(case, mode)
+    out = dense_ref.dense_render(inp, cam, H, W, 3, bg, antialiasing=antialiasing)
+    assert int(out["radii"].gt(0).sum()) == case["scene"]["means3D"].shape[0]
+    _decisions_agree(o, out)
+    assert not bool(out["tie"].any())
+    assert float(out["alpha_max"]) < 0.99 and int((out["n_contrib"] > 0).sum()) > 0.5 * H * W
+    assert np.abs(out["color"].detach().numpy() - o.color).max() < 1e-5
+    assert np.abs(out["invdepth"].detach().numpy() - o.invdepth).max() < 1e-5
+    assert np.abs(out["final_T"].numpy() - o.get("final_T").reshape(-1)).max() < 1e-5
+
+    def loss():
+        return dense_ref.loss_of(dense_ref.dense_render(inp, cam, H, W, 3, bg, antialiasing=antialiasing), gc, gi)
+
+    exact = {}
+    if antialiasing:
+        dense_ref.loss_of(dense_ref.dense_render(inp, cam, H, W, 3, bg, antialiasing=True, aa_quirk=False),
+                          gc, gi).backward()
+        exact = {k: t.grad.clone() for k, t in inp.items()}
+    for k, t in inp.items():
+        fd = dense_ref.finite_difference(loss, t.data)
+        scale = float(fd.abs().max())
+        assert scale > 0
+        if antialiasing:  # finite differences == exact autograd of the dense forward
+            ok, rel = common.allclose_rel(exact[k].numpy(), fd.numpy(), rtol=1e-5, atol=1e-9)
+            assert ok, f"{mode} aa: autograd(exact) d{k} vs finite differences rel err {rel:.3e}"
+            if k not in ("opacities", "shs", "colors_precomp"):
+                continue
+        ok, rel = common.allclose_rel(og[PAIRS[k]].reshape(t.shape), fd.numpy(), rtol=1e-4, atol=1e-8)
+        assert ok, f"{mode} aa={antialiasing}: oracle d{k} vs finite differences rel err {rel:.3e}"
 
 
 def test_binning_invariants():
