@@ -1,25 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark: rendered Mpix/s, forward+backward, 1M Gaussians @ 1920x1080 (BASELINE.json).
 
-One step = for each view this rank owns: forward + backward of the differentiable rasterizer
-through the drop-in surface (diff_gaussian_rasterization.GaussianRasterizer + autograd),
-gradients accumulated into the replicated Gaussian parameters; then, with N>1 ranks, one
-RCCL all_reduce(SUM) of the 236 B/Gaussian parameter-gradient bucket.
-A step is one optimizer step's batch.  At N=1 it is ONE view (BASELINE config 2: a single
-1080p view, fwd+bwd; no collective).  At N>1 each rank renders a mini-batch of `--views-per-rank`
-views (default 8: config 4's 8-view batch, per GPU), accumulates their gradients and joins ONE
-all-reduce, so the collective is amortised over the batch as a data-parallel training step would
-do it; the per-view work is the same at every N (weak scaling; the views of all ranks are distinct
-cameras on one ring).
+One step = one optimizer step's batch of camera views (BASELINE config 4): for each
+view this rank owns, forward + backward of the differentiable rasterizer through the drop-in
+surface (diff_gaussian_rasterization.GaussianRasterizer + autograd), gradients accumulated into
+the replicated Gaussian parameters; then, with N>1 ranks, ONE RCCL all_reduce(SUM) of the
+236 B/Gaussian parameter-gradient bucket.  Every view is BASELINE config 2's workload (1M
+Gaussians, SH degree 3, one 1920x1080 ring view, fwd+bwd).
+
+Default (strong scaling, config 4 as §8e defines it): `--views-total 8` views per step at every N,
+view v on rank v mod N -- 8 views on one GPU, 1 view + the all-reduce per GPU at N=8, so the N=1
+and N=8 lines describe the same 8-view step.  `--views-per-rank K` (weak scaling): K views per
+rank at every N, the same K at N=1.
 
 Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes
+import glob
+import hashlib
 import json
 import os
+import shutil
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -35,6 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # VALU issue peak: 256 CUs x 4 SIMD-32 units, one wave64 VALU instruction per 2 cycles per SIMD
 # (MI355X_MICROARCH.md), at the 2.4 GHz the PMC runs measure (GRBM_GUI_ACTIVE / kernel time)
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1,228.8 G wave-instructions/s
+N_RING = 8  # distinct ring cameras (synthetic.Camera)
 
 
 def parse():
@@ -45,13 +53,19 @@ def parse():
     ap.add_argument("--P", type=int, default=1_000_000)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--views-total", type=int, default=8,
+                    help="views per step over all ranks (strong scaling; view v on rank v mod N)")
     ap.add_argument("--views-per-rank", type=int, default=0,
-                    help="views per rank per step; 0 = 1 on one GPU, 8 (one all-reduce per 8-view batch) on N>1")
+                    help="> 0: weak scaling, this many views per rank at every N (overrides --views-total)")
     ap.add_argument("--antialiasing", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median reported)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-aux", action="store_true", help="skip the §8f side measurements (distCUDA2)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 --pmc passes (traffic then from the stamped profiles/ file)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
     return ap.parse_args()
 
 
@@ -73,6 +87,54 @@ def algorithmic_bytes(P, M, L, N, T, P_vis):
         "render_bwd": L * 44 + N * 24 + T * 8,                  # id + record per instance; 24 B/pixel in
         "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in
     }
+
+
+def lib_sha256():
+    """Identity of the native library this process rasterizes with (stamps PMC traffic figures)."""
+    import diff_gaussian_rasterization as dgr
+    h = hashlib.sha256()
+    with open(dgr._C.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()
+
+
+def pmc_traffic(args, timeout=240):
+    """HBM traffic per launch of every rasterizer kernel, measured now on this build: two
+    rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: together they exceed the 4 TCC counters
+    of one pass) over this script's own workload (`--pmc-child`: the same views, 1 warm-up + 1
+    step), each a child process under a time limit; bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per
+    MI355X_MICROARCH.md §HBM, per launch (tools/pmc_summary.py).  None if rocprofv3 is absent or a
+    pass fails."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_summary
+    tmp = tempfile.mkdtemp(prefix="gsr_pmc_")
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "1", "--warmup", "1",
+             "--P", str(args.P), "--width", str(args.width), "--height", str(args.height),
+             "--views-total", str(args.views_total), "--views-per-rank", str(args.views_per_rank)]
+    if args.antialiasing:
+        child.append("--antialiasing")
+    env = dict(os.environ, TMPDIR=tmp)
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            r = subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(tmp, counter),
+                                "-o", "run", "--"] + child, env=env, cwd=ROOT, timeout=timeout,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            if r.returncode != 0:
+                return None
+        with open(os.devnull, "w") as devnull:
+            old, sys.stdout = sys.stdout, devnull
+            try:
+                pmc_summary.main(tmp)
+            finally:
+                sys.stdout = old
+        return json.load(open(os.path.join(tmp, "pmc_traffic.json")))["bytes_per_launch"]
+    except Exception:
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():
@@ -104,9 +166,15 @@ def main():
     scene = synthetic.make_scene(P, seed=0)
     params = {k: v.to(dev).requires_grad_(True) for k, v in scene.items()}
     M = params["shs"].shape[1]
-    vpr = args.views_per_rank or (1 if world == 1 else 8)
-    n_ring = max(8, vpr * world)  # distinct cameras for every view of every rank
-    views = multiview.views_for_rank(rank, world, vpr, n_views=n_ring)
+    if args.views_per_rank > 0:  # weak scaling: K views per rank, distinct cameras over all ranks
+        mode, scaling = "weak", "weak"
+        n_ring = max(N_RING, args.views_per_rank * world)
+        views = multiview.views_for_rank(rank, world, args.views_per_rank, n_views=n_ring)
+    else:  # strong scaling: a fixed batch of views per step, dealt round-robin
+        mode, scaling = "strong", "strong"
+        n_ring = max(N_RING, args.views_total)
+        views = multiview.views_of_batch(rank, world, args.views_total)
+    views_step = world * len(views) if mode == "weak" else args.views_total
     cams, grads = [], []
     for v in views:
         cam = synthetic.Camera(W, H, view=v, n_views=n_ring)
@@ -138,6 +206,12 @@ def main():
         if record_allreduce:
             e1.record()
             ar_events.append((e0, e1, nbytes))
+
+    if args.pmc_child:  # the workload of one --pmc pass (pmc_traffic): nothing printed, nothing timed
+        for _ in range(args.warmup + args.steps):
+            step()
+        torch.cuda.synchronize()
+        return
 
     for _ in range(args.warmup):
         step()
@@ -182,7 +256,7 @@ def main():
                      "fraction_of_step": round(ar_ms / (elapsed / args.steps * 1e3), 3),
                      "algbw_GBps": round(ar_events[0][2] / (ar_ms * 1e-3) / 1e9, 1)}
 
-    # geometry of the workload (one extra forward outside the timed region)
+    # geometry of the workload (one extra forward per view outside the timed region)
     with torch.no_grad():
         Ls, vis = [], []
         for s in cams:  # per-view geometry, averaged like the per-kernel times are
@@ -196,7 +270,7 @@ def main():
         P_vis = round(sum(vis) / len(vis))
     N = H * W
     T = ((W + 15) // 16) * ((H + 15) // 16)
-    pix_total = world * len(views) * N * args.steps
+    pix_total = views_step * N * args.steps
     value = pix_total / elapsed / 1e6
     if rank != 0:
         if world > 1:
@@ -208,31 +282,48 @@ def main():
         ab = algorithmic_bytes(P, M, L, N, T, P_vis)
         dom = max(kern, key=lambda k: kern[k]["avg_ms"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):
+        sha = lib_sha256()
+        traffic, traffic_src, traffic_all = None, None, None
+        measured = None if (args.no_pmc or world > 1) else pmc_traffic(args)
+        if measured and dom in measured:
+            traffic, traffic_src, traffic_all = measured[dom], "rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (this run)", \
+                measured
+        else:  # the committed figures, only if they were measured on this very library build
+            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
             try:
-                traffic = json.load(open(tf)).get(dom)
+                stamped = json.load(open(tf))
+                if stamped.get("lib_sha256") == sha:
+                    traffic, traffic_src = stamped["bytes_per_launch"].get(dom), "profiles/pmc_traffic.json (same build)"
+                    traffic_all = stamped["bytes_per_launch"]
+                else:
+                    traffic_src = "stale: profiles/pmc_traffic.json was measured on another build"
             except Exception:
-                traffic = None
+                traffic_src = "unavailable"
         valu = None  # secondary roofline: render kernels are VALU-issue bound, not HBM bound
         vf = os.path.join(ROOT, "profiles", "pmc_valu.json")
-        if os.path.exists(vf):
-            try:
-                vi = json.load(open(vf))
+        try:
+            vi = json.load(open(vf))
+            if vi.get("lib_sha256") == sha:
+                vi = vi["winst_per_launch"]
                 valu = {k: {"winst_per_launch": vi[k],
                             "achieved_Ginst_s": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
                             "frac": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
                         for k in kern if k in vi}
-                valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": "profiles/pmc_valu.json (SQ_INSTS_VALU)",
+                valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": "profiles/pmc_valu.json (SQ_INSTS_VALU, same build)",
                         "kernels": valu}
-            except Exception:
-                valu = None
+        except Exception:
+            valu = None
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": traffic_src, "traffic_stale": traffic is None and traffic_src is not None
+                    and traffic_src.startswith("stale"), "lib_sha256": sha[:16],
                     "algorithmic_bytes": ab[dom],
                     "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
-                                    "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1)} for k, v in kern.items()},
+                                    "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1),
+                                    "algorithmic_bytes": ab[k], "traffic": (traffic_all or {}).get(k)}
+                                for k, v in kern.items()},
+                    # the depth and tile sorts share their kernels: their traffic is reported together
+                    "radix_sorts_traffic": (traffic_all or {}).get("radix_sorts"),
                     "valu": valu}
 
     cpu = None
@@ -246,6 +337,13 @@ def main():
                "sparse_adam": aux_sparse_adam(dgr, params, cams[0], grads[0], args),
                "train_iteration": aux_train_iteration(dgr, params, cams[0], H, W)}
 
+    if mode == "strong":
+        workload = (f"BASELINE config 4: {args.views_total} views per step of config 2 ({P} Gaussians, SH deg 3, "
+                    f"{W}x{H}, fwd+bwd each), view v on rank v mod {world}"
+                    + (", one RCCL grad all-reduce per step" if world > 1 else ", grads accumulated on one GPU"))
+    else:
+        workload = (f"{args.views_per_rank} views per rank per step of config 2 ({P} Gaussians, SH deg 3, {W}x{H}, "
+                    f"fwd+bwd each)" + (", one RCCL grad all-reduce per step" if world > 1 else ""))
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
         "value": round(value, 2),
@@ -255,13 +353,12 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seed-0 Gaussian cloud, SURVEY.md §8d; ring camera views)",
-        "config": {"workload": f"{P} Gaussians, SH deg 3, {W}x{H}, {len(views)} view(s)/rank, fwd+bwd"
-                               + (" + RCCL grad all-reduce" if world > 1 else ""),
-                   "P": P, "width": W, "height": H, "views_per_rank": len(views), "num_rendered": L,
+        "config": {"workload": workload, "P": P, "width": W, "height": H, "views_per_step": views_step,
+                   "views_per_rank": len(views), "num_rendered": L, "num_rendered_per_view": Ls,
                    "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
@@ -491,23 +588,29 @@ def aux_ssim(H, W, dev, args, reps=20):
 
 
 def cpu_baseline(args, scene, s, grad):
-    """The CPU oracle (oracle/gsr_oracle.c, OpenMP) on the same view: one forward+backward."""
+    """The CPU oracle (oracle/gsr_oracle.c, OpenMP) on the bench's first view: one
+    forward+backward per run, --cpu-reps runs, the median reported."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         gc, gi = grad
-        t = time.perf_counter()
-        o = oracle.OracleRaster(scene["means3D"], scene["opacities"], s.bg.cpu(), s.viewmatrix.cpu(),
-                                s.projmatrix.cpu(), s.campos.cpu(), s.tanfovx, s.tanfovy, s.image_height,
-                                s.image_width, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
-                                rotations=scene["rotations"], antialiasing=args.antialiasing, nthreads=threads)
-        o.backward(gc.cpu(), gi.cpu())
-        dt = time.perf_counter() - t
+        gc, gi = gc.cpu(), gi.cpu()
+        times = []
+        for _ in range(max(1, args.cpu_reps)):
+            t = time.perf_counter()
+            o = oracle.OracleRaster(scene["means3D"], scene["opacities"], s.bg.cpu(), s.viewmatrix.cpu(),
+                                    s.projmatrix.cpu(), s.campos.cpu(), s.tanfovx, s.tanfovy, s.image_height,
+                                    s.image_width, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
+                                    rotations=scene["rotations"], antialiasing=args.antialiasing, nthreads=threads)
+            o.backward(gc, gi)
+            times.append(time.perf_counter() - t)
+            del o
+        dt = statistics.median(times)
         return {"value": round(s.image_height * s.image_width / dt / 1e6, 3), "unit": "Mpix/s", "cores": threads,
-                "kind": "port", "seconds": round(dt, 2),
-                "sample": f"one full fwd+bwd of the bench view ({args.P} Gaussians, "
-                          f"{s.image_width}x{s.image_height}) by the C/OpenMP oracle"}
+                "kind": "port", "seconds": round(dt, 3), "runs_s": [round(x, 3) for x in times],
+                "sample": f"one full fwd+bwd of one bench view ({args.P} Gaussians, {s.image_width}x"
+                          f"{s.image_height}) by the C/OpenMP oracle, median of {len(times)} runs"}
     except Exception as e:  # the baseline must never take the GPU result down
         return {"value": None, "unit": "Mpix/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 

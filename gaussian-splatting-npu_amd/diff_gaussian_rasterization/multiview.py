@@ -26,6 +26,16 @@ def views_for_rank(rank, world, views_per_rank=1, n_views=8):
     return [(rank + i * world) % n_views for i in range(views_per_rank)]
 
 
+def views_of_batch(rank, world, views_total=8):
+    """Views this rank renders when a step is a fixed batch of `views_total` views dealt
+    round-robin (strong scaling): v = rank, rank + world, ... < views_total."""
+    if not (0 <= rank < world):
+        raise ValueError(f"rank {rank} outside world {world}")
+    if views_total < world:
+        raise ValueError(f"{views_total} views cannot occupy {world} ranks")
+    return list(range(rank, views_total, world))
+
+
 def grad_bucket(params, order=PARAM_ORDER):
     """Flat fp32 view of every parameter gradient (a fresh contiguous buffer)."""
     return torch.cat([params[k].grad.reshape(-1) for k in order])

@@ -196,3 +196,13 @@ def test_single_process_is_a_noop():
         assert torch.equal(params[k].grad, before[k])
     with pytest.raises(ValueError):
         multiview.views_for_rank(2, 2)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_views_of_batch_strong_scaling(world):
+    """bench.py's default step: the same 8-view batch at every N, each view on exactly one rank."""
+    per = [multiview.views_of_batch(r, world, 8) for r in range(world)]
+    assert sorted(v for vs in per for v in vs) == list(range(8))
+    assert all(len(vs) == 8 // world for vs in per)
+    with pytest.raises(ValueError):
+        multiview.views_of_batch(0, 16, 8)

@@ -32,7 +32,7 @@ def short_name(k):
     return None
 
 
-def main(d):
+def main(d, lib_sha256=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -76,13 +76,24 @@ def main(d):
 
     traffic = per_launch(lambda e: (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
                          if "FETCH_SIZE" in e and "WRITE_SIZE" in e else None)
-    json.dump({k: round(v) for k, v in traffic.items()}, open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
+    # stamped with the library they were measured on: bench.py uses committed figures only for that build
+    json.dump({"lib_sha256": lib_sha256, "bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
+              open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
     # VALU wave-instructions per launch (bench.py's secondary, VALU-issue roofline)
     valu = per_launch(lambda e: e.get("SQ_INSTS_VALU"))
-    json.dump({k: round(v) for k, v in valu.items()}, open(os.path.join(d, "pmc_valu.json"), "w"), indent=1)
+    json.dump({"lib_sha256": lib_sha256, "winst_per_launch": {k: round(v) for k, v in valu.items()}},
+              open(os.path.join(d, "pmc_valu.json"), "w"), indent=1)
     print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
                      indent=1))
 
 
+def lib_sha256(path=None):
+    import hashlib
+    path = path or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "gaussian-splatting-npu_amd", "diff_gaussian_rasterization", "libgsr_hip.so")
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], lib_sha256())
