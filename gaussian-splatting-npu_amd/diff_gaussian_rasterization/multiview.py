@@ -123,3 +123,142 @@ def max_over_ranks(seconds, device=None, group=None):
     t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+# ---- train.py's iteration as a data-parallel step ------------------------
+# GaussianModel's parameter groups, in its optimizer order (scene/gaussian_model.py:186-193)
+TRAIN_GROUPS = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+# train.py's learning rates at iteration 1 (arguments/__init__.py:74-100; xyz is scaled by the
+# scene's spatial_lr_scale and decays with get_expon_lr_func -- the caller's update_learning_rate)
+TRAIN_LR = {"xyz": 0.00016, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 0.025, "scaling": 0.005,
+            "rotation": 0.001}
+
+
+class DataParallelTrainer:
+    """train.py's iteration (train.py:97-183) over G ranks, one process per GPU.
+
+    The reference trains on one random view per iteration on one GPU.  Here one step takes a
+    batch of views; every rank holds a full replica of the Gaussians and renders its share of the
+    batch (view v on rank v mod G, `views_of_batch`), and:
+
+    1. renders each of its views through GaussianRasterizer with train.py's inputs
+       (activations of gaussian_model.py:40-48,102-135; the separate-DC surface train.py selects
+       with SparseGaussianAdam, gaussian_renderer/__init__.py:82-100; image clamped to [0, 1],
+       :119), loss = (1 - lambda_dssim) L1 + lambda_dssim (1 - fused SSIM) (train.py:119-124),
+       backward; the per-view losses of the batch add up, so the step's gradient is the SUM of its
+       views' gradients;
+    2. keeps train.py's densification statistics per view, locally (train.py:166,
+       gaussian_model.py:471-473: max screen radius, norm of that view's screen-space gradient,
+       visit count);
+    3. all-reduces (SUM) ONE flat fp32 buffer: every parameter gradient (236 B per Gaussian at SH
+       degree 3; the parameters' .grad are views into it, so autograd accumulates into it in place
+       and the collective runs in place) plus one visibility count per Gaussian, so the same
+       collective tells every rank which Gaussians some view of the step saw;
+    4. steps the same optimizer on every rank: SparseGaussianAdam on the Gaussians visible in the
+       step (train.py:180-183) or torch Adam (the default optimizer_type); identical reduced inputs
+       keep the replicas bit-identical without a broadcast.
+
+    Densification itself stays with the caller (GaussianModel.densify_and_prune); before it runs,
+    `reduced_densification_stats()` gives every rank the statistics of ALL views since the last
+    reset (SUM of accum/denom, MAX of max_radii2D) -- reduced once at that point, not per step, so
+    nothing is counted twice.  Backend-agnostic: RCCL ("nccl") on MI355X nodes, gloo in the tests.
+    """
+
+    def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None):
+        import diff_gaussian_rasterization as dgr
+        self._dgr = dgr
+        dev = raw["xyz"].device
+        self.device = dev
+        self.P = P = raw["xyz"].shape[0]
+        self.group = group
+        self.lambda_dssim = lambda_dssim
+        self.bg = bg if bg is not None else torch.zeros(3, device=dev)
+        lr = dict(TRAIN_LR, **(lr or {}))
+        sizes = [raw[k].numel() for k in TRAIN_GROUPS]
+        # [gradients of every group | visibility count per Gaussian]
+        self.flat = torch.zeros(sum(sizes) + P, dtype=torch.float32, device=dev)
+        self.params = {}
+        off = 0
+        for k, n in zip(TRAIN_GROUPS, sizes):
+            p = torch.nn.Parameter(raw[k].detach().to(dev, torch.float32).contiguous().clone())
+            p.grad = self.flat[off:off + n].view_as(p)
+            self.params[k] = p
+            off += n
+        self.visible_count = self.flat[off:off + P]
+        groups = [{"params": [self.params[k]], "lr": lr[k], "name": k} for k in TRAIN_GROUPS]
+        self.sparse = optimizer == "sparse_adam"
+        self.optimizer = (dgr.SparseGaussianAdam(groups, lr=0.0, eps=1e-15) if self.sparse
+                          else torch.optim.Adam(groups, lr=0.0, eps=1e-15))
+        self.stats = densification_stats(P, dev)
+
+    def activations(self):
+        """GaussianModel.get_* (gaussian_model.py:102-135)."""
+        p = self.params
+        return {"means3D": p["xyz"], "dc": p["f_dc"], "shs": p["f_rest"],
+                "opacities": torch.sigmoid(p["opacity"]), "scales": torch.exp(p["scaling"]),
+                "rotations": torch.nn.functional.normalize(p["rotation"])}
+
+    def zero_grad(self):
+        self.flat.zero_()
+
+    def render(self, settings, act=None):
+        """gaussian_renderer.render with separate_sh=True: (clamped image, screen-space points, radii)."""
+        act = act or self.activations()
+        means2D = torch.zeros_like(act["means3D"], requires_grad=True)
+        means2D.retain_grad()
+        img, radii, _ = self._dgr.GaussianRasterizer(settings)(
+            means3D=act["means3D"], means2D=means2D, dc=act["dc"], shs=act["shs"], colors_precomp=None,
+            opacities=act["opacities"], scales=act["scales"], rotations=act["rotations"], cov3D_precomp=None)
+        return img.clamp(0, 1), means2D, radii
+
+    def render_and_backward(self, views):
+        """Step 1-2 for this rank's views: [(GaussianRasterizationSettings, gt image (3,H,W))].
+        Gradients accumulate into the flat buffer; returns the per-view losses."""
+        from fused_ssim import fused_ssim
+        losses = []
+        for settings, gt in views:
+            img, means2D, radii = self.render(settings)
+            l1 = (img - gt).abs().mean()
+            loss = (1.0 - self.lambda_dssim) * l1 + self.lambda_dssim * (1.0 - fused_ssim(img[None], gt[None]))
+            loss.backward()
+            with torch.no_grad():
+                add_view_stats(self.stats, means2D.grad, radii)
+                self.visible_count += (radii > 0).to(self.visible_count.dtype)
+            losses.append(loss.detach())
+        return losses
+
+    def reduce(self):
+        """Step 3: one in-place all_reduce(SUM) of gradients + visibility counts.  Returns bytes."""
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return 0
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        return self.flat.numel() * self.flat.element_size()
+
+    @torch.no_grad()
+    def optimizer_step(self):
+        """Step 4 (train.py:176-183)."""
+        if self.sparse:
+            self.optimizer.step(self.visible_count > 0, self.P)
+        else:
+            self.optimizer.step()
+
+    def step(self, views):
+        self.zero_grad()
+        losses = self.render_and_backward(views)
+        self.reduce()
+        self.optimizer_step()
+        return losses
+
+    def reduced_densification_stats(self):
+        """Copies of the densification statistics of every view of every rank since the last
+        reset (what GaussianModel.densify_and_prune reads): SUM of xyz_gradient_accum and denom,
+        MAX of max_radii2D.  The local accumulators are left as they are."""
+        out = densification_stats(self.P, self.device)
+        out["_sums"].copy_(self.stats["_sums"])
+        out["max_radii2D"].copy_(self.stats["max_radii2D"])
+        allreduce_densification_stats(out, self.group)
+        return out
+
+    def reset_densification_stats(self):
+        self.stats["_sums"].zero_()
+        self.stats["max_radii2D"].zero_()

@@ -1,0 +1,129 @@
+"""Data-parallel training mode: multiview.DataParallelTrainer on real
+rasterizer gradients (needs an MI355X: -m gpu).
+
+Two gloo ranks share the one GPU of the test box (the driver's multi-GPU nodes run the same code
+over RCCL).  Each step is a batch of 4 of the 8 ring views, view j of the batch on rank j mod 2;
+after ITERS steps of train.py's iteration (sparse Adam, L1 + D-SSIM, separate-DC render) the
+parameters of both ranks must be bit-identical to each other AND to a single process that renders
+the same views and sums the two ranks' gradient buffers itself (x0 + x1: a two-rank all-reduce adds
+each element once, and float addition commutes), and the reduced densification statistics must
+equal the single process's.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+P, H, W, VIEWS, BATCH, ITERS, WORLD = 2000, 96, 128, 8, 4, 3, 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setup(dev):
+    """Trainer (perturbed start of the seed-0 cloud), settings per view and ground-truth images."""
+    import synthetic
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import multiview
+    gt = synthetic.make_scene(P, seed=0)
+    g = torch.Generator().manual_seed(5)
+    raw = {"xyz": gt["means3D"] + 0.02 * torch.randn(P, 3, generator=g),
+           "f_dc": gt["shs"][:, :1] + 0.3 * torch.randn(P, 1, 3, generator=g),
+           "f_rest": gt["shs"][:, 1:].clone(),
+           "opacity": torch.full((P, 1), -1.0),
+           "scaling": torch.log(gt["scales"]) + 0.3 * torch.randn(P, 3, generator=g),
+           "rotation": gt["rotations"] + 0.1 * torch.randn(P, 4, generator=g)}
+    trainer = multiview.DataParallelTrainer({k: v.to(dev) for k, v in raw.items()}, lr={"xyz": 4.8e-4})
+    settings = []
+    for v in range(VIEWS):
+        c = synthetic.Camera(W, H, view=v)
+        settings.append(dgr.GaussianRasterizationSettings(
+            H, W, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev), 1.0, c.world_view_transform.to(dev),
+            c.full_proj_transform.to(dev), 3, c.camera_center.to(dev), False, False, False))
+    gt_t = {k: v.to(dev) for k, v in gt.items()}
+    with torch.no_grad():
+        targets = [dgr.GaussianRasterizer(s)(means3D=gt_t["means3D"], means2D=torch.zeros_like(gt_t["means3D"]),
+                                             shs=gt_t["shs"], opacities=gt_t["opacities"], scales=gt_t["scales"],
+                                             rotations=gt_t["rotations"])[0].clamp(0, 1) for s in settings]
+    return trainer, settings, targets
+
+
+def _rank_views(it, rank, settings, targets):
+    from diff_gaussian_rasterization import multiview
+    batch = [(BATCH * it + j) % VIEWS for j in range(BATCH)]
+    return [(settings[batch[j]], targets[batch[j]]) for j in multiview.views_of_batch(rank, WORLD, BATCH)]
+
+
+def _result(trainer):
+    st = trainer.reduced_densification_stats()
+    return ({k: p.detach().cpu().numpy() for k, p in trainer.params.items()},
+            {k: st[k].cpu().numpy() for k in ("xyz_gradient_accum", "denom", "max_radii2D")})
+
+
+def _worker(rank, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "gaussian-splatting-npu_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        trainer, settings, targets = _setup(dev)
+        for it in range(ITERS):
+            trainer.step(_rank_views(it, rank, settings, targets))
+        torch.cuda.synchronize()
+        q.put((rank,) + _result(trainer))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_match_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+
+    # the single-process run of the same step: both ranks' views, their buffers summed here
+    dev = torch.device("cuda", 0)
+    trainer, settings, targets = _setup(dev)
+    start = {k: p.detach().clone() for k, p in trainer.params.items()}
+    for it in range(ITERS):
+        trainer.zero_grad()
+        trainer.render_and_backward(_rank_views(it, 0, settings, targets))
+        g0 = trainer.flat.clone()
+        trainer.zero_grad()
+        trainer.render_and_backward(_rank_views(it, 1, settings, targets))
+        trainer.flat += g0
+        trainer.optimizer_step()
+    torch.cuda.synchronize()
+    params, stats = _result(trainer)
+    assert any(not torch.equal(start[k], trainer.params[k]) for k in start), "the step changed nothing"
+    for rank, p_r, s_r in res:
+        for k in params:
+            np.testing.assert_array_equal(p_r[k], params[k], err_msg=f"rank {rank} {k}")
+        np.testing.assert_array_equal(s_r["denom"], stats["denom"])
+        np.testing.assert_array_equal(s_r["max_radii2D"], stats["max_radii2D"])
+        np.testing.assert_allclose(s_r["xyz_gradient_accum"], stats["xyz_gradient_accum"], rtol=1e-5, atol=1e-9)
+    assert stats["denom"].max() > 0
