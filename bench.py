@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-aux", action="store_true", help="skip the §8f side measurements (distCUDA2)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc passes (traffic then from the stamped profiles/ file)")
+    ap.add_argument("--no-fused-accumulation", action="store_true",
+                    help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
     return ap.parse_args()
 
@@ -195,9 +197,12 @@ def main():
         for s, (gc, gi) in zip(cams, grads):
             rast = dgr.GaussianRasterizer(raster_settings=s)
             means2D = torch.zeros_like(params["means3D"], requires_grad=True)
-            color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
-                                     opacities=params["opacities"], scales=params["scales"],
-                                     rotations=params["rotations"])
+            # views after the first add their gradients into the parameters' .grad inside the
+            # backward kernel (dgr.accumulate_grads_in_place) instead of autograd's separate add
+            with dgr.accumulate_grads_in_place(not args.no_fused_accumulation):
+                color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
+                                         opacities=params["opacities"], scales=params["scales"],
+                                         rotations=params["rotations"])
             torch.autograd.backward([color, inv], [gc, gi])
         if record_allreduce:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

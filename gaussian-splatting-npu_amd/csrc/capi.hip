@@ -17,6 +17,11 @@
 
 using namespace gsr;
 
+static_assert(GSR_ACC_MEANS3D == ACC_MEANS3D && GSR_ACC_DC == ACC_DC && GSR_ACC_SH == ACC_SH &&
+                  GSR_ACC_OPACITY == ACC_OPACITY && GSR_ACC_SCALES == ACC_SCALES &&
+                  GSR_ACC_ROTATIONS == ACC_ROTATIONS && GSR_ACC_COV3D == ACC_COV3D && GSR_ACC_COLORS == ACC_COLORS,
+              "include/gsr.h accumulate bits match the kernel's");
+
 namespace {
 
 thread_local std::string g_err;
@@ -503,15 +508,18 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     return GSR_OK;
 }
 
-int gsr_backward_dc(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
-                 const float* dc, const float* shs, const float* colors_precomp, const float* opacities, const float* scales,
-                 float scale_modifier, const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
-                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
-                 char* geom_buffer, char* binning_buffer, char* image_buffer, const float* dL_dpix,
-                 const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
-                 float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale,
-                 float* dL_drot, bool antialiasing, bool debug, gsr_stream_t stream)
+int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int width, int height,
+                        const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                        const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                        const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                        const float* campos, float tan_fovx, float tan_fovy, const int* radii, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, const float* dL_invdepths,
+                        float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                        float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                        float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
+                        gsr_stream_t stream)
 {
+    if (accumulate & ~(unsigned)GSR_ACC_ALL) return fail(GSR_ERR_INVALID, "unknown accumulate bits");
     if (dc && !dL_ddc) return fail(GSR_ERR_INVALID, "dc given without dL_ddc");
     if (dc && colors_precomp)
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
@@ -586,12 +594,30 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
     p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;
     p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;
+    p.acc = accumulate;
     {
         ProfScope ps_(PK_PREPROCESS_BWD, s);
         HIP_TRY(launch_preprocess_bwd(p, s));
     }
     DEBUG_SYNC(s);
     return GSR_OK;
+}
+
+int gsr_backward_dc(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                    const float* dc, const float* shs, const float* colors_precomp, const float* opacities,
+                    const float* scales, float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                    const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                    float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                    const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic,
+                    float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D, float* dL_dcov3D,
+                    float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot, bool antialiasing, bool debug,
+                    gsr_stream_t stream)
+{
+    return gsr_backward_dc_acc(P, D, M, R, background, width, height, means3D, dc, shs, colors_precomp, opacities,
+                               scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos,
+                               tan_fovx, tan_fovy, radii, geom_buffer, binning_buffer, image_buffer, dL_dpix,
+                               dL_invdepths, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D,
+                               dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug, 0u, stream);
 }
 
 // ---- the non-dc entry points: the reference's Rasterizer API (rasterizer.h:31-90) ----

@@ -299,8 +299,18 @@ __device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, in
     }
 }
 
+// acc: add to the destination (in-place gradient accumulation) instead of overwriting it
+__device__ __forceinline__ float4 acc4(float4* d, float4 v, bool acc)
+{
+    if (acc) {
+        const float4 o = *d;
+        v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    }
+    return v;
+}
+
 __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const float* lds, int stride, int col0,
-                                             int ncols)
+                                             int ncols, bool acc = false)
 {
     const int total = n * w;
     int e0 = 0;
@@ -315,13 +325,14 @@ __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const flo
                 vv[q] = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
                 if (++j == w) { j = 0; g++; }
             }
-            d4[f] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            d4[f] = acc4(d4 + f, make_float4(vv[0], vv[1], vv[2], vv[3]), acc);
         }
         e0 = nv4 << 2;
     }
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) {
         const int g = e / w, j = e - g * w;
-        dst[e] = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
+        const float v = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
+        dst[e] = acc ? dst[e] + v : v;
     }
 }
 
@@ -341,16 +352,17 @@ __device__ __forceinline__ void lds_copy_in(float* lds, const float* src, int to
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) lds[e] = src[e];
 }
 
-__device__ __forceinline__ void lds_copy_out(float* dst, const float* lds, int total)
+__device__ __forceinline__ void lds_copy_out(float* dst, const float* lds, int total, bool acc = false)
 {
     int e0 = 0;
     if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)lds & 15) == 0) {
         const int nv4 = total >> 2;
+        float4* d4 = reinterpret_cast<float4*>(dst);
         for (int f = threadIdx.x; f < nv4; f += blockDim.x)
-            reinterpret_cast<float4*>(dst)[f] = reinterpret_cast<const float4*>(lds)[f];
+            d4[f] = acc4(d4 + f, reinterpret_cast<const float4*>(lds)[f], acc);
         e0 = nv4 << 2;
     }
-    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) dst[e] = lds[e];
+    for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) dst[e] = acc ? dst[e] + lds[e] : lds[e];
 }
 
 // Reference getHigherMsb (rasterizer_impl.cu:35-50)

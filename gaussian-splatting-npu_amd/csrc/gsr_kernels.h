@@ -83,6 +83,12 @@ enum GradField {
 };
 constexpr int GRAD_REC = 12;
 
+// In-place gradient accumulation (gsr_backward_dc_acc): bit set = that output array is added to.
+enum AccBits : uint32_t {
+    ACC_MEANS3D = 1u, ACC_DC = 2u, ACC_SH = 4u, ACC_OPACITY = 8u, ACC_SCALES = 16u, ACC_ROTATIONS = 32u,
+    ACC_COV3D = 64u, ACC_COLORS = 128u
+};
+
 struct PreprocessBwdArgs {
     int P, D, M;
     const float* means3D;
@@ -121,6 +127,7 @@ struct PreprocessBwdArgs {
     float* dL_ddc;  // (P,1,3) when dc is given
     float* dL_dscale;
     float* dL_drot;
+    uint32_t acc;  // GSR_ACC_* bits (include/gsr.h): outputs added to instead of overwritten
 };
 
 struct AdamArgs {

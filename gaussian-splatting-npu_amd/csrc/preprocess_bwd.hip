@@ -13,6 +13,9 @@ namespace gsr {
 
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
+// One output element: written, or added to when the caller accumulates into it (AccBits).
+__device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p + v : v; }
+
 // Per-Gaussian inputs, loaded before the workgroup's SH staging so that their memory round trips
 // overlap it (and each other): every load is issued unconditionally (clamped indices, values
 // masked after), so no branch sits between a load and the next one.
@@ -149,7 +152,7 @@ __device__ __forceinline__ void sh_term(int k, float x, float y, float z, float&
 // the same row: every coefficient is read before it is overwritten).
 // Coefficients at or beyond `kw` (the row width in coefficients) are not written.
 template <int K0, int K1>
-__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh, int kw = K1)
+__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh, int kw = K1, bool acc = false)
 {
 #pragma unroll
     for (int k = K0; k < K1; k++) {
@@ -160,12 +163,12 @@ __device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, floa
             for (int c = 0; c < 3; c++) {
                 const float v = sh[(k - K0) * 3 + c];
                 const float t = v * st.dRGB[c];
-                dsh[(k - K0) * 3 + c] = b * st.dRGB[c];
+                put(&dsh[(k - K0) * 3 + c], b * st.dRGB[c], acc);
                 st.ddir[0] += t * gx;
                 st.ddir[1] += t * gy;
                 st.ddir[2] += t * gz;
             }
-        } else if (k < kw) {
+        } else if (k < kw && !acc) {
 #pragma unroll
             for (int c = 0; c < 3; c++) dsh[(k - K0) * 3 + c] = 0.f;
         }
@@ -183,9 +186,10 @@ __device__ __forceinline__ void bwd_finish(const PreprocessBwdArgs& a, int idx, 
         dmy += dn.y;
         dmz += dn.z;
     }
-    dmean[0] = dmx;
-    dmean[1] = dmy;
-    dmean[2] = dmz;
+    const bool acc = a.acc & ACC_MEANS3D;
+    put(dmean, dmx, acc);
+    put(dmean + 1, dmy, acc);
+    put(dmean + 2, dmz, acc);
 }
 
 // Everything of one Gaussian except the SH coefficients: the reduced render gradients,
@@ -204,13 +208,22 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
         a.dL_dconic[4 * i] = 0.f; a.dL_dconic[4 * i + 1] = 0.f; a.dL_dconic[4 * i + 2] = 0.f;
         a.dL_dconic[4 * i + 3] = 0.f;
-        a.dL_dopacity[i] = 0.f;
-        a.dL_dcolor[3 * i] = 0.f; a.dL_dcolor[3 * i + 1] = 0.f; a.dL_dcolor[3 * i + 2] = 0.f;
+        // accumulated outputs gain nothing from a culled Gaussian: left as they are
+        if (!(a.acc & ACC_OPACITY)) a.dL_dopacity[i] = 0.f;
+        if (!(a.acc & ACC_COLORS)) {
+            a.dL_dcolor[3 * i] = 0.f; a.dL_dcolor[3 * i + 1] = 0.f; a.dL_dcolor[3 * i + 2] = 0.f;
+        }
         if (a.dL_dinvdepth) a.dL_dinvdepth[i] = 0.f;
+        if (!(a.acc & ACC_COV3D)) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) dcov_out[k] = 0.f;
-        if (a.dL_dscale) { a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f; }
-        if (a.dL_drot) { float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f; }
+            for (int k = 0; k < 6; k++) dcov_out[k] = 0.f;
+        }
+        if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
+            a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
+        }
+        if (a.dL_drot && !(a.acc & ACC_ROTATIONS)) {
+            float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f;
+        }
         return;
     }
 
@@ -232,7 +245,12 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
     a.dL_dmean2D[3 * i] = g[GF_MEAN2D_X]; a.dL_dmean2D[3 * i + 1] = g[GF_MEAN2D_Y]; a.dL_dmean2D[3 * i + 2] = 0.f;
     a.dL_dconic[4 * i] = g[GF_CONIC_A]; a.dL_dconic[4 * i + 1] = g[GF_CONIC_B]; a.dL_dconic[4 * i + 2] = 0.f;
     a.dL_dconic[4 * i + 3] = g[GF_CONIC_C];
-    a.dL_dcolor[3 * i] = g[GF_COLOR_R]; a.dL_dcolor[3 * i + 1] = g[GF_COLOR_G]; a.dL_dcolor[3 * i + 2] = g[GF_COLOR_B];
+    {
+        const bool acc = a.acc & ACC_COLORS;
+        put(a.dL_dcolor + 3 * i, g[GF_COLOR_R], acc);
+        put(a.dL_dcolor + 3 * i + 1, g[GF_COLOR_G], acc);
+        put(a.dL_dcolor + 3 * i + 2, g[GF_COLOR_B], acc);
+    }
     if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
 
     // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
@@ -276,13 +294,13 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
         const float dL_dopacity_v = g[GF_OPACITY];
         const float d_h_convolution_scaling = dL_dopacity_v * in.opacity;
-        a.dL_dopacity[idx] = dL_dopacity_v * h_convolution_scaling;
+        put(a.dL_dopacity + idx, dL_dopacity_v * h_convolution_scaling, a.acc & ACC_OPACITY);
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
                                                                     : d_h_convolution_scaling / (2 * h_convolution_scaling);
     } else {
         c_xx += h_var;
         c_yy += h_var;
-        a.dL_dopacity[idx] = g[GF_OPACITY];
+        put(a.dL_dopacity + idx, g[GF_OPACITY], a.acc & ACC_OPACITY);
     }
     float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
     if (a.antialiasing) {
@@ -317,7 +335,7 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         for (int k = 0; k < 6; k++) dcov[k] = 0;
     }
 #pragma unroll
-    for (int k = 0; k < 6; k++) dcov_out[k] = dcov[k];
+    for (int k = 0; k < 6; k++) put(dcov_out + k, dcov[k], a.acc & ACC_COV3D);
     const float(*V)[3] = Vrk.m;
     const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
                           (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
@@ -405,9 +423,10 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         const mat3 Rt = mat3_T(R);
         mat3 G = mat3_T(dL_dM);
         float* ds = a.dL_dscale + 3 * i;
-        ds[0] = Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2];
-        ds[1] = Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2];
-        ds[2] = Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2];
+        const bool acc_s = a.acc & ACC_SCALES;
+        put(ds, Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2], acc_s);
+        put(ds + 1, Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2], acc_s);
+        put(ds + 2, Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2], acc_s);
 #pragma unroll
         for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
         const float(*gm)[3] = G.m;
@@ -420,10 +439,15 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         dq.w = 2 * r * (gm[0][1] - gm[1][0]) + 2 * x * (gm[2][0] + gm[0][2]) + 2 * y * (gm[1][2] + gm[2][1]) -
                4 * z * (gm[1][1] + gm[0][0]);
         float* dr = a.dL_drot + 4 * i;
-        dr[0] = dq.x; dr[1] = dq.y; dr[2] = dq.z; dr[3] = dq.w;
+        const bool acc_r = a.acc & ACC_ROTATIONS;
+        put(dr, dq.x, acc_r); put(dr + 1, dq.y, acc_r); put(dr + 2, dq.z, acc_r); put(dr + 3, dq.w, acc_r);
     } else {
-        if (a.dL_dscale) { a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f; }
-        if (a.dL_drot) { float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f; }
+        if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
+            a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
+        }
+        if (a.dL_drot && !(a.acc & ACC_ROTATIONS)) {
+            float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f;
+        }
     }
 }
 
@@ -451,8 +475,10 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
                 const size_t w3 = (size_t)a.M * 3;
                 float* dsh = a.dL_dsh + idx * w3;
                 // ncoef <= M: no read past the row; no write past it either (M < 16)
-                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M);
-                for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
+                const bool acc = a.acc & ACC_SH;
+                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
+                if (!acc)
+                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
             }
             bwd_finish(a, idx, st);
         }
@@ -474,8 +500,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             bwd_finish(a, idx, st);
         }
         __syncthreads();
-        lds_copy_out(a.dL_ddc + (size_t)base * 3, s_sh, n * 3);
-        if (wr > 0) lds_copy_out(a.dL_dsh + (size_t)base * wr, s_rest, n * wr);
+        lds_copy_out(a.dL_ddc + (size_t)base * 3, s_sh, n * 3, a.acc & ACC_DC);
+        if (wr > 0) lds_copy_out(a.dL_dsh + (size_t)base * wr, s_rest, n * wr, a.acc & ACC_SH);
         return;
     }
     if (a.dc) {  // separate dc, wide rest rows: dc -> columns 0-2, rest -> 3..47
@@ -490,8 +516,9 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
             bwd_finish(a, idx, st);
         }
         __syncthreads();
-        lds_rows_out(a.dL_ddc + (size_t)base * 3, 3, n, s_sh, SH_STRIDE, 0, 48);
-        if (a.dL_dsh && wr > 0) lds_rows_out(a.dL_dsh + (size_t)base * wr, wr, n, s_sh, SH_STRIDE, 3, 48);
+        lds_rows_out(a.dL_ddc + (size_t)base * 3, 3, n, s_sh, SH_STRIDE, 0, 48, a.acc & ACC_DC);
+        if (a.dL_dsh && wr > 0)
+            lds_rows_out(a.dL_dsh + (size_t)base * wr, wr, n, s_sh, SH_STRIDE, 3, 48, a.acc & ACC_SH);
         return;
     }
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
@@ -510,10 +537,11 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     }
     __syncthreads();
     float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48);
+    const bool acc = a.acc & ACC_SH;
     for (int f = threadIdx.x; f < n * 12; f += 256) {
         const int g = f / 12, j = f - g * 12;
         const float* q = &s_sh[g * SH_STRIDE + 4 * j];
-        dst[f] = make_float4(q[0], q[1], q[2], q[3]);
+        dst[f] = acc4(dst + f, make_float4(q[0], q[1], q[2], q[3]), acc);
     }
 }
 

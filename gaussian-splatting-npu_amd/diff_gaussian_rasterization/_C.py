@@ -47,6 +47,7 @@ def _load():
     lib.gsr_backward_dc.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp,
                                     _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _b, _b, _vp]
+    lib.gsr_backward_dc_acc.argtypes = lib.gsr_backward_dc.argtypes[:-1] + [ctypes.c_uint, _vp]
     lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
     lib.gsr_adam_update_multi.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
@@ -184,14 +185,23 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return L, out_color, radii, geom, binning, img, out_invdepth
 
 
+# accumulate= keys -> gsr.h GSR_ACC_* bits
+ACC_BITS = {"means3D": 1, "dc": 2, "sh": 4, "opacities": 8, "scales": 16, "rotations": 32, "cov3D_precomp": 64,
+            "colors_precomp": 128}
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                  dL_dout_invdepth, sh, degree, campos, geomBuffer, R, binningBuffer, imageBuffer,
-                                 antialiasing, debug, dc=None):
+                                 antialiasing, debug, dc=None, accumulate=None):
     """RasterizeGaussiansBackwardNPU (rasterize_points.cu:126-223).  With `dc` (the separate-DC
     form) the result carries dL_ddc (P,1,3) before dL_dsh, as the accelerated upstream op returns
     it: (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
-    dL_drotations)."""
+    dL_drotations).
+
+    accumulate: optional {ACC_BITS key: tensor} -- the kernel ADDS that input's gradient into the
+    given contiguous float32 tensor of the input's size (gsr_backward_dc_acc) and the result holds
+    None in its place."""
     _require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
@@ -199,32 +209,50 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
     M, has_dc = _sh_split(sh, dc)
     # Render-pass gradients (one allocation): mean2D 3 | colors 3 | conic 4 | invdepth 1.
     # The HIP backward writes every element (no atomics, no pre-zeroing needed).
-    acc = torch.empty((P * 11,), dtype=torch.float32, device=dev)
-    dL_dmeans2D = acc[0:3 * P].view(P, 3)
-    dL_dcolors = acc[3 * P:6 * P].view(P, 3)
-    dL_dconic = acc[6 * P:10 * P].view(P, 2, 2)
+    rbuf = torch.empty((P * 11,), dtype=torch.float32, device=dev)
+    dL_dmeans2D = rbuf[0:3 * P].view(P, 3)
+    dL_dcolors = rbuf[3 * P:6 * P].view(P, 3)
+    dL_dconic = rbuf[6 * P:10 * P].view(P, 2, 2)
     has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0
-    dL_dinvdepths = acc[10 * P:11 * P].view(P, 1)
+    dL_dinvdepths = rbuf[10 * P:11 * P].view(P, 1)
     # Parameter gradients, fully written by the HIP kernel (zeros for culled Gaussians), in ONE
     # buffer laid out as multiview.PARAM_ORDER (means3D | sh | opacity | scales | rotations) then
     # cov3D: autograd keeps these views as the leaves' .grad, so a multi-GPU step all-reduces the
     # buffer in place instead of gathering and scattering 236 B per Gaussian around the collective.
     # With dc, its gradient sits between means3D and the rest (multiview.PARAM_ORDER_DC).
-    sizes = [3 * P, 3 * P if has_dc else 0, 3 * M * P, P, 3 * P, 4 * P, 6 * P]
+    acc = dict(accumulate or {})
+    for k, t in acc.items():
+        n = {"means3D": 3 * P, "dc": 3 * P, "sh": 3 * M * P, "opacities": P, "scales": 3 * P, "rotations": 4 * P,
+             "cov3D_precomp": 6 * P, "colors_precomp": 3 * P}.get(k)
+        if n is None:
+            raise RuntimeError(f"accumulate: unknown gradient {k!r}")
+        if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n:
+            raise RuntimeError(f"accumulate[{k!r}] must be a contiguous float32 tensor of {n} elements on {dev}")
+    if "dc" in acc and not has_dc:
+        raise RuntimeError("accumulate['dc'] given without dc")
+    sizes = [0 if "means3D" in acc else 3 * P, 3 * P if has_dc and "dc" not in acc else 0,
+             0 if "sh" in acc else 3 * M * P, 0 if "opacities" in acc else P, 0 if "scales" in acc else 3 * P,
+             0 if "rotations" in acc else 4 * P, 0 if "cov3D_precomp" in acc else 6 * P]
     parts = torch.split(torch.empty((sum(sizes),), dtype=torch.float32, device=dev), sizes)
-    dL_dmeans3D = parts[0].view(P, 3)
-    dL_ddc = parts[1].view(P, 1, 3) if has_dc else None
-    dL_dsh = parts[2].view(P, M, 3)
-    dL_dopacity = parts[3].view(P, 1)
-    dL_dscales = parts[4].view(P, 3)
-    dL_drotations = parts[5].view(P, 4)
-    dL_dcov3D = parts[6].view(P, 6)
+    dL_dmeans3D = acc.get("means3D", parts[0]).view(P, 3)
+    dL_ddc = acc.get("dc", parts[1]).view(P, 1, 3) if has_dc else None
+    dL_dsh = acc.get("sh", parts[2]).view(P, M, 3)
+    dL_dopacity = acc.get("opacities", parts[3]).view(P, 1)
+    dL_dscales = acc.get("scales", parts[4]).view(P, 3)
+    dL_drotations = acc.get("rotations", parts[5]).view(P, 4)
+    dL_dcov3D = acc.get("cov3D_precomp", parts[6]).view(P, 6)
+    if "colors_precomp" in acc:
+        dL_dcolors = acc["colors_precomp"].view(P, 3)
 
     def result():
+        r = {"means3D": dL_dmeans3D, "dc": dL_ddc, "sh": dL_dsh, "opacities": dL_dopacity, "scales": dL_dscales,
+             "rotations": dL_drotations, "cov3D_precomp": dL_dcov3D, "colors_precomp": dL_dcolors}
+        r = {k: (None if k in acc else v) for k, v in r.items()}
         if has_dc:
-            return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscales,
-                    dL_drotations)
-        return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+            return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["dc"],
+                    r["sh"], r["scales"], r["rotations"])
+        return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["sh"],
+                r["scales"], r["rotations"])
 
     if P == 0:
         return result()
@@ -238,7 +266,10 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
 
     dpix = p(dL_dout_color, "dL_dout_color")
     dinv = p(dL_dout_invdepth, "dL_dout_invdepth") if has_inv else None
-    _check(lib.gsr_backward_dc(
+    mask = 0
+    for k in acc:
+        mask |= ACC_BITS[k]
+    _check(lib.gsr_backward_dc_acc(
         P, int(degree), M, int(R), p(background, "bg"), W, H, p(means3D, "means3D"),
         p(dc, "dc") if has_dc else None, p(sh, "sh"),
         p(colors, "colors_precomp"), p(opacities, "opacities"), p(scales, "scales"), float(scale_modifier),
@@ -248,7 +279,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
         dpix, dinv, dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(), dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
         dL_dinvdepths.data_ptr() if has_inv else None, dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
         dL_ddc.data_ptr() if has_dc else None, dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(),
-        dL_drotations.data_ptr(), bool(antialiasing), bool(debug), _stream(dev)))
+        dL_drotations.data_ptr(), bool(antialiasing), bool(debug), mask, _stream(dev)))
     return result()
 
 

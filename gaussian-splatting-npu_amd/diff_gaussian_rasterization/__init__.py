@@ -11,6 +11,8 @@ takes ``dc=`` (SH coefficient 0 apart from the rest, gaussian_renderer/__init__.
 (scene/gaussian_model.py:194-196).  All compute is the HIP library behind ``_C`` (gfx950); there is
 no CPU path.
 """
+import contextlib
+import threading
 from typing import NamedTuple
 
 import torch
@@ -18,7 +20,41 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam",
+           "accumulate_grads_in_place"]
+
+_state = threading.local()
+
+
+@contextlib.contextmanager
+def accumulate_grads_in_place(enabled=True):
+    """Forwards run inside this context hand their backward an in-place accumulation: a
+    rasterizer input that is a leaf tensor with an existing float32 ``.grad`` of its own shape
+    gets this view's gradient ADDED to that ``.grad`` by the HIP backward kernel itself
+    (gsr_backward_dc_acc: one fp32 add per element, the arithmetic of autograd's AccumulateGrad
+    ``grad += new``), and the autograd function returns None for it -- instead of a fresh
+    gradient tensor that autograd then adds with a separate pass over it.  A multi-view step
+    (several views into one set of parameter gradients) saves that pass per view.
+    Inputs without a ``.grad`` yet (a step's first view), non-leaf inputs (activations) and
+    leaves with gradient hooks take the ordinary path.  Off by default: outside the context every
+    call is exactly the reference's."""
+    prev = getattr(_state, "accumulate", False)
+    _state.accumulate = bool(enabled)
+    try:
+        yield
+    finally:
+        _state.accumulate = prev
+
+
+def _accumulation_target(t):
+    """t's existing .grad, if the backward may add into it in place."""
+    if t is None or t.numel() == 0 or not t.requires_grad or not t.is_leaf or t._backward_hooks \
+            or getattr(t, "_post_accumulate_grad_hooks", None):
+        return None
+    g = t.grad
+    if g is None or g.dtype != torch.float32 or g.device != t.device or g.shape != t.shape or not g.is_contiguous():
+        return None
+    return g
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -59,6 +95,13 @@ class _RasterizeGaussians(torch.autograd.Function):
             s.campos, s.prefiltered, s.antialiasing, s.debug, dc=dc)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        # in-place accumulation (accumulate_grads_in_place): the inputs whose .grad the backward
+        # may add into, kept by reference (leaves: the same tensors save_for_backward keeps)
+        ctx.acc_inputs = None
+        if getattr(_state, "accumulate", False):
+            ctx.acc_inputs = {"means3D": means3D, "dc": dc, "sh": sh, "opacities": opacities, "scales": scales,
+                              "rotations": rotations, "cov3D_precomp": cov3Ds_precomp,
+                              "colors_precomp": colors_precomp}
         # outputs without a gradient (always radii; invdepth when the loss ignores it) arrive as None
         # instead of zero tensors that autograd would fill with a kernel of its own; backward treats
         # None as zero
@@ -77,10 +120,17 @@ class _RasterizeGaussians(torch.autograd.Function):
                                          device=means3D.device)
         if grad_out_depth is None:
             grad_out_depth = torch.Tensor([])  # no invdepth term (rasterize_points.cu:174-182 with zeros)
+        accumulate = None
+        if ctx.acc_inputs is not None:
+            accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in ctx.acc_inputs.items())
+                          if g is not None}
+            if "dc" in accumulate and (dc is None or dc.numel() == 0):
+                del accumulate["dc"]
         grads = _C.rasterize_gaussians_backward(
             s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth, sh, s.sh_degree,
-            s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug, dc=dc)
+            s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug, dc=dc,
+            accumulate=accumulate)
         if len(grads) == 9:
             (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
              grad_scales, grad_rotations) = grads

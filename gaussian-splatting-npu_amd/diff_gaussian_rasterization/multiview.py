@@ -217,7 +217,10 @@ class DataParallelTrainer:
         from fused_ssim import fused_ssim
         losses = []
         for settings, gt in views:
-            img, means2D, radii = self.render(settings)
+            # xyz, f_dc, f_rest enter the rasterizer as leaves whose .grad are views of the flat
+            # buffer: the backward kernel adds into them directly (no separate accumulation pass)
+            with self._dgr.accumulate_grads_in_place():
+                img, means2D, radii = self.render(settings)
             l1 = (img - gt).abs().mean()
             loss = (1.0 - self.lambda_dssim) * l1 + self.lambda_dssim * (1.0 - fused_ssim(img[None], gt[None]))
             loss.backward()

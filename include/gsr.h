@@ -224,6 +224,29 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
                     float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
                     bool antialiasing, bool debug, gsr_stream_t stream);
 
+/* gsr_backward_dc with in-place gradient accumulation: for every GSR_ACC_* bit set
+ * in `accumulate`, the matching parameter-gradient array is ADDED to (out += this
+ * call's gradient, one fp32 add per element, as autograd's AccumulateGrad does
+ * `grad += new`) instead of overwritten.  A multi-view step (several views'
+ * backward passes into one gradient buffer) then costs no separate
+ * accumulation pass over the 236 B/Gaussian of gradients.  The render-pass outputs
+ * (dL_dmean2D, dL_dconic, dL_dinvdepth) are always written. */
+enum {
+    GSR_ACC_MEANS3D = 1, GSR_ACC_DC = 2, GSR_ACC_SH = 4, GSR_ACC_OPACITY = 8, GSR_ACC_SCALES = 16,
+    GSR_ACC_ROTATIONS = 32, GSR_ACC_COV3D = 64, GSR_ACC_COLORS = 128, GSR_ACC_ALL = 255
+};
+int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int width, int height,
+                        const float* means3D, const float* dc, const float* shs,
+                        const float* colors_precomp, const float* opacities, const float* scales,
+                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                        const float* viewmatrix, const float* projmatrix, const float* campos,
+                        float tan_fovx, float tan_fovy, const int* radii, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix,
+                        const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic,
+                        float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth, float* dL_dmean3D,
+                        float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                        bool antialiasing, bool debug, unsigned accumulate, gsr_stream_t stream);
+
 /* Visibility-masked Adam step (the accelerated upstream's `_C.adamUpdate`, called
  * by SparseGaussianAdam.step(visibility, N) from train.py:180-183): for each of the
  * N Gaussians with visible[i] set, its M consecutive elements of param are updated
