@@ -299,14 +299,34 @@ __device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, in
     }
 }
 
-// acc: add to the destination (in-place gradient accumulation) instead of overwriting it
-__device__ __forceinline__ float4 acc4(float4* d, float4 v, bool acc)
+// Stores d4[f] = val(f) for f in [0, nv4) over the block's threads; with acc, d4[f] += val(f)
+// (in-place gradient accumulation).  Accumulating, each thread first issues the loads of up to
+// ACC_BATCH of its old values at once and only then adds and stores, so a block pays one memory
+// latency per ACC_BATCH elements instead of one per element.
+constexpr int ACC_BATCH = 6;
+template <typename F>
+__device__ __forceinline__ void store_f4(float4* d4, int nv4, bool acc, F val)
 {
-    if (acc) {
-        const float4 o = *d;
-        v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    if (!acc) {
+        for (int f = threadIdx.x; f < nv4; f += blockDim.x) d4[f] = val(f);
+        return;
     }
-    return v;
+    for (int f0 = 0; f0 < nv4; f0 += ACC_BATCH * (int)blockDim.x) {
+        float4 old[ACC_BATCH];
+#pragma unroll
+        for (int i = 0; i < ACC_BATCH; i++) {
+            const int f = f0 + i * (int)blockDim.x + (int)threadIdx.x;
+            if (f < nv4) old[i] = d4[f];
+        }
+#pragma unroll
+        for (int i = 0; i < ACC_BATCH; i++) {
+            const int f = f0 + i * (int)blockDim.x + (int)threadIdx.x;
+            if (f < nv4) {
+                const float4 v = val(f);
+                d4[f] = make_float4(old[i].x + v.x, old[i].y + v.y, old[i].z + v.z, old[i].w + v.w);
+            }
+        }
+    }
 }
 
 __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const float* lds, int stride, int col0,
@@ -316,8 +336,7 @@ __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const flo
     int e0 = 0;
     if (((uintptr_t)dst & 15) == 0) {
         const int nv4 = total >> 2;
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        for (int f = threadIdx.x; f < nv4; f += blockDim.x) {
+        store_f4(reinterpret_cast<float4*>(dst), nv4, acc, [&](int f) {
             float vv[4];
             int g = (4 * f) / w, j = 4 * f - g * w;
 #pragma unroll
@@ -325,8 +344,8 @@ __device__ __forceinline__ void lds_rows_out(float* dst, int w, int n, const flo
                 vv[q] = col0 + j < ncols ? lds[g * stride + col0 + j] : 0.f;
                 if (++j == w) { j = 0; g++; }
             }
-            d4[f] = acc4(d4 + f, make_float4(vv[0], vv[1], vv[2], vv[3]), acc);
-        }
+            return make_float4(vv[0], vv[1], vv[2], vv[3]);
+        });
         e0 = nv4 << 2;
     }
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) {
@@ -357,9 +376,8 @@ __device__ __forceinline__ void lds_copy_out(float* dst, const float* lds, int t
     int e0 = 0;
     if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)lds & 15) == 0) {
         const int nv4 = total >> 2;
-        float4* d4 = reinterpret_cast<float4*>(dst);
-        for (int f = threadIdx.x; f < nv4; f += blockDim.x)
-            d4[f] = acc4(d4 + f, reinterpret_cast<const float4*>(lds)[f], acc);
+        store_f4(reinterpret_cast<float4*>(dst), nv4, acc,
+                 [&](int f) { return reinterpret_cast<const float4*>(lds)[f]; });
         e0 = nv4 << 2;
     }
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) dst[e] = acc ? dst[e] + lds[e] : lds[e];

@@ -15,6 +15,8 @@ __device__ __forceinline__ float sq(float x) { return x * x; }
 
 // One output element: written, or added to when the caller accumulates into it (AccBits).
 __device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p + v : v; }
+// the same with the old value already loaded (bwd_gather prefetches them)
+__device__ __forceinline__ void put(float* p, float v, bool acc, float old) { *p = acc ? old + v : v; }
 
 // Per-Gaussian inputs, loaded before the workgroup's SH staging so that their memory round trips
 // overlap it (and each other): every load is issued unconditionally (clamped indices, values
@@ -29,6 +31,8 @@ struct BwdIn {
     f3 scale;
     float opacity;
     uint8_t clamped;
+    // accumulating (AccBits): the outputs' current values, loaded here with everything else
+    float old_mean[3], old_opacity, old_scale[3], old_rot[4];
 };
 
 constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +3 us, 2: +10 us)
@@ -49,6 +53,19 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
         const float* rp = a.rotations + 4 * i;
         in.rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
         in.scale = {a.scales[3 * i], a.scales[3 * i + 1], a.scales[3 * i + 2]};
+    }
+    if (a.acc & ACC_MEANS3D) {
+        in.old_mean[0] = a.dL_dmean3D[3 * i]; in.old_mean[1] = a.dL_dmean3D[3 * i + 1];
+        in.old_mean[2] = a.dL_dmean3D[3 * i + 2];
+    }
+    if (a.acc & ACC_OPACITY) in.old_opacity = a.dL_dopacity[i];
+    if (a.acc & ACC_SCALES) {
+        in.old_scale[0] = a.dL_dscale[3 * i]; in.old_scale[1] = a.dL_dscale[3 * i + 1];
+        in.old_scale[2] = a.dL_dscale[3 * i + 2];
+    }
+    if (a.acc & ACC_ROTATIONS) {  // the destination is the caller's .grad: no alignment assumed
+        const float* r = a.dL_drot + 4 * i;
+        in.old_rot[0] = r[0]; in.old_rot[1] = r[1]; in.old_rot[2] = r[2]; in.old_rot[3] = r[3];
     }
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) in.g[q] = 0.f;
@@ -104,6 +121,7 @@ struct BwdState {
     float dRGB[3];        // dL/dcolor, zeroed for clamped channels (backward.cu:41-44)
     float dmx, dmy, dmz;  // dL/dmean3D without the view-direction term
     float ddir[3];        // dL/d(normalised direction), summed over the SH coefficients
+    float old_mean[3];    // accumulating: dL/dmean3D's current value
 };
 
 // Coefficient k's factor dRGB/dsh_k (backward.cu:51-100, same expressions: dL/dsh is
@@ -187,9 +205,9 @@ __device__ __forceinline__ void bwd_finish(const PreprocessBwdArgs& a, int idx, 
         dmz += dn.z;
     }
     const bool acc = a.acc & ACC_MEANS3D;
-    put(dmean, dmx, acc);
-    put(dmean + 1, dmy, acc);
-    put(dmean + 2, dmz, acc);
+    put(dmean, dmx, acc, st.old_mean[0]);
+    put(dmean + 1, dmy, acc, st.old_mean[1]);
+    put(dmean + 2, dmz, acc, st.old_mean[2]);
 }
 
 // Everything of one Gaussian except the SH coefficients: the reduced render gradients,
@@ -202,6 +220,7 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
     st.ncoef = 0;
     st.dmx = st.dmy = st.dmz = 0.f;
     st.ddir[0] = st.ddir[1] = st.ddir[2] = 0.f;
+    st.old_mean[0] = in.old_mean[0]; st.old_mean[1] = in.old_mean[1]; st.old_mean[2] = in.old_mean[2];
     float* dcov_out = a.dL_dcov3D + 6 * i;
 
     if (!in.visible) {
@@ -294,13 +313,13 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
         const float dL_dopacity_v = g[GF_OPACITY];
         const float d_h_convolution_scaling = dL_dopacity_v * in.opacity;
-        put(a.dL_dopacity + idx, dL_dopacity_v * h_convolution_scaling, a.acc & ACC_OPACITY);
+        put(a.dL_dopacity + idx, dL_dopacity_v * h_convolution_scaling, a.acc & ACC_OPACITY, in.old_opacity);
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
                                                                     : d_h_convolution_scaling / (2 * h_convolution_scaling);
     } else {
         c_xx += h_var;
         c_yy += h_var;
-        put(a.dL_dopacity + idx, g[GF_OPACITY], a.acc & ACC_OPACITY);
+        put(a.dL_dopacity + idx, g[GF_OPACITY], a.acc & ACC_OPACITY, in.old_opacity);
     }
     float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
     if (a.antialiasing) {
@@ -424,9 +443,9 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         mat3 G = mat3_T(dL_dM);
         float* ds = a.dL_dscale + 3 * i;
         const bool acc_s = a.acc & ACC_SCALES;
-        put(ds, Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2], acc_s);
-        put(ds + 1, Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2], acc_s);
-        put(ds + 2, Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2], acc_s);
+        put(ds, Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2], acc_s, in.old_scale[0]);
+        put(ds + 1, Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2], acc_s, in.old_scale[1]);
+        put(ds + 2, Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2], acc_s, in.old_scale[2]);
 #pragma unroll
         for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
         const float(*gm)[3] = G.m;
@@ -440,7 +459,8 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
                4 * z * (gm[1][1] + gm[0][0]);
         float* dr = a.dL_drot + 4 * i;
         const bool acc_r = a.acc & ACC_ROTATIONS;
-        put(dr, dq.x, acc_r); put(dr + 1, dq.y, acc_r); put(dr + 2, dq.z, acc_r); put(dr + 3, dq.w, acc_r);
+        put(dr, dq.x, acc_r, in.old_rot[0]); put(dr + 1, dq.y, acc_r, in.old_rot[1]);
+        put(dr + 2, dq.z, acc_r, in.old_rot[2]); put(dr + 3, dq.w, acc_r, in.old_rot[3]);
     } else {
         if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
             a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
@@ -536,13 +556,11 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         bwd_finish(a, idx, st);
     }
     __syncthreads();
-    float4* dst = reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48);
-    const bool acc = a.acc & ACC_SH;
-    for (int f = threadIdx.x; f < n * 12; f += 256) {
+    store_f4(reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48), n * 12, a.acc & ACC_SH, [&](int f) {
         const int g = f / 12, j = f - g * 12;
         const float* q = &s_sh[g * SH_STRIDE + 4 * j];
-        dst[f] = acc4(dst + f, make_float4(q[0], q[1], q[2], q[3]), acc);
-    }
+        return make_float4(q[0], q[1], q[2], q[3]);
+    });
 }
 
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)

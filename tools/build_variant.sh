@@ -1,0 +1,20 @@
+#!/bin/bash
+# Build libgsr_hip.so with extra compiler flags into ab/<name>.so (for tools/ab.sh A/B runs).
+# Usage: tools/build_variant.sh <name> "<extra hipcc flags>"
+set -eu
+cd "$(dirname "$0")/.."
+NAME=$1
+EXTRA=${2:-}
+B=/tmp/gsr_variant_$NAME
+rm -rf "$B"; mkdir -p "$B" ab
+cd gaussian-splatting-npu_amd
+for f in csrc/*.hip; do
+  o=$B/$(basename "$f" .hip).o
+  fl=""
+  [ "$(basename "$f")" = render.hip ] && fl="-fno-slp-vectorize"
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -Wall -Wno-unused-function \
+      -I../include -Icsrc $fl $EXTRA -c "$f" -o "$o" &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../ab/$NAME.so $B/*.o
+echo "built ab/$NAME.so"
