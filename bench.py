@@ -65,6 +65,12 @@ def parse():
     ap.add_argument("--no-aux", action="store_true", help="skip the §8f side measurements (distCUDA2)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc passes (traffic then from the stamped profiles/ file)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="render the views of a step one after the other on one stream")
+    ap.add_argument("--no-prefix-stream", action="store_true",
+                    help="run the forward's binning prefix on the caller's stream, not the library's priority stream")
+    ap.add_argument("--batch-views", action="store_true",
+                    help="render this rank's views as one MultiViewRasterizer batch (one backward preprocess pass)")
     ap.add_argument("--no-fused-accumulation", action="store_true",
                     help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
@@ -163,6 +169,7 @@ def main():
     lib = dgr._C.lib
     lib.gsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     lib.gsr_profile_kernel_name.restype = ctypes.c_char_p
+    lib.gsr_set_prefix_stream(0 if args.no_prefix_stream else 1)
 
     H, W, P = args.height, args.width, args.P
     scene = synthetic.make_scene(P, seed=0)
@@ -191,19 +198,55 @@ def main():
 
     ar_events = []  # (start, end) around the all-reduce, recorded only in the instrumented pass below
 
-    def step(record_allreduce=False):
+    # Views alternate between two HIP streams: the forward of view v+1 (preprocess, the
+    # latency-bound sorts and scans, render) runs while the backward of view v occupies the GPU.
+    # The backward passes add into the same .grad buffers in view order (dgr.accumulate_grads_in_place
+    # orders them with an event), the forward of every view reads only the parameters.
+    main_stream = torch.cuda.current_stream(dev)
+    streams = [main_stream] + ([torch.cuda.Stream(dev)] if (args.overlap and len(cams) > 1) else [])
+
+    # the screen-space gradient receptacles (gaussian_renderer's screenspace_points), one per view
+    means2Ds = [torch.zeros_like(params["means3D"], requires_grad=True) for _ in cams]
+
+    # --batch-views: this rank's views as ONE MultiViewRasterizer node (each view's forward, then
+    # every view's render backward and one preprocess backward over the Gaussians for the batch)
+    mv = dgr.MultiViewRasterizer(cams) if args.batch_views else None
+    means2D_batch = torch.zeros((len(cams), P, 3), device=dev, requires_grad=True) if mv else None
+    gc_batch = torch.stack([g[0] for g in grads]) if mv else None
+    gi_batch = torch.stack([g[1] for g in grads]) if mv else None
+
+    def step(record_allreduce=False, overlap=True):
         for p in params.values():
             p.grad = None
-        for s, (gc, gi) in zip(cams, grads):
-            rast = dgr.GaussianRasterizer(raster_settings=s)
-            means2D = torch.zeros_like(params["means3D"], requires_grad=True)
-            # views after the first add their gradients into the parameters' .grad inside the
-            # backward kernel (dgr.accumulate_grads_in_place) instead of autograd's separate add
-            with dgr.accumulate_grads_in_place(not args.no_fused_accumulation):
-                color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
-                                         opacities=params["opacities"], scales=params["scales"],
-                                         rotations=params["rotations"])
-            torch.autograd.backward([color, inv], [gc, gi])
+        for m in means2Ds:
+            m.grad = None
+        if mv is not None:
+            means2D_batch.grad = None
+            color, radii, inv = mv(means3D=params["means3D"], means2D=means2D_batch, shs=params["shs"],
+                                   opacities=params["opacities"], scales=params["scales"],
+                                   rotations=params["rotations"])
+            torch.autograd.backward([color, inv], [gc_batch, gi_batch])
+            nbytes = multiview.allreduce_grads(params)
+            if record_allreduce:
+                raise RuntimeError("--batch-views: all-reduce events not recorded")
+            return
+        n_st = len(streams) if overlap else 1
+        for st in streams[1:n_st]:
+            st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
+        for i, (s, (gc, gi)) in enumerate(zip(cams, grads)):
+            st = streams[i % n_st]
+            with torch.cuda.stream(st):
+                rast = dgr.GaussianRasterizer(raster_settings=s)
+                means2D = means2Ds[i]
+                # views after the first add their gradients into the parameters' .grad inside the
+                # backward kernel (dgr.accumulate_grads_in_place) instead of autograd's separate add
+                with dgr.accumulate_grads_in_place(not args.no_fused_accumulation):
+                    color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
+                                             opacities=params["opacities"], scales=params["scales"],
+                                             rotations=params["rotations"])
+                torch.autograd.backward([color, inv], [gc, gi])
+        for st in streams[1:n_st]:
+            main_stream.wait_stream(st)
         if record_allreduce:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -236,9 +279,10 @@ def main():
     # recorded around every launch cost ~3% of the step, so they stay out of the timed region)
     kern = {}
     if not args.no_profile:
+        # one stream: every kernel's duration is its own, not shared with an overlapping view's
         lib.gsr_profile_enable(1)
         for _ in range(args.steps):
-            step()
+            step(overlap=False)
         torch.cuda.synchronize()
         nk = 16
         tot = (ctypes.c_double * nk)()

@@ -70,6 +70,59 @@ int pinned(uint32_t** out)
 }
 
 // ---------------------------------------------------------------------------
+// The forward's binning prefix (preprocess, depth sort, scan, emission, tile sort, tile ranges,
+// tile order: small, latency-bound launches) runs on an internal stream of the highest priority,
+// forked from the caller's stream and joined back into it before render_fwd.  When the caller
+// overlaps views on several streams (the forward of view v+1 beside the backward of view v,
+// bench.py), the dispatcher then places the prefix's workgroups ahead of the queued workgroups of
+// the other view's long kernels instead of behind them.  Buffers stay stream-ordered for the caller:
+// everything the prefix writes is joined into its stream before the entry point returns.
+// ---------------------------------------------------------------------------
+struct PrefixStream {
+    hipStream_t s = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+constexpr int MAX_DEVICES = 64;
+thread_local PrefixStream g_prefix[MAX_DEVICES];
+thread_local bool g_prefix_off = false;  // gsr_set_prefix_stream(0): everything on the caller's stream
+
+int prefix_begin(hipStream_t caller, hipStream_t* out)
+{
+    *out = caller;
+    if (g_prefix_off) return GSR_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail_hip(e, __LINE__);
+    if (dev < 0 || dev >= MAX_DEVICES) return GSR_OK;
+    PrefixStream& ps = g_prefix[dev];
+    if (!ps.s) {
+        int least = 0, greatest = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipStreamCreateWithPriority(&ps.s, hipStreamNonBlocking, greatest)) != hipSuccess)
+            return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.fork, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.join, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
+    }
+    if ((e = hipEventRecord(ps.fork, caller)) != hipSuccess) return fail_hip(e, __LINE__);
+    if ((e = hipStreamWaitEvent(ps.s, ps.fork, 0)) != hipSuccess) return fail_hip(e, __LINE__);
+    *out = ps.s;
+    return GSR_OK;
+}
+
+// the caller's stream waits for everything enqueued on the prefix stream so far
+int prefix_end(hipStream_t caller, hipStream_t prefix)
+{
+    if (prefix == caller) return GSR_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail_hip(e, __LINE__);
+    PrefixStream& ps = g_prefix[dev];
+    if ((e = hipEventRecord(ps.join, prefix)) != hipSuccess) return fail_hip(e, __LINE__);
+    if ((e = hipStreamWaitEvent(caller, ps.join, 0)) != hipSuccess) return fail_hip(e, __LINE__);
+    return GSR_OK;
+}
+
+// ---------------------------------------------------------------------------
 // Optional per-kernel timing with HIP events recorded on the launch stream
 // (bench.py's roofline leg).  Off by default; costs two event records per
 // launch when on.
@@ -127,6 +180,12 @@ extern "C" {
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
 const char* gsr_version(void) { return "gsr-hip 0.1 gfx950"; }
+
+int gsr_set_prefix_stream(int on)
+{
+    g_prefix_off = on == 0;
+    return GSR_OK;
+}
 
 int gsr_profile_enable(int on)
 {
@@ -324,17 +383,22 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
     *num_rendered = 0;
     if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
     uint32_t* h = nullptr;
-    int rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
-                                     colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
-                                     viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                     radii, debug, stream, &h);
+    hipStream_t ps = nullptr;
+    int rc = prefix_begin((hipStream_t)stream, &ps);
     if (rc) return rc;
-    return forward_geometry_wait(h, stream, num_rendered);
+    rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                 colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                 viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                 radii, debug, ps, &h);
+    if (rc) return rc;
+    rc = forward_geometry_wait(h, ps, num_rendered);
+    const int rj = prefix_end((hipStream_t)stream, ps);
+    return rc ? rc : rj;
 }
 
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, bool emitted);
+                               float* depth, bool debug, gsr_stream_t stream, bool emitted, hipStream_t prefix);
 
 int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P, int num_rendered,
                        const float* background, int width, int height, const float* colors_precomp,
@@ -342,18 +406,24 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
 {
     (void)radii;
     (void)colors_precomp;
+    hipStream_t ps = nullptr;
+    const int rc = prefix_begin((hipStream_t)stream, &ps);
+    if (rc) return rc;
     return forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, num_rendered, background, width,
-                               height, out_color, depth, debug, stream, false);
+                               height, out_color, depth, debug, stream, false, ps);
 }
 
 // Forward, second half.  `emitted`: the early emission (gsr_forward_prealloc_dc) already wrote the
 // instances into this binning buffer.
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, bool emitted)
+                               float* depth, bool debug, gsr_stream_t stream, bool emitted, hipStream_t prefix)
 {
-    hipStream_t s = (hipStream_t)stream;  // colors_precomp was folded into the render record by preprocess
-    if (P <= 0) return GSR_OK;
+    // binning on the prefix stream, render_fwd on the caller's (colors_precomp was folded into the
+    // render record by preprocess)
+    hipStream_t s = prefix;
+    hipStream_t caller = (hipStream_t)stream;
+    if (P <= 0) return prefix_end(caller, prefix);
     const int L = num_rendered;
     const GeomLayout g = geom_layout(P);
     const ImageLayout im = image_layout(width, height);
@@ -410,6 +480,11 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
         ProfScope ps_(PK_TILE_ORDER, s);
         HIP_TRY(launch_tile_order(ranges, nullptr, T, tile_order, s));
     }
+    {
+        const int rc = prefix_end(caller, prefix);
+        if (rc) return rc;
+    }
+    s = caller;
     RenderFwdArgs r;
     r.ranges = ranges;
     r.tile_order = tile_order;
@@ -472,17 +547,20 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     *num_rendered = 0;
     if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
     uint32_t* h = nullptr;
-    int rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
-                                     colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
-                                     viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                     radii, debug, stream, &h);
+    hipStream_t ps = nullptr;
+    int rc = prefix_begin((hipStream_t)stream, &ps);
+    if (rc) return rc;
+    rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                 colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                 viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                 radii, debug, ps, &h);
     if (rc) return rc;
     // Emission does not need num_rendered on the host: enqueue it now, so the GPU works through
     // the read-back below instead of idling until the host launches it (it resolves its output
     // arrays from the device-side total and writes nothing if the buffer is too small).
     const bool early = binning_buffer != nullptr && binning_capacity > 0;
     if (early) {
-        hipStream_t s = (hipStream_t)stream;
+        hipStream_t s = ps;
         const GeomLayout g = geom_layout(P);
         const ImageLayout im = image_layout(width, height);
         const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
@@ -497,12 +575,16 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
                                             (int)(gx * gy), s));
     }
     int L = 0;
-    rc = forward_geometry_wait(h, stream, &L);
+    rc = forward_geometry_wait(h, ps, &L);
     *num_rendered = L;
-    if (rc) return rc;
-    if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity) return GSR_OK;  // caller allocates
+    if (rc) {
+        prefix_end((hipStream_t)stream, ps);
+        return rc;
+    }
+    if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity)  // caller allocates
+        return prefix_end((hipStream_t)stream, ps);
     rc = forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
-                             out_color, depth, debug, stream, early && L > 0);
+                             out_color, depth, debug, stream, early && L > 0, ps);
     if (rc) return rc;
     *rendered = 1;
     return GSR_OK;
@@ -618,6 +700,119 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
                                tan_fovx, tan_fovy, radii, geom_buffer, binning_buffer, image_buffer, dL_dpix,
                                dL_invdepths, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth, dL_dmean3D,
                                dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug, 0u, stream);
+}
+
+int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
+                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* const* viewmatrices,
+                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
+                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
+                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
+                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
+                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
+                       gsr_stream_t stream)
+{
+    if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
+    if (accumulate & ~(unsigned)GSR_ACC_ALL) return fail(GSR_ERR_INVALID, "unknown accumulate bits");
+    if (dc && !dL_ddc) return fail(GSR_ERR_INVALID, "dc given without dL_ddc");
+    if (dc && colors_precomp)
+        return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
+    if (dc && M > 0 && (!shs || !dL_dsh)) return fail(GSR_ERR_INVALID, "dc given with M > 0 but shs/dL_dsh NULL");
+    if (!R || !viewmatrices || !projmatrices || !campos || !tan_fovx || !tan_fovy || !geom_buffers ||
+        !binning_buffers || !image_buffers || !dL_dpix || !dL_dmean2D)
+        return fail(GSR_ERR_INVALID, "null per-view array");
+    const bool has_inv = dL_invdepths != nullptr;
+    hipStream_t s = (hipStream_t)stream;
+    if (P <= 0) return GSR_OK;
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const int T = (int)(gx * gy);
+
+    PreprocessBwdViewsArgs A;
+    PreprocessBwdArgs& p = A.a;
+    p.P = P; p.D = D; p.M = dc ? M + 1 : M;
+    p.means3D = means3D; p.radii = nullptr; p.shs = shs; p.dc = dc; p.dL_ddc = dc ? dL_ddc : nullptr;
+    p.clamped = nullptr;
+    p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
+    p.cov3D_precomp = cov3D_precomp;
+    p.view = nullptr; p.proj = nullptr; p.campos = nullptr;
+    p.focal_x = p.focal_y = p.tan_fovx = p.tan_fovy = 0.f;
+    p.antialiasing = antialiasing;
+    p.grad_inst = nullptr; p.valid = nullptr; p.emit_start = nullptr; p.tiles_touched = nullptr;
+    p.has_invdepth = has_inv;
+    p.conic_opacity = nullptr;
+    p.W = width; p.H = height;
+    p.dL_dmean2D = nullptr; p.dL_dconic = nullptr; p.dL_dinvdepth = nullptr;
+    p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
+    p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;
+    p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;
+    p.acc = accumulate;
+    A.V = V;
+    for (int v = 0; v < V; v++) {
+        char* gb = geom_buffers[v];
+        char* ib = image_buffers[v];
+        char* bb = binning_buffers[v];
+        const int L = R[v];
+        if (!gb || !ib || (L > 0 && !bb)) return fail(GSR_ERR_ALLOC, "null state buffer");
+        if (!dL_dpix[v] || !dL_dmean2D[v] || (has_inv && !dL_invdepths[v]))
+            return fail(GSR_ERR_INVALID, "null per-view gradient");
+        const BinLayout b = bin_layout(L);
+        // BACKWARD::render of view v (rasterizer_impl.cu:399-418): its per-(tile, Gaussian) records
+        if (L > 0) {
+            RenderBwdArgs r;
+            r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+            r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+            r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
+            r.W = width; r.H = height; r.grid_x = gx;
+            r.bg = background;
+            r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
+            r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
+            r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+            r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
+            r.dL_dpixels = dL_dpix[v];
+            r.dL_invdepths = has_inv ? dL_invdepths[v] : nullptr;
+            r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);
+            r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
+            r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
+            {
+                ProfScope ps_(PK_TILE_ORDER, s);
+                HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,
+                                          at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
+            }
+            {
+                ProfScope ps_(PK_RENDER_BWD, s);
+                HIP_TRY(launch_render_bwd(r, T, s));
+            }
+            DEBUG_SYNC(s);
+        }
+        BwdView& bv = A.v[v];
+        bv.view = viewmatrices[v];
+        bv.proj = projmatrices[v];
+        bv.campos = campos[v];
+        bv.tan_fovx = tan_fovx[v];
+        bv.tan_fovy = tan_fovy[v];
+        bv.focal_y = height / (2.0f * tan_fovy[v]);
+        bv.focal_x = width / (2.0f * tan_fovx[v]);
+        bv.radii = (radii && radii[v]) ? radii[v] : at<int>(gb, g.off[GEOM_RADII]);
+        bv.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
+        bv.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
+        bv.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+        bv.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
+        bv.grad_inst = L > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
+        bv.valid = L > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
+        bv.dL_dmean2D = dL_dmean2D[v];
+    }
+    // BACKWARD::preprocess of the whole batch: one pass over the Gaussians
+    {
+        ProfScope ps_(PK_PREPROCESS_BWD, s);
+        HIP_TRY(launch_preprocess_bwd_views(A, s));
+    }
+    DEBUG_SYNC(s);
+    return GSR_OK;
 }
 
 // ---- the non-dc entry points: the reference's Rasterizer API (rasterizer.h:31-90) ----

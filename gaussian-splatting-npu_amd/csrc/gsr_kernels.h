@@ -130,6 +130,30 @@ struct PreprocessBwdArgs {
     uint32_t acc;  // GSR_ACC_* bits (include/gsr.h): outputs added to instead of overwritten
 };
 
+// Multi-view backward (gsr_backward_views): one entry per camera view of the batch.  The
+// per-Gaussian parameters and their gradients are shared (PreprocessBwdArgs), everything
+// view-dependent comes from here; each view's screen-space gradient is written separately.
+constexpr int MAX_VIEWS = 16;
+struct BwdView {
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float focal_x, focal_y, tan_fovx, tan_fovy;
+    const int* radii;
+    const float4* conic_opacity;
+    const uint8_t* clamped;
+    const uint32_t* emit_start;
+    const uint32_t* tiles_touched;
+    const float* grad_inst;
+    const uint32_t* valid;
+    float* dL_dmean2D;  // (P,3)
+};
+struct PreprocessBwdViewsArgs {
+    PreprocessBwdArgs a;
+    int V;  // 0: the single view of `a`
+    BwdView v[MAX_VIEWS];
+};
+
 struct AdamArgs {
     float* param;
     const float* grad;
@@ -179,6 +203,7 @@ hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, u
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
+hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, hipStream_t s);
 
 // fused SSIM (ssim.hip); dA/dB/dC null: map only
 hipError_t launch_ssim_fwd(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,

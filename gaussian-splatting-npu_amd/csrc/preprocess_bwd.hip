@@ -37,18 +37,70 @@ struct BwdIn {
 
 constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +3 us, 2: +10 us)
 
-__device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in)
+// Sum of one Gaussian's per-tile gradient records of one view.  Its records are contiguous
+// (emission order); entries that contributed to no pixel were never written (their bit in the valid
+// mask is 0) and are not read (most slots: records are sparse).  The mask has one bit per slot
+// (L/8 bytes: it stays in L2), so a Gaussian's flags are one or two words; its flagged records are
+// then read REC_BATCH at a time in slot order (bitwise reproducible sums).
+__device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
+                                               const uint32_t* valid, const float* grad_inst, int idx,
+                                               float (&g)[GF_NUM])
+{
+#pragma unroll
+    for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
+    const uint32_t e0 = emit_start[idx];
+    const uint32_t e1 = e0 + tiles_touched[idx];  // 0 tiles for culled Gaussians
+    for (uint32_t w0 = e0 & ~31u; w0 < e1; w0 += 32) {
+        uint32_t bits = valid[w0 >> 5];
+        if (w0 < e0) bits &= ~0u << (e0 - w0);
+        if (e1 - w0 < 32u) bits &= (1u << (e1 - w0)) - 1u;
+        while (bits) {
+            bool v[REC_BATCH];
+            uint32_t sl[REC_BATCH];
+#pragma unroll
+            for (int k = 0; k < REC_BATCH; k++) {
+                v[k] = bits != 0u;
+                sl[k] = w0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
+                bits &= bits - 1u;
+            }
+            float4 r[REC_BATCH][3];
+#pragma unroll
+            for (int k = 0; k < REC_BATCH; k++) {
+                if (v[k]) {
+                    const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
+                    r[k][0] = rec[0];
+                    r[k][1] = rec[1];
+                    r[k][2] = rec[2];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < REC_BATCH; k++) {
+                if (v[k]) {
+                    g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
+                    g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
+                    g[8] += r[k][2].x; g[9] += r[k][2].y;
+                }
+            }
+        }
+    }
+}
+
+// The per-Gaussian parameters (and, accumulating, the outputs' old values); with `view` also the
+// launch's own view: visibility, conic, clamp flags and records.
+__device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in, bool view = true)
 {
     const size_t i = (size_t)idx;
-    in.visible = a.radii[idx] > 0;
-    in.co = a.conic_opacity[idx];
+    if (view) {
+        in.visible = a.radii[idx] > 0;
+        in.co = a.conic_opacity[idx];
+        in.clamped = a.clamped[idx];
+    }
     if (a.cov3D_precomp) {  // uniform over the launch
 #pragma unroll
         for (int k = 0; k < 6; k++) in.cov[k] = a.cov3D_precomp[6 * i + k];
     }
     in.mean = {a.means3D[3 * i], a.means3D[3 * i + 1], a.means3D[3 * i + 2]};
     in.opacity = a.opacities[idx];
-    in.clamped = a.clamped[idx];
     if (a.scales) {  // uniform over the launch
         const float* rp = a.rotations + 4 * i;
         in.rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
@@ -67,49 +119,7 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
         const float* r = a.dL_drot + 4 * i;
         in.old_rot[0] = r[0]; in.old_rot[1] = r[1]; in.old_rot[2] = r[2]; in.old_rot[3] = r[3];
     }
-#pragma unroll
-    for (int q = 0; q < GF_NUM; q++) in.g[q] = 0.f;
-    // This Gaussian's records are contiguous (emission order); entries that contributed to no
-    // pixel were never written (their bit in the valid mask is 0) and are not read (most slots:
-    // records are sparse).  The mask has one bit per slot (L/8 bytes: it stays in L2), so a
-    // Gaussian's flags are one or two words; its flagged records are then read REC_BATCH at a time
-    // in slot order (bitwise reproducible sums).
-    const uint32_t e0 = a.emit_start[idx];
-    const uint32_t e1 = e0 + a.tiles_touched[idx];  // 0 tiles for culled Gaussians
-    for (uint32_t w0 = e0 & ~31u; w0 < e1; w0 += 32) {
-        uint32_t bits = a.valid[w0 >> 5];
-        if (w0 < e0) bits &= ~0u << (e0 - w0);
-        if (e1 - w0 < 32u) bits &= (1u << (e1 - w0)) - 1u;
-        while (bits) {
-        bool v[REC_BATCH];
-        uint32_t sl[REC_BATCH];
-#pragma unroll
-        for (int k = 0; k < REC_BATCH; k++) {
-            v[k] = bits != 0u;
-            sl[k] = w0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
-            bits &= bits - 1u;
-        }
-        float4 r[REC_BATCH][3];
-#pragma unroll
-        for (int k = 0; k < REC_BATCH; k++) {
-            if (v[k]) {
-                const float4* rec = reinterpret_cast<const float4*>(a.grad_inst + (size_t)sl[k] * GRAD_REC);
-                r[k][0] = rec[0];
-                r[k][1] = rec[1];
-                r[k][2] = rec[2];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < REC_BATCH; k++) {
-            if (v[k]) {
-                float* g = in.g;
-                g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
-                g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
-                g[8] += r[k][2].x; g[9] += r[k][2].y;
-            }
-        }
-        }
-    }
+    if (view) gather_records(a.emit_start, a.tiles_touched, a.valid, a.grad_inst, idx, in.g);
 }
 
 // Per-Gaussian state carried from the non-SH part into the SH halves and the final dL/dmean3D.
@@ -210,9 +220,275 @@ __device__ __forceinline__ void bwd_finish(const PreprocessBwdArgs& a, int idx, 
     put(dmean + 2, dmz, acc, st.old_mean[2]);
 }
 
-// Everything of one Gaussian except the SH coefficients: the reduced render gradients,
+// One camera of the backward: the launch's own (single view) or an entry of the multi-view table.
+struct ViewCam {
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float focal_x, focal_y, tan_fovx, tan_fovy;
+};
+
+__device__ __forceinline__ ViewCam cam_of(const PreprocessBwdArgs& a)
+{
+    return {a.view, a.proj, a.campos, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy};
+}
+
+// One view's contribution to one visible Gaussian's gradients (no memory access).
+struct ViewGrad {
+    float g[GF_NUM];      // record sums with the per-Gaussian factors applied (dL/dmean2D, dL/dconic)
+    float dopacity;       // dL/dopacity (rescaled by the AA factor with antialiasing)
+    float dcov[6];        // dL/dcov3D
+    float dmx, dmy, dmz;  // dL/dmean3D without the view-direction (SH) term
+    f3 dir_orig;          // SH set-up: mean - campos, its normalisation and the unclamped dL/dcolor
+    float x, y, z;
+    float dRGB[3];
+};
+
+// The 3D covariance of a Gaussian: precomputed, or recomputed from scale and rotation
+// (forward.cu:114-151; bit-identical to the forward's).  Always into the local array: a pointer
+// choosing between two arrays would force both into scratch memory.
+__device__ __forceinline__ void cov3d_of(const PreprocessBwdArgs& a, const BwdIn& in, float (&cov)[6])
+{
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) cov[k] = in.cov[k];
+        return;
+    }
+    const float scl[3] = {in.scale.x, in.scale.y, in.scale.z};
+    computeCov3D(scl, a.scale_modifier, in.rot, cov);
+}
+
 // computeCov2DCUDA (backward.cu:147-326), the projection part of preprocessCUDA
-// (backward.cu:423-440), computeCov3D backward (backward.cu:330-393); sets up the SH state.
+// (backward.cu:423-440) and the set-up of computeColorFromSH's backward (backward.cu:28-49) for
+// one view: `gin` are the view's record sums, `co` its conic + rendered opacity.
+__device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const ViewCam& vc, const float (&gin)[GF_NUM],
+                                          const float4 co, uint8_t clamped, const f3 mean, float opacity,
+                                          const float (&cov3D)[6], ViewGrad& o)
+{
+    float* g = o.g;
+#pragma unroll
+    for (int q = 0; q < GF_NUM; q++) g[q] = gin[q];
+    {
+        // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
+        const float op = co.w;
+        const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
+        g[GF_MEAN2D_X] = (co.x * sx + co.y * sy) * (-op * (0.5f * a.W));
+        g[GF_MEAN2D_Y] = (co.y * sx + co.z * sy) * (-op * (0.5f * a.H));
+        g[GF_CONIC_A] *= -0.5f * op;
+        g[GF_CONIC_B] *= -0.5f * op;
+        g[GF_CONIC_C] *= -0.5f * op;
+    }
+
+    // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
+    const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
+    const float* view = vc.view;
+    f3 t = transformPoint4x3(mean, view);
+    const float limx = 1.3f * vc.tan_fovx;
+    const float limy = 1.3f * vc.tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+    const float h_x = vc.focal_x, h_y = vc.focal_y;
+    const mat3 J = mat3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z),
+                             0.0f, h_y / t.z, -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
+    const mat3 Wm = mat3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
+    const mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
+                               cov3D[5]);
+    const mat3 T = mat3_mul(Wm, J);
+    const mat3 cov2D = mat3_mul(mat3_mul(mat3_T(T), mat3_T(Vrk)), T);
+    float c_xx = cov2D.m[0][0];
+    float c_xy = cov2D.m[0][1];
+    float c_yy = cov2D.m[1][1];
+    const float h_var = 0.3f;
+    float d_inside_root = 0.f;
+    if (a.antialiasing) {
+        const float det_cov = c_xx * c_yy - c_xy * c_xy;
+        c_xx += h_var;
+        c_yy += h_var;
+        const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
+        const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
+        const float dL_dopacity_v = g[GF_OPACITY];
+        const float d_h_convolution_scaling = dL_dopacity_v * opacity;
+        o.dopacity = dL_dopacity_v * h_convolution_scaling;
+        d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
+                                                                    : d_h_convolution_scaling / (2 * h_convolution_scaling);
+    } else {
+        c_xx += h_var;
+        c_yy += h_var;
+        o.dopacity = g[GF_OPACITY];
+    }
+    float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
+    if (a.antialiasing) {
+        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
+        const float denom_f = d_inside_root / sq(w * w + w * (x + y) + x * y - z * z);
+        dL_dc_xx = w * (w * y + y * y + z * z) * denom_f;
+        dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
+        dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
+    }
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float(*Tm)[3] = T.m;
+    float* dcov = o.dcov;
+    if (denom2inv != 0) {
+        dL_dc_xx += denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
+                                 (denom - c_xx * c_yy) * dL_dconic.z);
+        dL_dc_yy += denom2inv * (-c_xx * c_xx * dL_dconic.z + 2 * c_xx * c_xy * dL_dconic.y +
+                                 (denom - c_xx * c_yy) * dL_dconic.x);
+        dL_dc_xy += denom2inv * 2 *
+                    (c_xy * c_yy * dL_dconic.x - (denom + 2 * c_xy * c_xy) * dL_dconic.y + c_xx * c_xy * dL_dconic.z);
+        dcov[0] = (Tm[0][0] * Tm[0][0] * dL_dc_xx + Tm[0][0] * Tm[1][0] * dL_dc_xy + Tm[1][0] * Tm[1][0] * dL_dc_yy);
+        dcov[3] = (Tm[0][1] * Tm[0][1] * dL_dc_xx + Tm[0][1] * Tm[1][1] * dL_dc_xy + Tm[1][1] * Tm[1][1] * dL_dc_yy);
+        dcov[5] = (Tm[0][2] * Tm[0][2] * dL_dc_xx + Tm[0][2] * Tm[1][2] * dL_dc_xy + Tm[1][2] * Tm[1][2] * dL_dc_yy);
+        dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_dc_xx + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_dc_xy +
+                  2 * Tm[1][0] * Tm[1][1] * dL_dc_yy;
+        dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_dc_xx + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_dc_xy +
+                  2 * Tm[1][0] * Tm[1][2] * dL_dc_yy;
+        dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_dc_xx + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_dc_xy +
+                  2 * Tm[1][1] * Tm[1][2] * dL_dc_yy;
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; k++) dcov[k] = 0;
+    }
+    const float(*V)[3] = Vrk.m;
+    const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
+    const float dL_dT01 = 2 * (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_xy;
+    const float dL_dT02 = 2 * (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xx +
+                          (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_xy;
+    const float dL_dT10 = 2 * (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xy;
+    const float dL_dT11 = 2 * (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xy;
+    const float dL_dT12 = 2 * (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_yy +
+                          (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xy;
+    const float(*Wq)[3] = Wm.m;
+    const float dL_dJ00 = Wq[0][0] * dL_dT00 + Wq[0][1] * dL_dT01 + Wq[0][2] * dL_dT02;
+    const float dL_dJ02 = Wq[2][0] * dL_dT00 + Wq[2][1] * dL_dT01 + Wq[2][2] * dL_dT02;
+    const float dL_dJ11 = Wq[1][0] * dL_dT10 + Wq[1][1] * dL_dT11 + Wq[1][2] * dL_dT12;
+    const float dL_dJ12 = Wq[2][0] * dL_dT10 + Wq[2][1] * dL_dT11 + Wq[2][2] * dL_dT12;
+    const float tz = 1.f / t.z;
+    const float tz2 = tz * tz;
+    const float tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                   (2 * h_y * t.y) * tz3 * dL_dJ12;
+    if (a.has_invdepth) dL_dtz -= g[GF_INVDEPTH] / (t.z * t.z);
+    const f3 dm_cov = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, view);
+    float dmx = dm_cov.x, dmy = dm_cov.y, dmz = dm_cov.z;
+
+    // ---------------- preprocessCUDA (backward.cu:423-440) ----------------
+    {
+        const float* proj = vc.proj;
+        const f3 m = mean;
+        const float4 m_hom = transformPoint4x4(m, proj);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        const float g2x = g[GF_MEAN2D_X], g2y = g[GF_MEAN2D_Y];
+        dmx += (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
+        dmy += (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
+        dmz += (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
+    }
+    o.dmx = dmx;
+    o.dmy = dmy;
+    o.dmz = dmz;
+
+    // ---------------- computeColorFromSH backward: set-up (backward.cu:28-49) ----------------
+    if (a.shs || a.dc) {
+        o.dir_orig = {mean.x - vc.campos[0], mean.y - vc.campos[1], mean.z - vc.campos[2]};
+        const f3 d = o.dir_orig;
+        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
+        o.x = d.x / len;
+        o.y = d.y / len;
+        o.z = d.z / len;
+#pragma unroll
+        for (int c = 0; c < 3; c++) o.dRGB[c] = g[GF_COLOR_R + c] * ((clamped >> c) & 1 ? 0 : 1);
+    }
+}
+
+// SH coefficients in use: (D + 1)^2, at most M and 16 (0: colors_precomp)
+__device__ __forceinline__ int sh_ncoef(const PreprocessBwdArgs& a)
+{
+    if (!a.shs && !a.dc) return 0;
+    int nc = (a.D + 1) * (a.D + 1);
+    nc = nc < a.M ? nc : a.M;
+    return nc < 16 ? nc : 16;
+}
+
+// computeCov3D backward (backward.cu:330-393): dL/dscale and dL/drot (w.r.t. the given, assumed
+// unit quaternion) from dL/dcov3D.
+__device__ __forceinline__ void cov3d_bwd(const PreprocessBwdArgs& a, const BwdIn& in, const float* d, float (&ds)[3],
+                                          float4& dq)
+{
+    const float r = in.rot.x, x = in.rot.y, y = in.rot.z, z = in.rot.w;
+    const mat3 R = mat3_cols(
+        1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+        2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+        2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+    const float mod = a.scale_modifier;
+    const f3 s = {mod * in.scale.x, mod * in.scale.y, mod * in.scale.z};
+    S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
+    const mat3 M = mat3_mul(S, R);
+    const mat3 dL_dSigma = mat3_cols(d[0], 0.5f * d[1], 0.5f * d[2], 0.5f * d[1], d[3], 0.5f * d[4],
+                                     0.5f * d[2], 0.5f * d[4], d[5]);
+    mat3 M2;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int w = 0; w < 3; w++) M2.m[c][w] = 2.0f * M.m[c][w];
+    const mat3 dL_dM = mat3_mul(M2, dL_dSigma);
+    const mat3 Rt = mat3_T(R);
+    mat3 G = mat3_T(dL_dM);
+    ds[0] = Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2];
+    ds[1] = Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2];
+    ds[2] = Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2];
+#pragma unroll
+    for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
+    const float(*gm)[3] = G.m;
+    dq.x = 2 * z * (gm[0][1] - gm[1][0]) + 2 * y * (gm[2][0] - gm[0][2]) + 2 * x * (gm[1][2] - gm[2][1]);
+    dq.y = 2 * y * (gm[1][0] + gm[0][1]) + 2 * z * (gm[2][0] + gm[0][2]) + 2 * r * (gm[1][2] - gm[2][1]) -
+           4 * x * (gm[2][2] + gm[1][1]);
+    dq.z = 2 * x * (gm[1][0] + gm[0][1]) + 2 * r * (gm[2][0] - gm[0][2]) + 2 * z * (gm[1][2] + gm[2][1]) -
+           4 * y * (gm[2][2] + gm[0][0]);
+    dq.w = 2 * r * (gm[0][1] - gm[1][0]) + 2 * x * (gm[2][0] + gm[0][2]) + 2 * y * (gm[1][2] + gm[2][1]) -
+           4 * z * (gm[1][1] + gm[0][0]);
+}
+
+// The scale / rotation outputs from dL/dcov3D (zeros without scales), written or accumulated.
+__device__ __forceinline__ void put_scale_rot(const PreprocessBwdArgs& a, int idx, const BwdIn& in, const float* dcov)
+{
+    const size_t i = (size_t)idx;
+    if (a.scales) {
+        float ds[3];
+        float4 dq;
+        cov3d_bwd(a, in, dcov, ds, dq);
+        float* dsp = a.dL_dscale + 3 * i;
+        const bool acc_s = a.acc & ACC_SCALES;
+        put(dsp, ds[0], acc_s, in.old_scale[0]);
+        put(dsp + 1, ds[1], acc_s, in.old_scale[1]);
+        put(dsp + 2, ds[2], acc_s, in.old_scale[2]);
+        float* dr = a.dL_drot + 4 * i;
+        const bool acc_r = a.acc & ACC_ROTATIONS;
+        put(dr, dq.x, acc_r, in.old_rot[0]); put(dr + 1, dq.y, acc_r, in.old_rot[1]);
+        put(dr + 2, dq.z, acc_r, in.old_rot[2]); put(dr + 3, dq.w, acc_r, in.old_rot[3]);
+    } else {
+        if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
+            a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
+        }
+        if (a.dL_drot && !(a.acc & ACC_ROTATIONS)) {
+            float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f;
+        }
+    }
+}
+
+// Everything of one Gaussian except the SH coefficients, for the launch's own view: the reduced
+// render gradients, view_grad, computeCov3D backward; sets up the SH state.
 __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, const BwdIn& in, BwdState& st)
 {
     const size_t i = (size_t)idx;
@@ -246,20 +522,11 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         return;
     }
 
-    float g[GF_NUM];
-#pragma unroll
-    for (int q = 0; q < GF_NUM; q++) g[q] = in.g[q];
-    {
-        // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
-        const float4 co = in.co;
-        const float op = co.w;
-        const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
-        g[GF_MEAN2D_X] = (co.x * sx + co.y * sy) * (-op * (0.5f * a.W));
-        g[GF_MEAN2D_Y] = (co.y * sx + co.z * sy) * (-op * (0.5f * a.H));
-        g[GF_CONIC_A] *= -0.5f * op;
-        g[GF_CONIC_B] *= -0.5f * op;
-        g[GF_CONIC_C] *= -0.5f * op;
-    }
+    float cov3D[6];
+    cov3d_of(a, in, cov3D);
+    ViewGrad o;
+    view_grad(a, cam_of(a), in.g, in.co, in.clamped, in.mean, in.opacity, cov3D, o);
+    const float* g = o.g;
     // render-pass gradients of the reference glue (rasterize_points.cu:164-172), fully written
     a.dL_dmean2D[3 * i] = g[GF_MEAN2D_X]; a.dL_dmean2D[3 * i + 1] = g[GF_MEAN2D_Y]; a.dL_dmean2D[3 * i + 2] = 0.f;
     a.dL_dconic[4 * i] = g[GF_CONIC_A]; a.dL_dconic[4 * i + 1] = g[GF_CONIC_B]; a.dL_dconic[4 * i + 2] = 0.f;
@@ -271,204 +538,22 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
         put(a.dL_dcolor + 3 * i + 2, g[GF_COLOR_B], acc);
     }
     if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
-
-    // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
-    float cov_local[6];
-    const float* cov3D = in.cov;
-    if (!a.cov3D_precomp) {  // forward.cu:114-151 recomputed (bit-identical to the forward's)
-        const float scl[3] = {in.scale.x, in.scale.y, in.scale.z};
-        computeCov3D(scl, a.scale_modifier, in.rot, cov_local);
-        cov3D = cov_local;
-    }
-    const f3 mean = in.mean;
-    const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
-    const float* view = a.view;
-    f3 t = transformPoint4x3(mean, view);
-    const float limx = 1.3f * a.tan_fovx;
-    const float limy = 1.3f * a.tan_fovy;
-    const float txtz = t.x / t.z;
-    const float tytz = t.y / t.z;
-    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
-    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
-    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
-    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
-    const float h_x = a.focal_x, h_y = a.focal_y;
-    const mat3 J = mat3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z),
-                             0.0f, h_y / t.z, -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
-    const mat3 Wm = mat3_cols(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
-    const mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
-                               cov3D[5]);
-    const mat3 T = mat3_mul(Wm, J);
-    const mat3 cov2D = mat3_mul(mat3_mul(mat3_T(T), mat3_T(Vrk)), T);
-    float c_xx = cov2D.m[0][0];
-    float c_xy = cov2D.m[0][1];
-    float c_yy = cov2D.m[1][1];
-    const float h_var = 0.3f;
-    float d_inside_root = 0.f;
-    if (a.antialiasing) {
-        const float det_cov = c_xx * c_yy - c_xy * c_xy;
-        c_xx += h_var;
-        c_yy += h_var;
-        const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
-        const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
-        const float dL_dopacity_v = g[GF_OPACITY];
-        const float d_h_convolution_scaling = dL_dopacity_v * in.opacity;
-        put(a.dL_dopacity + idx, dL_dopacity_v * h_convolution_scaling, a.acc & ACC_OPACITY, in.old_opacity);
-        d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f
-                                                                    : d_h_convolution_scaling / (2 * h_convolution_scaling);
-    } else {
-        c_xx += h_var;
-        c_yy += h_var;
-        put(a.dL_dopacity + idx, g[GF_OPACITY], a.acc & ACC_OPACITY, in.old_opacity);
-    }
-    float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
-    if (a.antialiasing) {
-        const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
-        const float denom_f = d_inside_root / sq(w * w + w * (x + y) + x * y - z * z);
-        dL_dc_xx = w * (w * y + y * y + z * z) * denom_f;
-        dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
-        dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
-    }
-    const float denom = c_xx * c_yy - c_xy * c_xy;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    const float(*Tm)[3] = T.m;
-    float dcov[6];
-    if (denom2inv != 0) {
-        dL_dc_xx += denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
-                                 (denom - c_xx * c_yy) * dL_dconic.z);
-        dL_dc_yy += denom2inv * (-c_xx * c_xx * dL_dconic.z + 2 * c_xx * c_xy * dL_dconic.y +
-                                 (denom - c_xx * c_yy) * dL_dconic.x);
-        dL_dc_xy += denom2inv * 2 *
-                    (c_xy * c_yy * dL_dconic.x - (denom + 2 * c_xy * c_xy) * dL_dconic.y + c_xx * c_xy * dL_dconic.z);
-        dcov[0] = (Tm[0][0] * Tm[0][0] * dL_dc_xx + Tm[0][0] * Tm[1][0] * dL_dc_xy + Tm[1][0] * Tm[1][0] * dL_dc_yy);
-        dcov[3] = (Tm[0][1] * Tm[0][1] * dL_dc_xx + Tm[0][1] * Tm[1][1] * dL_dc_xy + Tm[1][1] * Tm[1][1] * dL_dc_yy);
-        dcov[5] = (Tm[0][2] * Tm[0][2] * dL_dc_xx + Tm[0][2] * Tm[1][2] * dL_dc_xy + Tm[1][2] * Tm[1][2] * dL_dc_yy);
-        dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_dc_xx + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_dc_xy +
-                  2 * Tm[1][0] * Tm[1][1] * dL_dc_yy;
-        dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_dc_xx + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_dc_xy +
-                  2 * Tm[1][0] * Tm[1][2] * dL_dc_yy;
-        dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_dc_xx + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_dc_xy +
-                  2 * Tm[1][1] * Tm[1][2] * dL_dc_yy;
-    } else {
+    put(a.dL_dopacity + idx, o.dopacity, a.acc & ACC_OPACITY, in.old_opacity);
 #pragma unroll
-        for (int k = 0; k < 6; k++) dcov[k] = 0;
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) put(dcov_out + k, dcov[k], a.acc & ACC_COV3D);
-    const float(*V)[3] = Vrk.m;
-    const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
-                          (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
-    const float dL_dT01 = 2 * (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xx +
-                          (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_xy;
-    const float dL_dT02 = 2 * (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xx +
-                          (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_xy;
-    const float dL_dT10 = 2 * (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_yy +
-                          (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xy;
-    const float dL_dT11 = 2 * (Tm[1][0] * V[1][0] + Tm[1][1] * V[1][1] + Tm[1][2] * V[1][2]) * dL_dc_yy +
-                          (Tm[0][0] * V[1][0] + Tm[0][1] * V[1][1] + Tm[0][2] * V[1][2]) * dL_dc_xy;
-    const float dL_dT12 = 2 * (Tm[1][0] * V[2][0] + Tm[1][1] * V[2][1] + Tm[1][2] * V[2][2]) * dL_dc_yy +
-                          (Tm[0][0] * V[2][0] + Tm[0][1] * V[2][1] + Tm[0][2] * V[2][2]) * dL_dc_xy;
-    const float(*Wq)[3] = Wm.m;
-    const float dL_dJ00 = Wq[0][0] * dL_dT00 + Wq[0][1] * dL_dT01 + Wq[0][2] * dL_dT02;
-    const float dL_dJ02 = Wq[2][0] * dL_dT00 + Wq[2][1] * dL_dT01 + Wq[2][2] * dL_dT02;
-    const float dL_dJ11 = Wq[1][0] * dL_dT10 + Wq[1][1] * dL_dT11 + Wq[1][2] * dL_dT12;
-    const float dL_dJ12 = Wq[2][0] * dL_dT10 + Wq[2][1] * dL_dT11 + Wq[2][2] * dL_dT12;
-    const float tz = 1.f / t.z;
-    const float tz2 = tz * tz;
-    const float tz3 = tz2 * tz;
-    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
-    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
-    float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
-                   (2 * h_y * t.y) * tz3 * dL_dJ12;
-    if (a.has_invdepth) dL_dtz -= g[GF_INVDEPTH] / (t.z * t.z);
-    const f3 dm_cov = transformVec4x3Transpose({dL_dtx, dL_dty, dL_dtz}, view);
-    float dmx = dm_cov.x, dmy = dm_cov.y, dmz = dm_cov.z;
-
-    // ---------------- preprocessCUDA (backward.cu:423-440) ----------------
-    {
-        const float* proj = a.proj;
-        const f3 m = mean;
-        const float4 m_hom = transformPoint4x4(m, proj);
-        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
-        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
-        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-        const float g2x = g[GF_MEAN2D_X], g2y = g[GF_MEAN2D_Y];
-        dmx += (proj[0] * m_w - proj[3] * mul1) * g2x + (proj[1] * m_w - proj[3] * mul2) * g2y;
-        dmy += (proj[4] * m_w - proj[7] * mul1) * g2x + (proj[5] * m_w - proj[7] * mul2) * g2y;
-        dmz += (proj[8] * m_w - proj[11] * mul1) * g2x + (proj[9] * m_w - proj[11] * mul2) * g2y;
-    }
-    st.dmx = dmx;
-    st.dmy = dmy;
-    st.dmz = dmz;
-
-    // ---------------- computeColorFromSH backward: set-up (backward.cu:28-49) ----------------
+    for (int k = 0; k < 6; k++) put(dcov_out + k, o.dcov[k], a.acc & ACC_COV3D);
+    st.dmx = o.dmx;
+    st.dmy = o.dmy;
+    st.dmz = o.dmz;
     if (a.shs || a.dc) {
-        const int deg = a.D;
-        int nc = (deg + 1) * (deg + 1);
-        nc = nc < a.M ? nc : a.M;
-        st.ncoef = nc < 16 ? nc : 16;
-        st.dir_orig = {mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]};
-        const f3 d = st.dir_orig;
-        const float len = sqrtf(d.x * d.x + d.y * d.y + d.z * d.z);
-        st.x = d.x / len;
-        st.y = d.y / len;
-        st.z = d.z / len;
-        const uint8_t cl = in.clamped;
+        st.ncoef = sh_ncoef(a);
+        st.dir_orig = o.dir_orig;
+        st.x = o.x;
+        st.y = o.y;
+        st.z = o.z;
 #pragma unroll
-        for (int c = 0; c < 3; c++) st.dRGB[c] = g[GF_COLOR_R + c] * ((cl >> c) & 1 ? 0 : 1);
+        for (int c = 0; c < 3; c++) st.dRGB[c] = o.dRGB[c];
     }
-
-    // ---------------- computeCov3D backward (backward.cu:330-393) ----------------
-    if (a.scales) {
-        const float r = in.rot.x, x = in.rot.y, y = in.rot.z, z = in.rot.w;
-        const mat3 R = mat3_cols(
-            1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
-            2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
-            2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
-        mat3 S = mat3_cols(1.0f, 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 1.0f);
-        const float mod = a.scale_modifier;
-        const f3 s = {mod * in.scale.x, mod * in.scale.y, mod * in.scale.z};
-        S.m[0][0] = s.x; S.m[1][1] = s.y; S.m[2][2] = s.z;
-        const mat3 M = mat3_mul(S, R);
-        const float* d = dcov;
-        const mat3 dL_dSigma = mat3_cols(d[0], 0.5f * d[1], 0.5f * d[2], 0.5f * d[1], d[3], 0.5f * d[4],
-                                         0.5f * d[2], 0.5f * d[4], d[5]);
-        mat3 M2;
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-#pragma unroll
-            for (int w = 0; w < 3; w++) M2.m[c][w] = 2.0f * M.m[c][w];
-        const mat3 dL_dM = mat3_mul(M2, dL_dSigma);
-        const mat3 Rt = mat3_T(R);
-        mat3 G = mat3_T(dL_dM);
-        float* ds = a.dL_dscale + 3 * i;
-        const bool acc_s = a.acc & ACC_SCALES;
-        put(ds, Rt.m[0][0] * G.m[0][0] + Rt.m[0][1] * G.m[0][1] + Rt.m[0][2] * G.m[0][2], acc_s, in.old_scale[0]);
-        put(ds + 1, Rt.m[1][0] * G.m[1][0] + Rt.m[1][1] * G.m[1][1] + Rt.m[1][2] * G.m[1][2], acc_s, in.old_scale[1]);
-        put(ds + 2, Rt.m[2][0] * G.m[2][0] + Rt.m[2][1] * G.m[2][1] + Rt.m[2][2] * G.m[2][2], acc_s, in.old_scale[2]);
-#pragma unroll
-        for (int w = 0; w < 3; w++) { G.m[0][w] *= s.x; G.m[1][w] *= s.y; G.m[2][w] *= s.z; }
-        const float(*gm)[3] = G.m;
-        float4 dq;
-        dq.x = 2 * z * (gm[0][1] - gm[1][0]) + 2 * y * (gm[2][0] - gm[0][2]) + 2 * x * (gm[1][2] - gm[2][1]);
-        dq.y = 2 * y * (gm[1][0] + gm[0][1]) + 2 * z * (gm[2][0] + gm[0][2]) + 2 * r * (gm[1][2] - gm[2][1]) -
-               4 * x * (gm[2][2] + gm[1][1]);
-        dq.z = 2 * x * (gm[1][0] + gm[0][1]) + 2 * r * (gm[2][0] - gm[0][2]) + 2 * z * (gm[1][2] + gm[2][1]) -
-               4 * y * (gm[2][2] + gm[0][0]);
-        dq.w = 2 * r * (gm[0][1] - gm[1][0]) + 2 * x * (gm[2][0] + gm[0][2]) + 2 * y * (gm[1][2] + gm[2][1]) -
-               4 * z * (gm[1][1] + gm[0][0]);
-        float* dr = a.dL_drot + 4 * i;
-        const bool acc_r = a.acc & ACC_ROTATIONS;
-        put(dr, dq.x, acc_r, in.old_rot[0]); put(dr + 1, dq.y, acc_r, in.old_rot[1]);
-        put(dr + 2, dq.z, acc_r, in.old_rot[2]); put(dr + 3, dq.w, acc_r, in.old_rot[3]);
-    } else {
-        if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
-            a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
-        }
-        if (a.dL_drot && !(a.acc & ACC_ROTATIONS)) {
-            float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f;
-        }
-    }
+    put_scale_rot(a, idx, in, o.dcov);
 }
 
 // SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's traffic.
@@ -479,28 +564,152 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
 // most 128-B lines of a row are then fetched in both halves.)
 constexpr int SH_STRIDE = 49;  // LDS dwords per row (odd)
 
-template <bool STAGED>
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a)
+// ---- multi-view batch (gsr_backward_views) ------------------------------------------------
+// One thread per Gaussian reads its parameters and SH row once and walks the V views of the batch:
+// per view the records, the 2D chain rule (view_grad), the screen-space gradient of that view and
+// the SH terms of that view's direction; dL/dcov3D, dL/dmean3D, dL/dopacity, dL/dcolor and dL/dsh
+// are summed over the views in registers, and scale / rotation are differentiated once from the
+// summed dL/dcov3D (linear in it).  The parameters (236 B per Gaussian at degree 3) are read and
+// their gradients written once per batch instead of once per view.
+__device__ __forceinline__ ViewCam cam_of(const BwdView& v)
+{
+    return {v.view, v.proj, v.campos, v.focal_x, v.focal_y, v.tan_fovx, v.tan_fovy};
+}
+
+// c0: SH coefficient 0 (3 floats), cr: coefficient k >= 1 at cr[3 (k - 1)]; d0 / dr the same for
+// dL/dsh (may alias c0 / cr: every coefficient is read before any is written), kw the number of
+// coefficients to write (zeros from the first unused one); acc: add to d0 / dr.
+__device__ __forceinline__ void bwd_views(const PreprocessBwdViewsArgs& A, int idx, const BwdIn& in, const float* c0,
+                                          const float* cr, float* d0, float* dr, int kw, bool acc_dc, bool acc_sh)
+{
+    const PreprocessBwdArgs& a = A.a;
+    const size_t i = (size_t)idx;
+    float cov3D[6];
+    cov3d_of(a, in, cov3D);
+    const int nc = sh_ncoef(a);
+    float dsh[16][3];
+#pragma unroll
+    for (int k = 0; k < 16; k++) dsh[k][0] = dsh[k][1] = dsh[k][2] = 0.f;
+    float dop = 0.f, dcol[3] = {0.f, 0.f, 0.f}, dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dm[3] = {0.f, 0.f, 0.f};
+    for (int v = 0; v < A.V; v++) {
+        const BwdView& bv = A.v[v];
+        float* m2 = bv.dL_dmean2D + 3 * i;
+        if (!(bv.radii[idx] > 0)) {
+            m2[0] = 0.f; m2[1] = 0.f; m2[2] = 0.f;
+            continue;
+        }
+        float gs[GF_NUM];
+        gather_records(bv.emit_start, bv.tiles_touched, bv.valid, bv.grad_inst, idx, gs);
+        ViewGrad o;
+        view_grad(a, cam_of(bv), gs, bv.conic_opacity[idx], bv.clamped[idx], in.mean, in.opacity, cov3D, o);
+        m2[0] = o.g[GF_MEAN2D_X]; m2[1] = o.g[GF_MEAN2D_Y]; m2[2] = 0.f;
+        dop += o.dopacity;
+#pragma unroll
+        for (int c = 0; c < 3; c++) dcol[c] += o.g[GF_COLOR_R + c];
+#pragma unroll
+        for (int k = 0; k < 6; k++) dcov[k] += o.dcov[k];
+        dm[0] += o.dmx;
+        dm[1] += o.dmy;
+        dm[2] += o.dmz;
+        if (nc > 0) {  // computeColorFromSH backward (backward.cu:51-141) for this view's direction
+            float ddir[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                if (k < nc) {
+                    float b, gx, gy, gz;
+                    sh_term(k, o.x, o.y, o.z, b, gx, gy, gz);
+                    const float* shk = k == 0 ? c0 : cr + 3 * (k - 1);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        const float t = shk[c] * o.dRGB[c];
+                        dsh[k][c] += b * o.dRGB[c];
+                        ddir[0] += t * gx;
+                        ddir[1] += t * gy;
+                        ddir[2] += t * gz;
+                    }
+                }
+            }
+            if (nc > 1) {  // degree 0 has no direction dependence
+                const f3 dn = dnormvdv(o.dir_orig, {ddir[0], ddir[1], ddir[2]});
+                dm[0] += dn.x;
+                dm[1] += dn.y;
+                dm[2] += dn.z;
+            }
+        }
+    }
+    put(a.dL_dopacity + i, dop, a.acc & ACC_OPACITY, in.old_opacity);
+    if (a.dL_dcolor) {
+        const bool acc = a.acc & ACC_COLORS;
+#pragma unroll
+        for (int c = 0; c < 3; c++) put(a.dL_dcolor + 3 * i + c, dcol[c], acc);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; k++) put(a.dL_dcov3D + 6 * i + k, dcov[k], a.acc & ACC_COV3D);
+    put_scale_rot(a, idx, in, dcov);
+    const bool acc_m = a.acc & ACC_MEANS3D;
+    float* dmean = a.dL_dmean3D + 3 * i;
+    put(dmean, dm[0], acc_m, in.old_mean[0]);
+    put(dmean + 1, dm[1], acc_m, in.old_mean[1]);
+    put(dmean + 2, dm[2], acc_m, in.old_mean[2]);
+    if (d0) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) put(d0 + c, dsh[0][c], acc_dc);
+    }
+    if (dr) {
+#pragma unroll
+        for (int k = 1; k < 16; k++)
+            if (k < kw) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) put(dr + 3 * (k - 1) + c, dsh[k][c], acc_sh);
+            }
+    }
+}
+
+// STAGED: the SH rows of the workgroup's 256 Gaussians go through LDS (see below); MULTI: the
+// multi-view batch (A.V views), else the single view of A.a.
+template <bool STAGED, bool MULTI>
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwdViewsArgs A)
 {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const PreprocessBwdArgs& a = A.a;
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
     BwdIn in;
     BwdState st;
-    if (idx < a.P) bwd_gather(a, idx, in);  // in flight during the SH staging below
+    if (idx < a.P) bwd_gather(a, idx, in, !MULTI);  // in flight during the SH staging below
+    // one Gaussian's work on its SH row (coefficient 0 at c0, k >= 1 at cr[3 (k - 1)]), in place
+    auto work = [&](float* c0, float* cr, int kw) {
+        if constexpr (MULTI) {
+            bwd_views(A, idx, in, c0, cr, c0, cr, kw, false, false);
+        } else {
+            bwd_core(a, idx, in, st);
+            sh_bwd_range<0, 1>(st, c0, c0);
+            sh_bwd_range<1, 16>(st, cr, cr, kw);
+            bwd_finish(a, idx, st);
+        }
+    };
     if (!STAGED) {
         if (idx < a.P) {
-            bwd_core(a, idx, in, st);
-            if (a.dL_dsh) {
-                const size_t w3 = (size_t)a.M * 3;
-                float* dsh = a.dL_dsh + idx * w3;
-                // ncoef <= M: no read past the row; no write past it either (M < 16)
-                const bool acc = a.acc & ACC_SH;
-                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
-                if (!acc)
-                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
+            const size_t w3 = (size_t)a.M * 3;
+            if constexpr (MULTI) {
+                const float* row = a.shs ? a.shs + idx * w3 : nullptr;
+                float* drow = (a.shs && a.dL_dsh) ? a.dL_dsh + idx * w3 : nullptr;
+                bwd_views(A, idx, in, row, row ? row + 3 : nullptr, drow, drow ? drow + 3 : nullptr, a.M,
+                          a.acc & ACC_SH, a.acc & ACC_SH);
+                if (a.dL_dsh && !(a.acc & ACC_SH))
+                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) a.dL_dsh[idx * w3 + k] = 0.f;
+            } else {
+                bwd_core(a, idx, in, st);
+                if (a.dL_dsh) {
+                    float* dsh = a.dL_dsh + idx * w3;
+                    // ncoef <= M: no read past the row; no write past it either (M < 16)
+                    const bool acc = a.acc & ACC_SH;
+                    if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
+                    if (!acc)
+                        for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
+                }
+                bwd_finish(a, idx, st);
             }
-            bwd_finish(a, idx, st);
         }
         return;
     }
@@ -511,14 +720,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
         if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
         __syncthreads();
-        if (idx < a.P) {
-            bwd_core(a, idx, in, st);
-            float* d0 = s_sh + 3 * threadIdx.x;
-            float* r = s_rest + wr * threadIdx.x;
-            sh_bwd_range<0, 1>(st, d0, d0);
-            sh_bwd_range<1, 16>(st, r, r, a.M);
-            bwd_finish(a, idx, st);
-        }
+        if (idx < a.P) work(s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x, a.M);
         __syncthreads();
         lds_copy_out(a.dL_ddc + (size_t)base * 3, s_sh, n * 3, a.acc & ACC_DC);
         if (wr > 0) lds_copy_out(a.dL_dsh + (size_t)base * wr, s_rest, n * wr, a.acc & ACC_SH);
@@ -530,11 +732,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
         if (a.shs && wr > 0) lds_rows_in(s_sh, SH_STRIDE, 3, 48, a.shs + (size_t)base * wr, wr, n);
         __syncthreads();
         float* row = s_sh + threadIdx.x * SH_STRIDE;
-        if (idx < a.P) {
-            bwd_core(a, idx, in, st);
-            sh_bwd_range<0, 16>(st, row, row);
-            bwd_finish(a, idx, st);
-        }
+        if (idx < a.P) work(row, row + 3, 16);
         __syncthreads();
         lds_rows_out(a.dL_ddc + (size_t)base * 3, 3, n, s_sh, SH_STRIDE, 0, 48, a.acc & ACC_DC);
         if (a.dL_dsh && wr > 0)
@@ -550,11 +748,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     }
     __syncthreads();
     float* row = s_sh + threadIdx.x * SH_STRIDE;
-    if (idx < a.P) {
-        bwd_core(a, idx, in, st);
-        sh_bwd_range<0, 16>(st, row, row);
-        bwd_finish(a, idx, st);
-    }
+    if (idx < a.P) work(row, row + 3, 16);
     __syncthreads();
     store_f4(reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48), n * 12, a.acc & ACC_SH, [&](int f) {
         const int g = f / 12, j = f - g * 12;
@@ -563,15 +757,33 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(PreprocessBwdArgs a
     });
 }
 
-hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
+template <bool MULTI>
+static hipError_t launch_bwd(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
+    const PreprocessBwdArgs& a = A.a;
     if (a.P <= 0) return hipSuccess;
     const bool staged = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
                         ((uintptr_t)a.dL_dsh % 16) == 0;
+    const dim3 grid((a.P + 255) / 256), block(256);
     if (staged || (a.dc && a.dL_ddc))
-        hipLaunchKernelGGL(preprocess_bwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), 256 * SH_STRIDE * 4, s, a);
-    else hipLaunchKernelGGL(preprocess_bwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((preprocess_bwd_kernel<true, MULTI>), grid, block, 256 * SH_STRIDE * 4, s, A);
+    else
+        hipLaunchKernelGGL((preprocess_bwd_kernel<false, MULTI>), grid, block, 0, s, A);
     return hipGetLastError();
+}
+
+hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
+{
+    PreprocessBwdViewsArgs A;
+    A.a = a;
+    A.V = 0;
+    return launch_bwd<false>(A, s);
+}
+
+hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
+{
+    if (A.V < 1 || A.V > MAX_VIEWS) return hipErrorInvalidValue;
+    return launch_bwd<true>(A, s);
 }
 
 }  // namespace gsr

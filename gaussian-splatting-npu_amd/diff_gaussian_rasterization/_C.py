@@ -48,6 +48,9 @@ def _load():
                                     _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp, _b, _b, _vp]
     lib.gsr_backward_dc_acc.argtypes = lib.gsr_backward_dc.argtypes[:-1] + [ctypes.c_uint, _vp]
+    lib.gsr_backward_views.argtypes = [_i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
+                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _vp, _vp, _vp, _b, _b, ctypes.c_uint, _vp]
     lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
     lib.gsr_adam_update_multi.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
@@ -123,10 +126,12 @@ def _sh_split(sh, dc):
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
                         viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
-                        prefiltered, antialiasing, debug, dc=None):
+                        prefiltered, antialiasing, debug, dc=None, out=None):
     """RasterizeGaussiansNPU (rasterize_points.cu:35-124).  `dc` (P,1,3): the separate-DC form of
     the accelerated upstream op (coefficient 0 apart from the rest in `sh`), selected by train.py
-    together with SparseGaussianAdam (train.py:37-41, gaussian_renderer/__init__.py:82-100)."""
+    together with SparseGaussianAdam (train.py:37-41, gaussian_renderer/__init__.py:82-100).
+    `out` (color (3,H,W), radii (P,), invdepth (1,H,W)): caller-provided outputs, e.g. slices of a
+    multi-view batch (MultiViewRasterizer) -- written in full."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     _require_gpu(means3D)
@@ -140,9 +145,16 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         return 0, out_color, radii, empty(), empty(), empty(), out_invdepth
 
     # every element of these is written by the HIP forward (radii by preprocess, pixels by render)
-    radii = torch.empty((P,), dtype=torch.int32, device=dev)
-    out_invdepth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
-    out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    if out is not None:
+        out_color, radii, out_invdepth = out
+        for t, shape, dt in ((out_color, (3, H, W), torch.float32), (radii, (P,), torch.int32),
+                             (out_invdepth, (1, H, W), torch.float32)):
+            if tuple(t.shape) != shape or t.dtype != dt or t.device != dev or not t.is_contiguous():
+                raise RuntimeError(f"out: expected a contiguous {dt} tensor of shape {shape} on {dev}")
+    else:
+        radii = torch.empty((P,), dtype=torch.int32, device=dev)
+        out_invdepth = torch.empty((1, H, W), dtype=torch.float32, device=dev)
+        out_color = torch.empty((3, H, W), dtype=torch.float32, device=dev)
     M, has_dc = _sh_split(sh, dc)
     if has_dc and (dc.dim() != 3 or dc.size(0) != P or dc.size(1) != 1 or dc.size(2) != 3):
         raise RuntimeError("dc must have dimensions (num_points, 1, 3)")
@@ -281,6 +293,91 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
         dL_ddc.data_ptr() if has_dc else None, dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(),
         dL_drotations.data_ptr(), bool(antialiasing), bool(debug), mask, _stream(dev)))
     return result()
+
+
+def _ptr_array(ts):
+    return (_vp * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+
+
+def rasterize_gaussians_backward_views(background, means3D, radii, colors, opacities, scales, rotations,
+                                       scale_modifier, cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy,
+                                       dL_dout_colors, dL_dout_invdepths, sh, degree, campos, geomBuffers, Rs,
+                                       binningBuffers, imageBuffers, antialiasing, debug, dc=None, accumulate=None):
+    """Backward of a batch of V views (gsr_backward_views): per-view lists of the forward's state
+    (radii (P,), camera, buffers, num_rendered) and dL_dout_colors (V,3,H,W), dL_dout_invdepths
+    (V,1,H,W) or None.  Returns (dL_dmeans2D (V,P,3), dL_dcolors, dL_dopacity, dL_dmeans3D,
+    dL_dcov3D, [dL_ddc,] dL_dsh, dL_dscales, dL_drotations): the screen-space gradient per view,
+    everything else summed over the views; `accumulate` as in rasterize_gaussians_backward."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    V = len(geomBuffers)
+    H, W = dL_dout_colors.size(2), dL_dout_colors.size(3)
+    M, has_dc = _sh_split(sh, dc)
+    has_inv = dL_dout_invdepths is not None and dL_dout_invdepths.numel() != 0
+    if dL_dout_colors.shape != (V, 3, H, W) or (has_inv and dL_dout_invdepths.shape != (V, 1, H, W)):
+        raise RuntimeError("dL_dout_colors must be (V,3,H,W) and dL_dout_invdepths (V,1,H,W)")
+    acc = dict(accumulate or {})
+    for k, t in acc.items():
+        n = {"means3D": 3 * P, "dc": 3 * P, "sh": 3 * M * P, "opacities": P, "scales": 3 * P, "rotations": 4 * P,
+             "cov3D_precomp": 6 * P, "colors_precomp": 3 * P}.get(k)
+        if n is None:
+            raise RuntimeError(f"accumulate: unknown gradient {k!r}")
+        if t.device != dev or t.dtype != torch.float32 or not t.is_contiguous() or t.numel() != n:
+            raise RuntimeError(f"accumulate[{k!r}] must be a contiguous float32 tensor of {n} elements on {dev}")
+    dL_dmeans2D = torch.empty((V, P, 3), dtype=torch.float32, device=dev)
+    sizes = [0 if "means3D" in acc else 3 * P, 3 * P if has_dc and "dc" not in acc else 0,
+             0 if "sh" in acc else 3 * M * P, 0 if "opacities" in acc else P, 0 if "scales" in acc else 3 * P,
+             0 if "rotations" in acc else 4 * P, 0 if "cov3D_precomp" in acc else 6 * P,
+             0 if "colors_precomp" in acc else 3 * P]
+    parts = torch.split(torch.empty((sum(sizes),), dtype=torch.float32, device=dev), sizes)
+    r = {"means3D": acc.get("means3D", parts[0]).view(P, 3),
+         "dc": acc.get("dc", parts[1]).view(P, 1, 3) if has_dc else None,
+         "sh": acc.get("sh", parts[2]).view(P, M, 3), "opacities": acc.get("opacities", parts[3]).view(P, 1),
+         "scales": acc.get("scales", parts[4]).view(P, 3), "rotations": acc.get("rotations", parts[5]).view(P, 4),
+         "cov3D_precomp": acc.get("cov3D_precomp", parts[6]).view(P, 6),
+         "colors_precomp": acc.get("colors_precomp", parts[7]).view(P, 3)}
+    keep = []
+
+    def p(t, name):
+        ptr, tt = _ptr(t, name, dev)
+        keep.append(tt)
+        return ptr
+
+    def cont(ts, name):
+        out = []
+        for t in ts:
+            ptr, tt = _ptr(t, name, dev)
+            keep.append(tt)
+            out.append(tt)
+        return out
+
+    views = cont(viewmatrices, "viewmatrix")
+    projs = cont(projmatrices, "projmatrix")
+    cams = cont(campos, "campos")
+    dpix = [dL_dout_colors[v].contiguous() for v in range(V)]
+    dinv = [dL_dout_invdepths[v].contiguous() for v in range(V)] if has_inv else None
+    keep.extend(dpix)
+    mask = 0
+    for k in acc:
+        mask |= ACC_BITS[k]
+    _check(lib.gsr_backward_views(
+        V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), p(background, "bg"), W, H, p(means3D, "means3D"),
+        p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"), p(opacities, "opacities"),
+        p(scales, "scales"), float(scale_modifier), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp"),
+        _ptr_array(views), _ptr_array(projs), _ptr_array(cams), (_f * V)(*[float(x) for x in tan_fovx]),
+        (_f * V)(*[float(x) for x in tan_fovy]), _ptr_array(radii), _ptr_array(geomBuffers),
+        _ptr_array([b if b.numel() else None for b in binningBuffers]), _ptr_array(imageBuffers),
+        _ptr_array(dpix), _ptr_array(dinv) if has_inv else None, _ptr_array([dL_dmeans2D[v] for v in range(V)]),
+        r["colors_precomp"].data_ptr(), r["opacities"].data_ptr(), r["means3D"].data_ptr(),
+        r["cov3D_precomp"].data_ptr(), r["dc"].data_ptr() if has_dc else None, r["sh"].data_ptr() if M else None,
+        r["scales"].data_ptr(), r["rotations"].data_ptr(), bool(antialiasing), bool(debug), mask, _stream(dev)))
+    r = {k: (None if k in acc else v) for k, v in r.items()}
+    if has_dc:
+        return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["dc"], r["sh"],
+                r["scales"], r["rotations"])
+    return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["sh"],
+            r["scales"], r["rotations"])
 
 
 def _adam_check(param, param_grad, exp_avg, exp_avg_sq, N, M, dev):

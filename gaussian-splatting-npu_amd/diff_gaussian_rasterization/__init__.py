@@ -21,7 +21,7 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam",
-           "accumulate_grads_in_place"]
+           "accumulate_grads_in_place", "MultiViewRasterizer", "rasterize_views"]
 
 _state = threading.local()
 
@@ -44,6 +44,13 @@ def accumulate_grads_in_place(enabled=True):
         yield
     finally:
         _state.accumulate = prev
+
+
+# Per device: an event recorded after the last backward run inside accumulate_grads_in_place.
+# Views rendered on different HIP streams (forward of one view overlapping the backward of the
+# previous) add into the same .grad buffers; each in-place accumulating backward first makes its
+# stream wait for this event, so the additions stay ordered.
+_acc_fence = {}
 
 
 def _accumulation_target(t):
@@ -126,11 +133,22 @@ class _RasterizeGaussians(torch.autograd.Function):
                           if g is not None}
             if "dc" in accumulate and (dc is None or dc.numel() == 0):
                 del accumulate["dc"]
+            dev = means3D.device
+            stream = torch.cuda.current_stream(dev)
+            fence = _acc_fence.get(dev)
+            if accumulate and fence is not None:
+                stream.wait_event(fence)
+            for g in accumulate.values():
+                g.record_stream(stream)  # may have been allocated on another view's stream
         grads = _C.rasterize_gaussians_backward(
             s.bg, means3D, radii, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
             s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, grad_out_depth, sh, s.sh_degree,
             s.campos, geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.antialiasing, s.debug, dc=dc,
             accumulate=accumulate)
+        if ctx.acc_inputs is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            _acc_fence[dev] = ev
         if len(grads) == 9:
             (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
              grad_scales, grad_rotations) = grads
@@ -173,6 +191,165 @@ class GaussianRasterizer(nn.Module):
             absent if rotations is None else rotations,
             absent if cov3D_precomp is None else cov3D_precomp,
             s, dc)
+
+
+def _check_inputs(shs, colors_precomp, scales, rotations, cov3D_precomp, dc):
+    """The reference's argument rules (diff_gaussian_rasterization/__init__.py:178-182)."""
+    if (shs is None) == (colors_precomp is None) or (dc is not None and colors_precomp is not None):
+        raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+    if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+            ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+        raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+
+
+_side_streams = {}
+
+
+def _side_stream(dev):
+    st = _side_streams.get(dev)
+    if st is None:
+        st = _side_streams[dev] = torch.cuda.Stream(dev)
+    return st
+
+
+def rasterize_views(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                    raster_settings, dc=None):
+    return _RasterizeViews.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                 cov3Ds_precomp, tuple(raster_settings), dc)
+
+
+class _RasterizeViews(torch.autograd.Function):
+    """A batch of V camera views of the same Gaussians as ONE autograd node (the
+    views of a data-parallel step).  Forward: each view through the single-view forward (same
+    kernels, bit-identical outputs) into slices of (V,3,H,W) / (V,P) / (V,1,H,W) outputs.
+    Backward: _C.rasterize_gaussians_backward_views -- every view's BACKWARD::render, then one
+    pass of BACKWARD::preprocess that reads each Gaussian's parameters once and writes their
+    gradients summed over the views, where V single-view backward passes would read and write the
+    236 B/Gaussian V times.  means2D is (V,P,3): its gradient is each view's screen-space gradient
+    (what train.py's densification statistics read, gaussian_model.py:471-473)."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings, dc=None):
+        V = len(raster_settings)
+        s0 = raster_settings[0]
+        H, W, P = s0.image_height, s0.image_width, means3D.size(0)
+        dev = means3D.device
+        colors = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
+        radii = torch.empty((V, P), dtype=torch.int32, device=dev)
+        invdepths = torch.empty((V, 1, H, W), dtype=torch.float32, device=dev)
+        state = []
+        # The views alternate between the caller's stream and a second one, so that one view's
+        # binning (preprocess, sorts, scans: small latency-bound launches) runs beside the
+        # previous view's render; the caller's stream then waits for both.
+        main = torch.cuda.current_stream(dev)
+        streams = [main] + ([_side_stream(dev)] if V > 1 else [])
+        for st in streams[1:]:
+            st.wait_stream(main)
+        for v, s in enumerate(raster_settings):
+            st = streams[v % len(streams)]
+            with torch.cuda.stream(st):
+                L, _, _, geom, binning, img, _ = _C.rasterize_gaussians(
+                    s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+                    s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+                    s.campos, s.prefiltered, s.antialiasing, s.debug, dc=dc, out=(colors[v], radii[v], invdepths[v]))
+            if st is not main:
+                for t in (geom, binning, img):
+                    t.record_stream(main)  # used by the backward on the caller's stream
+            state.append((L, geom, binning, img))
+        for st in streams[1:]:
+            main.wait_stream(st)
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = [st[0] for st in state]
+        ctx.set_materialize_grads(False)
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, dc,
+                              *[t for st in state for t in st[1:]])
+        ctx.acc_inputs = None
+        if getattr(_state, "accumulate", False):
+            ctx.acc_inputs = {"means3D": means3D, "dc": dc, "sh": sh, "opacities": opacities, "scales": scales,
+                              "rotations": rotations, "cov3D_precomp": cov3Ds_precomp,
+                              "colors_precomp": colors_precomp}
+        return colors, radii, invdepths
+
+    @staticmethod
+    def backward(ctx, grad_colors, _grad_radii, grad_invdepths):
+        ss = ctx.raster_settings
+        s0 = ss[0]
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, opacities, dc,
+         *bufs) = ctx.saved_tensors
+        V = len(ss)
+        if grad_colors is None:
+            grad_colors = torch.zeros((V, 3, s0.image_height, s0.image_width), dtype=torch.float32,
+                                      device=means3D.device)
+        accumulate = None
+        if ctx.acc_inputs is not None:
+            accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in ctx.acc_inputs.items())
+                          if g is not None}
+            if "dc" in accumulate and (dc is None or dc.numel() == 0):
+                del accumulate["dc"]
+            dev = means3D.device
+            stream = torch.cuda.current_stream(dev)
+            fence = _acc_fence.get(dev)
+            if accumulate and fence is not None:
+                stream.wait_event(fence)
+            for g in accumulate.values():
+                g.record_stream(stream)
+        grads = _C.rasterize_gaussians_backward_views(
+            s0.bg, means3D, [radii[v] for v in range(V)], colors_precomp, opacities, scales, rotations,
+            s0.scale_modifier, cov3Ds_precomp, [s.viewmatrix for s in ss], [s.projmatrix for s in ss],
+            [s.tanfovx for s in ss], [s.tanfovy for s in ss], grad_colors, grad_invdepths, sh, s0.sh_degree,
+            [s.campos for s in ss], bufs[0::3], ctx.num_rendered, bufs[1::3], bufs[2::3], s0.antialiasing, s0.debug,
+            dc=dc, accumulate=accumulate)
+        if ctx.acc_inputs is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            _acc_fence[dev] = ev
+        if len(grads) == 9:
+            (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_dc, grad_sh,
+             grad_scales, grad_rotations) = grads
+        else:
+            (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+             grad_scales, grad_rotations) = grads
+            grad_dc = None
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                grad_rotations, grad_cov3Ds_precomp, None, grad_dc)
+
+
+class MultiViewRasterizer(nn.Module):
+    """GaussianRasterizer over a batch of V <= 16 views of the same Gaussians (one settings tuple
+    per view; image size, background, scale modifier, SH degree and flags shared).  forward takes
+    GaussianRasterizer's inputs with means2D of shape (V,P,3) and returns (colors (V,3,H,W), radii
+    (V,P), invdepths (V,1,H,W)); each view's outputs are bit-identical to GaussianRasterizer's, the
+    parameter gradients are the sums over the views (see _RasterizeViews)."""
+
+    def __init__(self, raster_settings_list):
+        super().__init__()
+        ss = tuple(raster_settings_list)
+        if not 1 <= len(ss) <= 16:
+            raise ValueError("MultiViewRasterizer takes 1 to 16 views")
+        s0 = ss[0]
+        for s in ss[1:]:
+            if (s.image_height, s.image_width, float(s.scale_modifier), s.sh_degree, bool(s.prefiltered),
+                    bool(s.debug), bool(s.antialiasing)) != (s0.image_height, s0.image_width, float(s0.scale_modifier),
+                                                             s0.sh_degree, bool(s0.prefiltered), bool(s0.debug),
+                                                             bool(s0.antialiasing)) or not torch.equal(s.bg, s0.bg):
+                raise ValueError("the views of a MultiViewRasterizer must share image size, bg, scale_modifier, "
+                                 "sh_degree and flags")
+        self.raster_settings = ss
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None, dc=None):
+        _check_inputs(shs, colors_precomp, scales, rotations, cov3D_precomp, dc)
+        absent = torch.Tensor([])
+        return rasterize_views(
+            means3D, means2D,
+            absent if shs is None else shs,
+            absent if colors_precomp is None else colors_precomp,
+            opacities,
+            absent if scales is None else scales,
+            absent if rotations is None else rotations,
+            absent if cov3D_precomp is None else cov3D_precomp,
+            self.raster_settings, dc)
 
 
 class SparseGaussianAdam(torch.optim.Adam):

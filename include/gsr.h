@@ -247,6 +247,30 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
                         float* dL_dcov3D, float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
                         bool antialiasing, bool debug, unsigned accumulate, gsr_stream_t stream);
 
+/* Backward of a batch of V <= 16 camera views rendered from the same Gaussians (each with its
+ * own gsr_forward* call and state buffers): per view BACKWARD::render (rasterizer_impl.cu:399-418),
+ * then ONE pass of BACKWARD::preprocess over the Gaussians that reads each Gaussian's parameters
+ * once, walks the V views' records and writes the parameter gradients summed over the views
+ * (the views' loss terms add up) -- instead of V passes that each read the 236 B/Gaussian of
+ * parameters and write (or accumulate) the 236 B/Gaussian of gradients.  Per-view arrays hold
+ * one device pointer per view (viewmatrices, projmatrices, campos, radii (may be NULL: the
+ * forward's internal copy), state buffers, dL_dpix, dL_invdepths (NULL: no invdepth term in
+ * any view), dL_dmean2D: each view's (P,3) screen-space gradient); R, tan_fovx and tan_fovy are
+ * host arrays.  dL_dcolor (may be NULL) and the parameter gradients are the sums over the views;
+ * `accumulate` as in gsr_backward_dc_acc.  Results equal the sum of V gsr_backward_dc calls up to
+ * fp32 summation order. */
+int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
+                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* const* viewmatrices,
+                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
+                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
+                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
+                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
+                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
+                       gsr_stream_t stream);
+
 /* Visibility-masked Adam step (the accelerated upstream's `_C.adamUpdate`, called
  * by SparseGaussianAdam.step(visibility, N) from train.py:180-183): for each of the
  * N Gaussians with visible[i] set, its M consecutive elements of param are updated
@@ -264,6 +288,11 @@ int gsr_adam_update_multi(int n_groups, float* const* params, const float* const
                           float* const* exp_avgs, float* const* exp_avg_sqs, const int* Ms,
                           const float* lrs, const float* epss, const bool* visible, float b1,
                           float b2, int N, gsr_stream_t stream);
+
+/* The forward's binning prefix (preprocess .. tile order) runs on an internal stream of the
+ * highest priority, forked from and joined back into the caller's stream (on = 1, the
+ * default); on = 0 puts every launch on the caller's stream.  Per host thread. */
+int gsr_set_prefix_stream(int on);
 
 /* Debug / parity helper: writes the sorted 64-bit tile|depth keys
  * (rasterizer_impl.cu:102-104 layout, after the sort of :306-311) and the

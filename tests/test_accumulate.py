@@ -98,3 +98,40 @@ def test_accumulate_argument_checks():
     plain = dgr._C.rasterize_gaussians_backward(*args)
     assert out[3] is None
     torch.testing.assert_close(dst, plain[3] + 1.0, rtol=0, atol=0)
+
+
+def test_views_on_two_streams_match_one_stream():
+    """bench.py's step: views alternate between two HIP streams (the forward of one view overlapping
+    the backward of the previous); in-place accumulation stays ordered (the backward's event
+    fence), so every gradient is bit-identical to the one-stream run."""
+    import diff_gaussian_rasterization as dgr
+    import synthetic
+    case = common.make_case(P=20000, H=270, W=480)
+    sc = {k: v.to(DEV).requires_grad_(True) for k, v in case["scene"].items()}
+    cams = [synthetic.Camera(480, 270, view=v) for v in range(6)]
+    grads = [tuple(t.to(DEV) for t in synthetic.make_grads(270, 480, seed=20 + v)) for v in range(6)]
+    main = torch.cuda.current_stream(DEV)
+    side = torch.cuda.Stream(DEV)
+
+    def run(n_streams):
+        for t in sc.values():
+            t.grad = None
+        streams = [main, side][:n_streams]
+        for st in streams[1:]:
+            st.wait_stream(main)
+        for i, (cam, (gc, gi)) in enumerate(zip(cams, grads)):
+            st = streams[i % n_streams]
+            with torch.cuda.stream(st):
+                means2D = torch.zeros_like(sc["means3D"], requires_grad=True)
+                with dgr.accumulate_grads_in_place():
+                    color, radii, inv = dgr.GaussianRasterizer(_settings(case, cam))(means2D=means2D, **sc)
+                torch.autograd.backward([color, inv], [gc, gi])
+        for st in streams[1:]:
+            main.wait_stream(st)
+        torch.cuda.synchronize()
+        return {k: t.grad.detach().cpu().numpy().copy() for k, t in sc.items()}
+
+    one = run(1)
+    two = run(2)
+    for k in one:
+        np.testing.assert_array_equal(two[k], one[k], err_msg=k)

@@ -1,0 +1,155 @@
+"""MultiViewRasterizer: a batch of views as one autograd node (needs an MI355X: -m gpu).
+
+* forward: every view's image, radii and inverse depth are bit-identical to GaussianRasterizer on
+  that view (the same kernels run per view);
+* backward (gsr_backward_views: every view's render backward, then ONE preprocess backward over
+  the Gaussians): each view's screen-space gradient (means2D.grad[v]) is bit-identical to the
+  single-view one; the parameter gradients equal the sum of the single-view gradients up to fp32
+  summation order (1e-5 of each tensor's max), and the sum of the C oracle's per-view gradients
+  within the common gradient tolerance -- for every input mode, with antialiasing, with dc= and
+  with in-place accumulation into existing .grad buffers.
+"""
+import numpy as np
+import pytest
+import torch
+
+import common
+import synthetic
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+V, P, H, W = 4, 4000, 144, 176
+
+
+def _settings(cam, antialiasing, bg):
+    import diff_gaussian_rasterization as dgr
+    return dgr.GaussianRasterizationSettings(
+        H, W, cam.tanfovx, cam.tanfovy, bg, 1.0, cam.world_view_transform.to(DEV), cam.full_proj_transform.to(DEV),
+        3, cam.camera_center.to(DEV), False, False, antialiasing)
+
+
+def _case():
+    case = common.make_case(P=P, H=H, W=W, bg=(0.1, 0.2, 0.3))
+    g = torch.Generator().manual_seed(7)
+    case["colors_precomp"] = torch.rand(P, 3, generator=g)
+    o, _ = common.run_oracle(case, backward=False)
+    case["cov3D_precomp"] = torch.from_numpy(o.get("cov3D").copy())
+    case["cams"] = [synthetic.Camera(W, H, view=v) for v in range(V)]
+    case["grads"] = [synthetic.make_grads(H, W, seed=30 + v) for v in range(V)]
+    return case
+
+
+def _leaves(case, mode):
+    sc = case["scene"]
+    t = {"means3D": sc["means3D"], "opacities": sc["opacities"]}
+    if mode == "dc":
+        t["dc"], t["shs"] = sc["shs"][:, :1].contiguous(), sc["shs"][:, 1:].contiguous()
+    elif mode.startswith("sh"):
+        t["shs"] = sc["shs"]
+    else:
+        t["colors_precomp"] = case["colors_precomp"]
+    if mode.endswith("cov"):
+        t["cov3D_precomp"] = case["cov3D_precomp"]
+    else:
+        t["scales"], t["rotations"] = sc["scales"], sc["rotations"]
+    return {k: v.to(DEV).clone().requires_grad_(True) for k, v in t.items()}
+
+
+@pytest.mark.parametrize("mode,antialiasing", [("sh_scales", False), ("sh_scales", True), ("colors_cov", False),
+                                               ("dc", False), ("dc", True)])
+def test_multiview_matches_single_views(mode, antialiasing):
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, antialiasing, bg) for c in case["cams"]]
+    gc = torch.stack([g[0] for g in case["grads"]]).to(DEV)
+    gi = torch.stack([g[1] for g in case["grads"]]).to(DEV)
+
+    # single views, gradients accumulated by autograd
+    single = _leaves(case, mode)
+    imgs, radii, invs, m2 = [], [], [], []
+    for v, s in enumerate(settings):
+        means2D = torch.zeros_like(single["means3D"], requires_grad=True)
+        c, r, i = dgr.GaussianRasterizer(s)(means2D=means2D, **single)
+        torch.autograd.backward([c, i], [gc[v], gi[v]])
+        imgs.append(c.detach())
+        radii.append(r)
+        invs.append(i.detach())
+        m2.append(means2D.grad)
+
+    multi = _leaves(case, mode)
+    means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+    c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **multi)
+    torch.autograd.backward([c, i], [gc, gi])
+    torch.cuda.synchronize()
+    assert torch.equal(c.detach(), torch.stack(imgs)) and torch.equal(i.detach(), torch.stack(invs))
+    assert torch.equal(r, torch.stack(radii))
+    assert torch.equal(means2D.grad, torch.stack(m2)), "screen-space gradients"
+    for k in single:
+        a, b = multi[k].grad.cpu().numpy(), single[k].grad.cpu().numpy()
+        ok, rel = common.allclose_rel(a, b, rtol=1e-5, atol=1e-9)
+        assert ok, f"{mode} aa={antialiasing}: d{k} multi vs sum of single views rel {rel:.3e}"
+
+
+def test_multiview_matches_oracle_sum():
+    """Parameter gradients of the batch against the sum of the C oracle's per-view gradients."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, False, bg) for c in case["cams"]]
+    ref = None
+    for v, cam in enumerate(case["cams"]):
+        cv = dict(case, cam=cam, grad_color=case["grads"][v][0], grad_invdepth=case["grads"][v][1])
+        _, og = common.run_oracle(cv, nthreads=8)
+        ref = og if ref is None else {k: ref[k] + og[k] for k in ref}
+    t = _leaves(case, "sh_scales")
+    means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+    c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **t)
+    torch.autograd.backward([c, i], [torch.stack([g[0] for g in case["grads"]]).to(DEV),
+                                     torch.stack([g[1] for g in case["grads"]]).to(DEV)])
+    torch.cuda.synchronize()
+    for hk, ok_ in {"means3D": "dL_dmeans3D", "shs": "dL_dsh", "opacities": "dL_dopacity", "scales": "dL_dscales",
+                    "rotations": "dL_drotations"}.items():
+        a = t[hk].grad.cpu().numpy()
+        ok, rel = common.allclose_rel(a, ref[ok_].reshape(a.shape))
+        assert ok, f"d{hk} vs oracle sum rel {rel:.3e}"
+
+
+def test_multiview_in_place_accumulation():
+    """A second batch into the same .grad (accumulate_grads_in_place) equals autograd's own add."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, False, bg) for c in case["cams"]]
+    gc = torch.stack([g[0] for g in case["grads"]]).to(DEV)
+    gi = torch.stack([g[1] for g in case["grads"]]).to(DEV)
+
+    def run(fused):
+        t = _leaves(case, "sh_scales")
+        for _ in range(2):
+            means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+            with dgr.accumulate_grads_in_place(fused):
+                c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **t)
+            torch.autograd.backward([c, i], [gc, gi])
+        torch.cuda.synchronize()
+        return {k: v.grad.cpu().numpy() for k, v in t.items()}
+
+    a, b = run(False), run(True)
+    for k in a:
+        np.testing.assert_array_equal(b[k], a[k], err_msg=k)
+
+
+def test_multiview_argument_checks():
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    s = [_settings(c, False, bg) for c in case["cams"]]
+    with pytest.raises(ValueError):
+        dgr.MultiViewRasterizer([s[0], s[1]._replace(antialiasing=True)])
+    with pytest.raises(ValueError):
+        dgr.MultiViewRasterizer(s * 5)
+    t = _leaves(case, "sh_scales")
+    with pytest.raises(Exception, match="excatly one"):
+        dgr.MultiViewRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros((V, P, 3), device=DEV),
+                                   opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
