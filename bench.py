@@ -4,7 +4,9 @@
 One step = one optimizer step's batch of camera views (BASELINE config 4): for each
 view this rank owns, forward + backward of the differentiable rasterizer through the drop-in
 surface (diff_gaussian_rasterization.GaussianRasterizer + autograd), gradients accumulated into
-the replicated Gaussian parameters; then, with N>1 ranks, ONE RCCL all_reduce(SUM) of the
+the replicated Gaussian parameters (by default inside dgr.deferred_backward: each view's render
+backward right after its forward, the views alternating over two HIP streams, and ONE batched
+preprocess backward for the step's views); then, with N>1 ranks, ONE RCCL all_reduce(SUM) of the
 236 B/Gaussian parameter-gradient bucket.  Every view is BASELINE config 2's workload (1M
 Gaussians, SH degree 3, one 1920x1080 ring view, fwd+bwd).
 
@@ -17,6 +19,7 @@ Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import contextlib
 import ctypes
 import glob
 import hashlib
@@ -71,14 +74,20 @@ def parse():
                     help="run the forward's binning prefix on the caller's stream, not the library's priority stream")
     ap.add_argument("--batch-views", action="store_true",
                     help="render this rank's views as one MultiViewRasterizer batch (one backward preprocess pass)")
+    ap.add_argument("--no-deferred", dest="deferred", action="store_false",
+                    help="every view's full backward on its own (default: per-view render backward, ONE batched "
+                         "preprocess backward per step, dgr.deferred_backward)")
     ap.add_argument("--no-fused-accumulation", action="store_true",
                     help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
     return ap.parse_args()
 
 
-def algorithmic_bytes(P, M, L, N, T, P_vis):
-    """Compulsory HBM bytes per launch of each kernel (split per kernel)."""
+def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1):
+    """Compulsory HBM bytes per launch of each kernel (split per kernel).
+    views_per_bwd: views whose preprocess backward one launch covers (deferred_backward batches a
+    step's views: the parameters are read and their gradients written once, the per-view radii and
+    render gradients V times)."""
     params = 4 * (11 + 3 * M)  # means 12 + scales 12 + rot 16 + opacity 4 + SH 12M
     return {
         # params in; key, radius, tile count, rect out per Gaussian; splat record 48 + conic 16 +
@@ -93,7 +102,8 @@ def algorithmic_bytes(P, M, L, N, T, P_vis):
         "tile_order": T * 12,                                   # per-tile work in, launch order out
         "render_fwd": L * 44 + N * 24 + T * 8,                  # id + 40 B record per instance; 24 B/pixel out
         "render_bwd": L * 44 + N * 24 + T * 8,                  # id + record per instance; 24 B/pixel in
-        "preprocess_bwd": P * (params + 4) + P_vis * 48 + P * (40 + 12 * M),  # params + 48 B/G render grads in
+        # params + radii + 48 B/G render grads in, parameter gradients out
+        "preprocess_bwd": P * params + views_per_bwd * (P * 4 + P_vis * 48) + P * (40 + 12 * M),
     }
 
 
@@ -233,6 +243,17 @@ def main():
         n_st = len(streams) if overlap else 1
         for st in streams[1:n_st]:
             st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
+        with (dgr.deferred_backward() if args.deferred else contextlib.nullcontext()):
+            views_loop(n_st)
+        if record_allreduce:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        nbytes = multiview.allreduce_grads(params)
+        if record_allreduce:
+            e1.record()
+            ar_events.append((e0, e1, nbytes))
+
+    def views_loop(n_st):
         for i, (s, (gc, gi)) in enumerate(zip(cams, grads)):
             st = streams[i % n_st]
             with torch.cuda.stream(st):
@@ -247,13 +268,6 @@ def main():
                 torch.autograd.backward([color, inv], [gc, gi])
         for st in streams[1:n_st]:
             main_stream.wait_stream(st)
-        if record_allreduce:
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        nbytes = multiview.allreduce_grads(params)
-        if record_allreduce:
-            e1.record()
-            ar_events.append((e0, e1, nbytes))
 
     if args.pmc_child:  # the workload of one --pmc pass (pmc_traffic): nothing printed, nothing timed
         for _ in range(args.warmup + args.steps):
@@ -280,10 +294,13 @@ def main():
     kern = {}
     if not args.no_profile:
         # one stream: every kernel's duration is its own, not shared with an overlapping view's
+        # (the library's internal binning streams off as well)
+        lib.gsr_set_prefix_stream(0)
         lib.gsr_profile_enable(1)
         for _ in range(args.steps):
             step(overlap=False)
         torch.cuda.synchronize()
+        lib.gsr_set_prefix_stream(0 if args.no_prefix_stream else 1)
         nk = 16
         tot = (ctypes.c_double * nk)()
         cnt = (ctypes.c_int * nk)()
@@ -328,7 +345,7 @@ def main():
 
     roofline = None
     if kern:
-        ab = algorithmic_bytes(P, M, L, N, T, P_vis)
+        ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if args.deferred else 1)
         dom = max(kern, key=lambda k: kern[k]["avg_ms"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
         sha = lib_sha256()
@@ -408,7 +425,10 @@ def main():
         "data": "synthetic (seed-0 Gaussian cloud, SURVEY.md §8d; ring camera views)",
         "config": {"workload": workload, "P": P, "width": W, "height": H, "views_per_step": views_step,
                    "views_per_rank": len(views), "num_rendered": L, "num_rendered_per_view": Ls,
-                   "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}"},
+                   "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}",
+                   "execution": ("views alternating over 2 HIP streams" if args.overlap else "views on one stream")
+                   + ("; per view forward + render backward, one batched preprocess backward per step "
+                      "(deferred_backward)" if args.deferred else "; per view forward + full backward")},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "aux": aux,

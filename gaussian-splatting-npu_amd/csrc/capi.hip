@@ -56,16 +56,19 @@ int fail_hip(hipError_t e, int line)
         }                                                                                     \
     } while (0)
 
-// Pinned, device-mapped host words of this host thread.  The forward's kernels store the
+// Pinned, device-mapped host words of this host thread, one 16-word slot per view of a
+// multi-view forward (slot 0 for a single view).  The forward's kernels store the
 // prefiltered-violation flag and num_rendered straight into them (system-scope stores), so the
 // forward needs neither a device memset nor a D2H copy before its one stream synchronisation.
-int pinned(uint32_t** out)
+constexpr int PINNED_SLOT_WORDS = 16;
+int pinned(int slot, uint32_t** out)
 {
     if (!g_pinned) {
-        hipError_t e = hipHostMalloc((void**)&g_pinned, 64, hipHostMallocMapped | hipHostMallocCoherent);
+        hipError_t e = hipHostMalloc((void**)&g_pinned, 4 * PINNED_SLOT_WORDS * MAX_VIEWS,
+                                     hipHostMallocMapped | hipHostMallocCoherent);
         if (e != hipSuccess) return fail_hip(e, __LINE__);
     }
-    *out = g_pinned;
+    *out = g_pinned + PINNED_SLOT_WORDS * slot;
     return GSR_OK;
 }
 
@@ -78,36 +81,45 @@ int pinned(uint32_t** out)
 // the other view's long kernels instead of behind them.  Buffers stay stream-ordered for the caller:
 // everything the prefix writes is joined into its stream before the entry point returns.
 // ---------------------------------------------------------------------------
+constexpr int PREFIX_STREAMS = 4;  // views whose binning prefixes run side by side (gsr_forward_views)
 struct PrefixStream {
-    hipStream_t s = nullptr;
+    hipStream_t s[PREFIX_STREAMS] = {};
     hipEvent_t fork = nullptr, join = nullptr;
 };
 constexpr int MAX_DEVICES = 64;
 thread_local PrefixStream g_prefix[MAX_DEVICES];
 thread_local bool g_prefix_off = false;  // gsr_set_prefix_stream(0): everything on the caller's stream
 
-int prefix_begin(hipStream_t caller, hipStream_t* out)
+// n (<= PREFIX_STREAMS) prefix streams of the current device, each forked from `caller`; all of
+// them the caller's own stream when the prefix streams are off (or the device is out of range).
+int prefix_fork(hipStream_t caller, int n, hipStream_t* out)
 {
-    *out = caller;
+    for (int k = 0; k < n; k++) out[k] = caller;
     if (g_prefix_off) return GSR_OK;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail_hip(e, __LINE__);
     if (dev < 0 || dev >= MAX_DEVICES) return GSR_OK;
     PrefixStream& ps = g_prefix[dev];
-    if (!ps.s) {
-        int least = 0, greatest = 0;
-        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return fail_hip(e, __LINE__);
-        if ((e = hipStreamCreateWithPriority(&ps.s, hipStreamNonBlocking, greatest)) != hipSuccess)
-            return fail_hip(e, __LINE__);
+    if (!ps.fork) {
         if ((e = hipEventCreateWithFlags(&ps.fork, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
         if ((e = hipEventCreateWithFlags(&ps.join, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
     }
     if ((e = hipEventRecord(ps.fork, caller)) != hipSuccess) return fail_hip(e, __LINE__);
-    if ((e = hipStreamWaitEvent(ps.s, ps.fork, 0)) != hipSuccess) return fail_hip(e, __LINE__);
-    *out = ps.s;
+    for (int k = 0; k < n; k++) {
+        if (!ps.s[k]) {
+            int least = 0, greatest = 0;
+            if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return fail_hip(e, __LINE__);
+            if ((e = hipStreamCreateWithPriority(&ps.s[k], hipStreamNonBlocking, greatest)) != hipSuccess)
+                return fail_hip(e, __LINE__);
+        }
+        if ((e = hipStreamWaitEvent(ps.s[k], ps.fork, 0)) != hipSuccess) return fail_hip(e, __LINE__);
+        out[k] = ps.s[k];
+    }
     return GSR_OK;
 }
+
+int prefix_begin(hipStream_t caller, hipStream_t* out) { return prefix_fork(caller, 1, out); }
 
 // the caller's stream waits for everything enqueued on the prefix stream so far
 int prefix_end(hipStream_t caller, hipStream_t prefix)
@@ -260,7 +272,7 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
                                    float scale_modifier, const float* rotations, const float* cov3D_precomp,
                                    const float* viewmatrix, const float* projmatrix, const float* cam_pos,
                                    float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
-                                   bool debug, gsr_stream_t stream, uint32_t** h_out)
+                                   bool debug, gsr_stream_t stream, uint32_t** h_out, int slot = 0)
 {
     hipStream_t s = (hipStream_t)stream;
     if (width <= 0 || height <= 0) return fail(GSR_ERR_INVALID, "image size must be positive");
@@ -278,9 +290,9 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     const GeomLayout g = geom_layout(P);
     char* gb = geometry_buffer;
     // h[0]: prefiltered violation (written by preprocess), h[2]: num_rendered (written by the scan).
-    // This thread's previous forward has synchronised its stream, so no kernel still writes them.
+    // This thread's previous forward has read its num_rendered back, so no kernel still writes them.
     uint32_t* h;
-    int rc = pinned(&h);
+    int rc = pinned(slot, &h);
     if (rc) return rc;
     h[0] = 0;
     __atomic_store_n(&h[2], L_PENDING, __ATOMIC_RELEASE);
@@ -590,6 +602,88 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     return GSR_OK;
 }
 
+int gsr_forward_views(int V, int P, int D, int M, const float* background, int width, int height,
+                      const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                      const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                      const float* cov3D_precomp, const float* const* viewmatrices, const float* const* projmatrices,
+                      const float* const* campos, const float* tan_fovx, const float* tan_fovy, bool prefiltered,
+                      bool antialiasing, char* const* geometry_buffers, char* const* image_buffers,
+                      char* const* binning_buffers, const size_t* binning_capacity, float* const* out_colors,
+                      float* const* out_invdepths, int* const* radii, bool debug, gsr_stream_t stream,
+                      int* num_rendered, int* rendered)
+{
+    if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
+    if (!viewmatrices || !projmatrices || !campos || !tan_fovx || !tan_fovy || !geometry_buffers || !image_buffers ||
+        !binning_buffers || !binning_capacity || !out_colors || !out_invdepths || !num_rendered || !rendered)
+        return fail(GSR_ERR_INVALID, "null per-view array");
+    for (int v = 0; v < V; v++) {
+        num_rendered[v] = 0;
+        rendered[v] = 0;
+    }
+    if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
+    hipStream_t caller = (hipStream_t)stream;
+    const int n = V < PREFIX_STREAMS ? V : PREFIX_STREAMS;
+    hipStream_t ps[PREFIX_STREAMS];
+    int rc = prefix_fork(caller, n, ps);
+    if (rc) return rc;
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+
+    // Prefix stream k carries views k, k + n, k + 2n, ...: each view's first half (preprocess, depth
+    // sort, scan, early emission), and after its num_rendered is read back its second half (tile
+    // sort, ranges, order), then the first half of the stream's next view.  Up to n views' short
+    // latency-bound launch chains are in flight side by side, and no view's tile sort queues
+    // behind a later view's preprocess.  The renders go to the caller's stream in view order.
+    uint32_t* h[MAX_VIEWS];
+    auto first_half = [&](int v) -> int {
+        char* gb = geometry_buffers[v];
+        char* ib = image_buffers[v];
+        if (!gb || !ib) return fail(GSR_ERR_ALLOC, "null state buffer");
+        if (!out_colors[v] || !out_invdepths[v]) return fail(GSR_ERR_INVALID, "null per-view output");
+        const hipStream_t s = ps[v % n];
+        const int r = forward_geometry_launch(gb, ib, P, D, M, width, height, means3D, dc, shs, colors_precomp,
+                                              opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                              viewmatrices[v], projmatrices[v], campos[v], tan_fovx[v], tan_fovy[v],
+                                              prefiltered, antialiasing, radii ? radii[v] : nullptr, debug, s, &h[v], v);
+        if (r) return r;
+        if (binning_buffers[v] && binning_capacity[v] > 0) {
+            ProfScope ps_(PK_EMIT, s);
+            HIP_TRY(launch_emit_instances_early(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
+                                                at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
+                                                at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx,
+                                                at<uint32_t>(gb, g.off[GEOM_EMIT_START]), binning_buffers[v],
+                                                binning_capacity[v], at<uint2>(ib, im.off[IMG_RANGES]),
+                                                (int)(gx * gy), s));
+        }
+        return GSR_OK;
+    };
+    for (int v = 0; v < n && !rc; v++) rc = first_half(v);
+    for (int v = 0; v < V && !rc; v++) {
+        const hipStream_t s = ps[v % n];
+        int L = 0;
+        rc = forward_geometry_wait(h[v], s, &L);
+        num_rendered[v] = L;
+        if (rc) break;
+        // views whose binning buffer is too small are left to the caller (allocate
+        // gsr_binning_buffer_size(num_rendered[v]), then gsr_forward_render)
+        const bool early = binning_buffers[v] && binning_capacity[v] > 0;
+        if (early && gsr_binning_buffer_size(L) <= binning_capacity[v]) {
+            rc = forward_render_impl(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L, background,
+                                     width, height, out_colors[v], out_invdepths[v], debug, stream, L > 0, s);
+            if (rc) break;
+            rendered[v] = 1;
+        }
+        if (v + n < V) rc = first_half(v + n);
+    }
+    for (int k = 0; k < n; k++) {  // everything the prefix streams wrote is ordered before the caller's next work
+        const int rj = prefix_end(caller, ps[k]);
+        if (!rc) rc = rj;
+    }
+    return rc;
+}
+
 int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int width, int height,
                         const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                         const float* opacities, const float* scales, float scale_modifier, const float* rotations,
@@ -702,17 +796,64 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
                                dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug, 0u, stream);
 }
 
-int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
-                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
-                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
-                       const float* cov3D_precomp, const float* const* viewmatrices,
-                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
-                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
-                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
-                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
-                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
-                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
-                       gsr_stream_t stream)
+int gsr_backward_render(int P, int R, const float* background, int width, int height, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, const float* dL_invdepths,
+                        bool debug, gsr_stream_t stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (P < 0 || R < 0) return fail(GSR_ERR_INVALID, "P and R must be >= 0");
+    if (P == 0 || R == 0) return GSR_OK;
+    if (!geom_buffer || !image_buffer || !binning_buffer) return fail(GSR_ERR_ALLOC, "null state buffer");
+    if (!dL_dpix) return fail(GSR_ERR_INVALID, "null dL_dpix");
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const BinLayout b = bin_layout(R);
+    char* gb = geom_buffer;
+    char* ib = image_buffer;
+    char* bb = binning_buffer;
+    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const int T = (int)(gx * gy);
+    // BACKWARD::render (rasterizer_impl.cu:399-418): per-(tile, Gaussian) gradient records
+    RenderBwdArgs r;
+    r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
+    r.W = width; r.H = height; r.grid_x = gx;
+    r.bg = background;
+    r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
+    r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
+    r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
+    r.dL_dpixels = dL_dpix;
+    r.dL_invdepths = dL_invdepths;
+    r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);
+    r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
+    r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
+    {
+        ProfScope ps_(PK_TILE_ORDER, s);
+        HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,
+                                  at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
+    }
+    {
+        ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emit_instances
+        HIP_TRY(launch_render_bwd(r, T, s));
+    }
+    DEBUG_SYNC(s);
+    return GSR_OK;
+}
+
+int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int width, int height,
+                                  const float* means3D, const float* dc, const float* shs,
+                                  const float* colors_precomp, const float* opacities, const float* scales,
+                                  float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                  const float* const* viewmatrices, const float* const* projmatrices,
+                                  const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                  const int* const* radii, char* const* geom_buffers, char* const* binning_buffers,
+                                  bool has_invdepth, float* const* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                                  float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                                  float* dL_dscale, float* dL_drot, bool antialiasing, bool debug,
+                                  unsigned accumulate, gsr_stream_t stream)
 {
     if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
     if (accumulate & ~(unsigned)GSR_ACC_ALL) return fail(GSR_ERR_INVALID, "unknown accumulate bits");
@@ -721,16 +862,11 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
     if (dc && M > 0 && (!shs || !dL_dsh)) return fail(GSR_ERR_INVALID, "dc given with M > 0 but shs/dL_dsh NULL");
     if (!R || !viewmatrices || !projmatrices || !campos || !tan_fovx || !tan_fovy || !geom_buffers ||
-        !binning_buffers || !image_buffers || !dL_dpix || !dL_dmean2D)
+        !binning_buffers || !dL_dmean2D)
         return fail(GSR_ERR_INVALID, "null per-view array");
-    const bool has_inv = dL_invdepths != nullptr;
     hipStream_t s = (hipStream_t)stream;
     if (P <= 0) return GSR_OK;
     const GeomLayout g = geom_layout(P);
-    const ImageLayout im = image_layout(width, height);
-    const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
-    const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
-    const int T = (int)(gx * gy);
 
     PreprocessBwdViewsArgs A;
     PreprocessBwdArgs& p = A.a;
@@ -743,7 +879,9 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
     p.focal_x = p.focal_y = p.tan_fovx = p.tan_fovy = 0.f;
     p.antialiasing = antialiasing;
     p.grad_inst = nullptr; p.valid = nullptr; p.emit_start = nullptr; p.tiles_touched = nullptr;
-    p.has_invdepth = has_inv;
+    // a view rendered without an inverse-depth gradient has zero invdepth fields in its records:
+    // subtracting their (zero) term leaves its gradients bit-identical
+    p.has_invdepth = has_invdepth;
     p.conic_opacity = nullptr;
     p.W = width; p.H = height;
     p.dL_dmean2D = nullptr; p.dL_dconic = nullptr; p.dL_dinvdepth = nullptr;
@@ -754,41 +892,11 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
     A.V = V;
     for (int v = 0; v < V; v++) {
         char* gb = geom_buffers[v];
-        char* ib = image_buffers[v];
         char* bb = binning_buffers[v];
         const int L = R[v];
-        if (!gb || !ib || (L > 0 && !bb)) return fail(GSR_ERR_ALLOC, "null state buffer");
-        if (!dL_dpix[v] || !dL_dmean2D[v] || (has_inv && !dL_invdepths[v]))
-            return fail(GSR_ERR_INVALID, "null per-view gradient");
+        if (!gb || (L > 0 && !bb)) return fail(GSR_ERR_ALLOC, "null state buffer");
+        if (!dL_dmean2D[v]) return fail(GSR_ERR_INVALID, "null per-view gradient");
         const BinLayout b = bin_layout(L);
-        // BACKWARD::render of view v (rasterizer_impl.cu:399-418): its per-(tile, Gaussian) records
-        if (L > 0) {
-            RenderBwdArgs r;
-            r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
-            r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
-            r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
-            r.W = width; r.H = height; r.grid_x = gx;
-            r.bg = background;
-            r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
-            r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
-            r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
-            r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
-            r.dL_dpixels = dL_dpix[v];
-            r.dL_invdepths = has_inv ? dL_invdepths[v] : nullptr;
-            r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);
-            r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
-            r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
-            {
-                ProfScope ps_(PK_TILE_ORDER, s);
-                HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,
-                                          at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
-            }
-            {
-                ProfScope ps_(PK_RENDER_BWD, s);
-                HIP_TRY(launch_render_bwd(r, T, s));
-            }
-            DEBUG_SYNC(s);
-        }
         BwdView& bv = A.v[v];
         bv.view = viewmatrices[v];
         bv.proj = projmatrices[v];
@@ -806,13 +914,45 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
         bv.valid = L > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
         bv.dL_dmean2D = dL_dmean2D[v];
     }
-    // BACKWARD::preprocess of the whole batch: one pass over the Gaussians
+    // BACKWARD::preprocess (rasterizer_impl.cu:423-449) of the whole batch: one pass over the Gaussians
     {
         ProfScope ps_(PK_PREPROCESS_BWD, s);
         HIP_TRY(launch_preprocess_bwd_views(A, s));
     }
     DEBUG_SYNC(s);
     return GSR_OK;
+}
+
+int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
+                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* const* viewmatrices,
+                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
+                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
+                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
+                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
+                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
+                       gsr_stream_t stream)
+{
+    if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
+    if (!R || !geom_buffers || !binning_buffers || !image_buffers || !dL_dpix)
+        return fail(GSR_ERR_INVALID, "null per-view array");
+    const bool has_inv = dL_invdepths != nullptr;
+    if (P <= 0) return GSR_OK;
+    for (int v = 0; v < V; v++) {  // BACKWARD::render of every view: its per-(tile, Gaussian) records
+        if (!dL_dpix[v] || (has_inv && !dL_invdepths[v])) return fail(GSR_ERR_INVALID, "null per-view gradient");
+        const int rc = gsr_backward_render(P, R[v], background, width, height, geom_buffers[v], binning_buffers[v],
+                                           image_buffers[v], dL_dpix[v], has_inv ? dL_invdepths[v] : nullptr, debug,
+                                           stream);
+        if (rc) return rc;
+    }
+    return gsr_backward_preprocess_views(V, P, D, M, R, width, height, means3D, dc, shs, colors_precomp, opacities,
+                                         scales, scale_modifier, rotations, cov3D_precomp, viewmatrices,
+                                         projmatrices, campos, tan_fovx, tan_fovy, radii, geom_buffers,
+                                         binning_buffers, has_inv, dL_dmean2D, dL_dcolor, dL_dopacity, dL_dmean3D,
+                                         dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug,
+                                         accumulate, stream);
 }
 
 // ---- the non-dc entry points: the reference's Rasterizer API (rasterizer.h:31-90) ----
@@ -951,7 +1091,7 @@ int gsr_knn_dist2(int P, const float* points, float* dist2_out, void* workspace,
     if (P == 0) return GSR_OK;
     if (!points || !dist2_out || !workspace) return fail(GSR_ERR_INVALID, "null pointer");
     uint32_t* h;
-    int rc = pinned(&h);
+    int rc = pinned(0, &h);
     if (rc) return rc;
     HIP_TRY(knn_dist2(P, points, dist2_out, static_cast<char*>(workspace), h + 8, (hipStream_t)stream));
     return GSR_OK;

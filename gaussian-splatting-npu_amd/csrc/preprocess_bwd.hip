@@ -41,7 +41,8 @@ constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +
 // (emission order); entries that contributed to no pixel were never written (their bit in the valid
 // mask is 0) and are not read (most slots: records are sparse).  The mask has one bit per slot
 // (L/8 bytes: it stays in L2), so a Gaussian's flags are one or two words; its flagged records are
-// then read REC_BATCH at a time in slot order (bitwise reproducible sums).
+// then read B at a time in slot order (bitwise reproducible sums).
+template <int B = REC_BATCH>
 __device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
                                                const uint32_t* valid, const float* grad_inst, int idx,
                                                float (&g)[GF_NUM])
@@ -55,17 +56,17 @@ __device__ __forceinline__ void gather_records(const uint32_t* emit_start, const
         if (w0 < e0) bits &= ~0u << (e0 - w0);
         if (e1 - w0 < 32u) bits &= (1u << (e1 - w0)) - 1u;
         while (bits) {
-            bool v[REC_BATCH];
-            uint32_t sl[REC_BATCH];
+            bool v[B];
+            uint32_t sl[B];
 #pragma unroll
-            for (int k = 0; k < REC_BATCH; k++) {
+            for (int k = 0; k < B; k++) {
                 v[k] = bits != 0u;
                 sl[k] = w0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
                 bits &= bits - 1u;
             }
-            float4 r[REC_BATCH][3];
+            float4 r[B][3];
 #pragma unroll
-            for (int k = 0; k < REC_BATCH; k++) {
+            for (int k = 0; k < B; k++) {
                 if (v[k]) {
                     const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
                     r[k][0] = rec[0];
@@ -74,7 +75,7 @@ __device__ __forceinline__ void gather_records(const uint32_t* emit_start, const
                 }
             }
 #pragma unroll
-            for (int k = 0; k < REC_BATCH; k++) {
+            for (int k = 0; k < B; k++) {
                 if (v[k]) {
                     g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
                     g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
@@ -332,26 +333,29 @@ __device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const View
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     const float(*Tm)[3] = T.m;
     float* dcov = o.dcov;
-    if (denom2inv != 0) {
-        dL_dc_xx += denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
-                                 (denom - c_xx * c_yy) * dL_dconic.z);
-        dL_dc_yy += denom2inv * (-c_xx * c_xx * dL_dconic.z + 2 * c_xx * c_xy * dL_dconic.y +
-                                 (denom - c_xx * c_yy) * dL_dconic.x);
-        dL_dc_xy += denom2inv * 2 *
-                    (c_xy * c_yy * dL_dconic.x - (denom + 2 * c_xy * c_xy) * dL_dconic.y + c_xx * c_xy * dL_dconic.z);
-        dcov[0] = (Tm[0][0] * Tm[0][0] * dL_dc_xx + Tm[0][0] * Tm[1][0] * dL_dc_xy + Tm[1][0] * Tm[1][0] * dL_dc_yy);
-        dcov[3] = (Tm[0][1] * Tm[0][1] * dL_dc_xx + Tm[0][1] * Tm[1][1] * dL_dc_xy + Tm[1][1] * Tm[1][1] * dL_dc_yy);
-        dcov[5] = (Tm[0][2] * Tm[0][2] * dL_dc_xx + Tm[0][2] * Tm[1][2] * dL_dc_xy + Tm[1][2] * Tm[1][2] * dL_dc_yy);
-        dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_dc_xx + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_dc_xy +
-                  2 * Tm[1][0] * Tm[1][1] * dL_dc_yy;
-        dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_dc_xx + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_dc_xy +
-                  2 * Tm[1][0] * Tm[1][2] * dL_dc_yy;
-        dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_dc_xx + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_dc_xy +
-                  2 * Tm[1][1] * Tm[1][2] * dL_dc_yy;
-    } else {
+    // denom2inv == 0 (backward.cu:230-283): no conic terms and dL/dcov3D = 0 -- as selects, not a
+    // branch (a divergent branch here made the compiler spill dcov to scratch)
+    const bool nz = denom2inv != 0;
+    dL_dc_xx += nz ? denom2inv * (-c_yy * c_yy * dL_dconic.x + 2 * c_xy * c_yy * dL_dconic.y +
+                                  (denom - c_xx * c_yy) * dL_dconic.z)
+                   : 0.f;
+    dL_dc_yy += nz ? denom2inv * (-c_xx * c_xx * dL_dconic.z + 2 * c_xx * c_xy * dL_dconic.y +
+                                  (denom - c_xx * c_yy) * dL_dconic.x)
+                   : 0.f;
+    dL_dc_xy += nz ? denom2inv * 2 *
+                         (c_xy * c_yy * dL_dconic.x - (denom + 2 * c_xy * c_xy) * dL_dconic.y + c_xx * c_xy * dL_dconic.z)
+                   : 0.f;
+    dcov[0] = (Tm[0][0] * Tm[0][0] * dL_dc_xx + Tm[0][0] * Tm[1][0] * dL_dc_xy + Tm[1][0] * Tm[1][0] * dL_dc_yy);
+    dcov[3] = (Tm[0][1] * Tm[0][1] * dL_dc_xx + Tm[0][1] * Tm[1][1] * dL_dc_xy + Tm[1][1] * Tm[1][1] * dL_dc_yy);
+    dcov[5] = (Tm[0][2] * Tm[0][2] * dL_dc_xx + Tm[0][2] * Tm[1][2] * dL_dc_xy + Tm[1][2] * Tm[1][2] * dL_dc_yy);
+    dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_dc_xx + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_dc_xy +
+              2 * Tm[1][0] * Tm[1][1] * dL_dc_yy;
+    dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_dc_xx + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_dc_xy +
+              2 * Tm[1][0] * Tm[1][2] * dL_dc_yy;
+    dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_dc_xx + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_dc_xy +
+              2 * Tm[1][1] * Tm[1][2] * dL_dc_yy;
 #pragma unroll
-        for (int k = 0; k < 6; k++) dcov[k] = 0;
-    }
+    for (int k = 0; k < 6; k++) dcov[k] = nz ? dcov[k] : 0.f;
     const float(*V)[3] = Vrk.m;
     const float dL_dT00 = 2 * (Tm[0][0] * V[0][0] + Tm[0][1] * V[0][1] + Tm[0][2] * V[0][2]) * dL_dc_xx +
                           (Tm[1][0] * V[0][0] + Tm[1][1] * V[0][1] + Tm[1][2] * V[0][2]) * dL_dc_xy;
@@ -565,162 +569,180 @@ __device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, co
 constexpr int SH_STRIDE = 49;  // LDS dwords per row (odd)
 
 // ---- multi-view batch (gsr_backward_views) ------------------------------------------------
-// One thread per Gaussian reads its parameters and SH row once and walks the V views of the batch:
-// per view the records, the 2D chain rule (view_grad), the screen-space gradient of that view and
-// the SH terms of that view's direction; dL/dcov3D, dL/dmean3D, dL/dopacity, dL/dcolor and dL/dsh
-// are summed over the views in registers, and scale / rotation are differentiated once from the
-// summed dL/dcov3D (linear in it).  The parameters (236 B per Gaussian at degree 3) are read and
-// their gradients written once per batch instead of once per view.
+// LPG lanes per Gaussian (the next power of two >= V), lane v of a group working on view v: its
+// records, the 2D chain rule (view_grad), that view's screen-space gradient and the SH terms of
+// that view's direction.  The per-view contributions to dL/dcov3D, dL/dmean3D, dL/dopacity,
+// dL/dcolor and dL/dsh are summed over the group's lanes with DPP butterflies (a fixed tree: the
+// sums are identical in every lane and reproducible), and scale / rotation are differentiated once
+// from the summed dL/dcov3D (linear in it).  The parameters (236 B per Gaussian at degree 3) are
+// read and their gradients written once per batch instead of once per view, and the V views'
+// dependent gathers (records) are in flight side by side instead of one after another.
 __device__ __forceinline__ ViewCam cam_of(const BwdView& v)
 {
     return {v.view, v.proj, v.campos, v.focal_x, v.focal_y, v.tan_fovx, v.tan_fovy};
 }
 
-// c0: SH coefficient 0 (3 floats), cr: coefficient k >= 1 at cr[3 (k - 1)]; d0 / dr the same for
-// dL/dsh (may alias c0 / cr: every coefficient is read before any is written), kw the number of
-// coefficients to write (zeros from the first unused one); acc: add to d0 / dr.
-__device__ __forceinline__ void bwd_views(const PreprocessBwdViewsArgs& A, int idx, const BwdIn& in, const float* c0,
-                                          const float* cr, float* d0, float* dr, int kw, bool acc_dc, bool acc_sh)
+// x from another lane of its DPP row (CTRL: a dpp_ctrl code)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float x)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+
+// x summed over the LPG consecutive lanes of this lane's group (LPG <= 16: within one DPP row).
+// Every lane of the group must be active.
+template <int LPG>
+__device__ __forceinline__ float group_sum(float x)
+{
+    if constexpr (LPG >= 2) x += dpp_mov<0xB1>(x);   // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (LPG >= 4) x += dpp_mov<0x4E>(x);   // quad_perm [2,3,0,1]: lane ^ 2
+    if constexpr (LPG >= 8) x += dpp_mov<0x141>(x);  // row_half_mirror: the other quad of 8 lanes
+    if constexpr (LPG >= 16) x += dpp_mov<0x140>(x); // row_mirror: the other half of the row
+    return x;
+}
+
+// records in flight per lane: the V lanes of a Gaussian already gather side by side
+#ifndef GSR_VIEW_REC_BATCH
+#define GSR_VIEW_REC_BATCH 4
+#endif
+constexpr int VIEW_REC_BATCH = GSR_VIEW_REC_BATCH;
+
+// One lane's share of a Gaussian of the batch.  c0: SH coefficient 0 (3 floats), cr: coefficient
+// k >= 1 at cr[3 (k - 1)]; d0 / dr the same for dL/dsh (may alias c0 / cr: every lane of the group
+// reads coefficient k before its sum is written), kw the number of coefficients to write (zeros from
+// the first unused one); acc: add to d0 / dr.  `live`: the lane's Gaussian exists (lanes past P
+// run the same code on a clamped index, write nothing, and keep every lane in the reductions).
+template <int LPG>
+__device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A, int idx, bool live, int v,
+                                                const BwdIn& in, const float* c0, const float* cr, float* d0,
+                                                float* dr, int kw, bool acc_dc, bool acc_sh)
 {
     const PreprocessBwdArgs& a = A.a;
     const size_t i = (size_t)idx;
+    const bool has_view = live && v < A.V;
+    const BwdView& bv = A.v[v < A.V ? v : 0];
+    bool vis = false;
+    float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
+    uint8_t cl = 0;
+    float gs[GF_NUM];
+    if (has_view) {
+        vis = bv.radii[idx] > 0;
+        co = bv.conic_opacity[idx];
+        cl = bv.clamped[idx];
+    }
+    if (vis) {
+        gather_records<VIEW_REC_BATCH>(bv.emit_start, bv.tiles_touched, bv.valid, bv.grad_inst, idx, gs);
+    } else {
+#pragma unroll
+        for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
+    }
     float cov3D[6];
     cov3d_of(a, in, cov3D);
-    const int nc = sh_ncoef(a);
-    float dsh[16][3];
+    ViewGrad o;
+    if (vis) {
+        view_grad(a, cam_of(bv), gs, co, cl, in.mean, in.opacity, cov3D, o);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 16; k++) dsh[k][0] = dsh[k][1] = dsh[k][2] = 0.f;
-    float dop = 0.f, dcol[3] = {0.f, 0.f, 0.f}, dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dm[3] = {0.f, 0.f, 0.f};
-    for (int v = 0; v < A.V; v++) {
-        const BwdView& bv = A.v[v];
+        for (int q = 0; q < GF_NUM; q++) o.g[q] = 0.f;
+        o.dopacity = 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) o.dcov[k] = 0.f;
+        o.dmx = o.dmy = o.dmz = 0.f;
+        o.dir_orig = {1.f, 0.f, 0.f};
+        o.x = o.y = o.z = 0.f;
+        o.dRGB[0] = o.dRGB[1] = o.dRGB[2] = 0.f;
+    }
+    if (has_view) {
         float* m2 = bv.dL_dmean2D + 3 * i;
-        if (!(bv.radii[idx] > 0)) {
-            m2[0] = 0.f; m2[1] = 0.f; m2[2] = 0.f;
-            continue;
-        }
-        float gs[GF_NUM];
-        gather_records(bv.emit_start, bv.tiles_touched, bv.valid, bv.grad_inst, idx, gs);
-        ViewGrad o;
-        view_grad(a, cam_of(bv), gs, bv.conic_opacity[idx], bv.clamped[idx], in.mean, in.opacity, cov3D, o);
         m2[0] = o.g[GF_MEAN2D_X]; m2[1] = o.g[GF_MEAN2D_Y]; m2[2] = 0.f;
-        dop += o.dopacity;
+    }
+    const bool writer = live && v == 0;
+    {
+        const float dop = group_sum<LPG>(o.dopacity);
+        if (writer) put(a.dL_dopacity + i, dop, a.acc & ACC_OPACITY, in.old_opacity);
+    }
+    {
+        float dcol[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) dcol[c] += o.g[GF_COLOR_R + c];
+        for (int c = 0; c < 3; c++) dcol[c] = group_sum<LPG>(o.g[GF_COLOR_R + c]);
+        if (writer && a.dL_dcolor) {
+            const bool acc = a.acc & ACC_COLORS;
 #pragma unroll
-        for (int k = 0; k < 6; k++) dcov[k] += o.dcov[k];
-        dm[0] += o.dmx;
-        dm[1] += o.dmy;
-        dm[2] += o.dmz;
-        if (nc > 0) {  // computeColorFromSH backward (backward.cu:51-141) for this view's direction
-            float ddir[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-            for (int k = 0; k < 16; k++) {
-                if (k < nc) {
-                    float b, gx, gy, gz;
-                    sh_term(k, o.x, o.y, o.z, b, gx, gy, gz);
-                    const float* shk = k == 0 ? c0 : cr + 3 * (k - 1);
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        const float t = shk[c] * o.dRGB[c];
-                        dsh[k][c] += b * o.dRGB[c];
-                        ddir[0] += t * gx;
-                        ddir[1] += t * gy;
-                        ddir[2] += t * gz;
-                    }
-                }
-            }
-            if (nc > 1) {  // degree 0 has no direction dependence
-                const f3 dn = dnormvdv(o.dir_orig, {ddir[0], ddir[1], ddir[2]});
-                dm[0] += dn.x;
-                dm[1] += dn.y;
-                dm[2] += dn.z;
-            }
+            for (int c = 0; c < 3; c++) put(a.dL_dcolor + 3 * i + c, dcol[c], acc);
         }
     }
-    put(a.dL_dopacity + i, dop, a.acc & ACC_OPACITY, in.old_opacity);
-    if (a.dL_dcolor) {
-        const bool acc = a.acc & ACC_COLORS;
+    {
+        float dcov[6];
 #pragma unroll
-        for (int c = 0; c < 3; c++) put(a.dL_dcolor + 3 * i + c, dcol[c], acc);
+        for (int k = 0; k < 6; k++) dcov[k] = group_sum<LPG>(o.dcov[k]);
+        if (writer) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) put(a.dL_dcov3D + 6 * i + k, dcov[k], a.acc & ACC_COV3D);
+            put_scale_rot(a, idx, in, dcov);
+        }
     }
+    float dm[3] = {o.dmx, o.dmy, o.dmz};
+    const int nc = sh_ncoef(a);
+    if (nc > 0) {  // computeColorFromSH backward (backward.cu:51-141) for this lane's view direction
+        float ddir[3] = {0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < 6; k++) put(a.dL_dcov3D + 6 * i + k, dcov[k], a.acc & ACC_COV3D);
-    put_scale_rot(a, idx, in, dcov);
-    const bool acc_m = a.acc & ACC_MEANS3D;
-    float* dmean = a.dL_dmean3D + 3 * i;
-    put(dmean, dm[0], acc_m, in.old_mean[0]);
-    put(dmean + 1, dm[1], acc_m, in.old_mean[1]);
-    put(dmean + 2, dm[2], acc_m, in.old_mean[2]);
-    if (d0) {
+        for (int k = 0; k < 16; k++) {
+            const bool mine = live && (k % LPG) == v;  // the lane that writes coefficient k
+            if (k < nc) {
+                float b, gx, gy, gz;
+                sh_term(k, o.x, o.y, o.z, b, gx, gy, gz);
+                const float* shk = k == 0 ? c0 : cr + 3 * (k - 1);
+                float* dk = k == 0 ? d0 : (dr ? dr + 3 * (k - 1) : nullptr);
+                const bool acc = k == 0 ? acc_dc : acc_sh;
+                float sum[3];
 #pragma unroll
-        for (int c = 0; c < 3; c++) put(d0 + c, dsh[0][c], acc_dc);
-    }
-    if (dr) {
+                for (int c = 0; c < 3; c++) {
+                    const float t = shk[c] * o.dRGB[c];
+                    sum[c] = group_sum<LPG>(b * o.dRGB[c]);
+                    ddir[0] += t * gx;
+                    ddir[1] += t * gy;
+                    ddir[2] += t * gz;
+                }
+                if (mine && dk) {
 #pragma unroll
-        for (int k = 1; k < 16; k++)
-            if (k < kw) {
+                    for (int c = 0; c < 3; c++) put(dk + c, sum[c], acc);
+                }
+            } else if (k < kw && mine && k > 0 && dr && !acc_sh) {
 #pragma unroll
-                for (int c = 0; c < 3; c++) put(dr + 3 * (k - 1) + c, dsh[k][c], acc_sh);
+                for (int c = 0; c < 3; c++) dr[3 * (k - 1) + c] = 0.f;
             }
+        }
+        if (vis && nc > 1) {  // degree 0 has no direction dependence
+            const f3 dn = dnormvdv(o.dir_orig, {ddir[0], ddir[1], ddir[2]});
+            dm[0] += dn.x;
+            dm[1] += dn.y;
+            dm[2] += dn.z;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) dm[c] = group_sum<LPG>(dm[c]);
+    if (writer) {
+        const bool acc_m = a.acc & ACC_MEANS3D;
+        float* dmean = a.dL_dmean3D + 3 * i;
+        put(dmean, dm[0], acc_m, in.old_mean[0]);
+        put(dmean + 1, dm[1], acc_m, in.old_mean[1]);
+        put(dmean + 2, dm[2], acc_m, in.old_mean[2]);
     }
 }
 
-// STAGED: the SH rows of the workgroup's 256 Gaussians go through LDS (see below); MULTI: the
-// multi-view batch (A.V views), else the single view of A.a.
-template <bool STAGED, bool MULTI>
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwdViewsArgs A)
+// The SH rows of a workgroup's n Gaussians (from `base`, at most ROWS) staged through LDS: read
+// with coalesced 16-byte loads, work(c0, cr, kw) runs on row r in place, and the rows leave the
+// same way (see SH_STRIDE).  Every thread of the workgroup must call this.
+template <int ROWS, class Work>
+__device__ __forceinline__ void staged_sh(const PreprocessBwdArgs& a, float* s_sh, int base, int n, int r, Work work)
 {
-    extern __shared__ __attribute__((aligned(16))) float s_sh[];
-    const PreprocessBwdArgs& a = A.a;
-    const int base = blockIdx.x * 256;
-    const int idx = base + (int)threadIdx.x;
-    BwdIn in;
-    BwdState st;
-    if (idx < a.P) bwd_gather(a, idx, in, !MULTI);  // in flight during the SH staging below
-    // one Gaussian's work on its SH row (coefficient 0 at c0, k >= 1 at cr[3 (k - 1)]), in place
-    auto work = [&](float* c0, float* cr, int kw) {
-        if constexpr (MULTI) {
-            bwd_views(A, idx, in, c0, cr, c0, cr, kw, false, false);
-        } else {
-            bwd_core(a, idx, in, st);
-            sh_bwd_range<0, 1>(st, c0, c0);
-            sh_bwd_range<1, 16>(st, cr, cr, kw);
-            bwd_finish(a, idx, st);
-        }
-    };
-    if (!STAGED) {
-        if (idx < a.P) {
-            const size_t w3 = (size_t)a.M * 3;
-            if constexpr (MULTI) {
-                const float* row = a.shs ? a.shs + idx * w3 : nullptr;
-                float* drow = (a.shs && a.dL_dsh) ? a.dL_dsh + idx * w3 : nullptr;
-                bwd_views(A, idx, in, row, row ? row + 3 : nullptr, drow, drow ? drow + 3 : nullptr, a.M,
-                          a.acc & ACC_SH, a.acc & ACC_SH);
-                if (a.dL_dsh && !(a.acc & ACC_SH))
-                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) a.dL_dsh[idx * w3 + k] = 0.f;
-            } else {
-                bwd_core(a, idx, in, st);
-                if (a.dL_dsh) {
-                    float* dsh = a.dL_dsh + idx * w3;
-                    // ncoef <= M: no read past the row; no write past it either (M < 16)
-                    const bool acc = a.acc & ACC_SH;
-                    if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
-                    if (!acc)
-                        for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
-                }
-                bwd_finish(a, idx, st);
-            }
-        }
-        return;
-    }
-    const int n = min(256, a.P - base);
     if (a.dc && a.M <= 16) {  // separate dc (train.py's sparse-Adam layout), verbatim rows (see preprocess.hip)
         const int wr = (a.M - 1) * 3;
-        float* s_rest = s_sh + 768;
+        float* s_rest = s_sh + 3 * ROWS;
         lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
         if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
         __syncthreads();
-        if (idx < a.P) work(s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x, a.M);
+        work(s_sh + 3 * r, s_rest + wr * r, a.M);
         __syncthreads();
         lds_copy_out(a.dL_ddc + (size_t)base * 3, s_sh, n * 3, a.acc & ACC_DC);
         if (wr > 0) lds_copy_out(a.dL_dsh + (size_t)base * wr, s_rest, n * wr, a.acc & ACC_SH);
@@ -731,8 +753,8 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwd
         lds_rows_in(s_sh, SH_STRIDE, 0, 48, a.dc + (size_t)base * 3, 3, n);
         if (a.shs && wr > 0) lds_rows_in(s_sh, SH_STRIDE, 3, 48, a.shs + (size_t)base * wr, wr, n);
         __syncthreads();
-        float* row = s_sh + threadIdx.x * SH_STRIDE;
-        if (idx < a.P) work(row, row + 3, 16);
+        float* row = s_sh + r * SH_STRIDE;
+        work(row, row + 3, 16);
         __syncthreads();
         lds_rows_out(a.dL_ddc + (size_t)base * 3, 3, n, s_sh, SH_STRIDE, 0, 48, a.acc & ACC_DC);
         if (a.dL_dsh && wr > 0)
@@ -740,15 +762,15 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwd
         return;
     }
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
-    for (int f = threadIdx.x; f < n * 12; f += 256) {
+    for (int f = threadIdx.x; f < n * 12; f += blockDim.x) {
         const int g = f / 12, j = f - g * 12;
         const float4 v = src[f];
         float* d = &s_sh[g * SH_STRIDE + 4 * j];
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
     }
     __syncthreads();
-    float* row = s_sh + threadIdx.x * SH_STRIDE;
-    if (idx < a.P) work(row, row + 3, 16);
+    float* row = s_sh + r * SH_STRIDE;
+    work(row, row + 3, 16);
     __syncthreads();
     store_f4(reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48), n * 12, a.acc & ACC_SH, [&](int f) {
         const int g = f / 12, j = f - g * 12;
@@ -757,33 +779,112 @@ __global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwd
     });
 }
 
-template <bool MULTI>
-static hipError_t launch_bwd(const PreprocessBwdViewsArgs& A, hipStream_t s)
+// Shared-memory bytes of staged_sh for ROWS rows (either layout).
+constexpr int staged_lds_bytes(int rows) { return rows * SH_STRIDE * 4; }
+
+// STAGED: the SH rows of the workgroup's 256 Gaussians go through LDS (staged_sh), one thread per
+// Gaussian.
+template <bool STAGED>
+__global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwdArgs a)
 {
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const int base = blockIdx.x * 256;
+    const int idx = base + (int)threadIdx.x;
+    BwdIn in;
+    BwdState st;
+    if (idx < a.P) bwd_gather(a, idx, in);  // in flight during the SH staging
+    if (!STAGED) {
+        if (idx < a.P) {
+            const size_t w3 = (size_t)a.M * 3;
+            bwd_core(a, idx, in, st);
+            if (a.dL_dsh) {
+                float* dsh = a.dL_dsh + idx * w3;
+                // ncoef <= M: no read past the row; no write past it either (M < 16)
+                const bool acc = a.acc & ACC_SH;
+                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
+                if (!acc)
+                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
+            }
+            bwd_finish(a, idx, st);
+        }
+        return;
+    }
+    staged_sh<256>(a, s_sh, base, min(256, a.P - base), threadIdx.x, [&](float* c0, float* cr, int kw) {
+        if (idx < a.P) {
+            bwd_core(a, idx, in, st);
+            sh_bwd_range<0, 1>(st, c0, c0);
+            sh_bwd_range<1, 16>(st, cr, cr, kw);
+            bwd_finish(a, idx, st);
+        }
+    });
+}
+
+// The multi-view batch: 256 / LPG Gaussians per workgroup, LPG lanes each (bwd_views_group).
+template <int LPG, bool STAGED>
+__global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const PreprocessBwdViewsArgs A)
+{
+    constexpr int G = 256 / LPG;
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const PreprocessBwdArgs& a = A.a;
-    if (a.P <= 0) return hipSuccess;
-    const bool staged = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
-                        ((uintptr_t)a.dL_dsh % 16) == 0;
-    const dim3 grid((a.P + 255) / 256), block(256);
-    if (staged || (a.dc && a.dL_ddc))
-        hipLaunchKernelGGL((preprocess_bwd_kernel<true, MULTI>), grid, block, 256 * SH_STRIDE * 4, s, A);
-    else
-        hipLaunchKernelGGL((preprocess_bwd_kernel<false, MULTI>), grid, block, 0, s, A);
-    return hipGetLastError();
+    const int gl = (int)threadIdx.x / LPG, v = (int)threadIdx.x % LPG;
+    const int base = blockIdx.x * G;
+    const bool live = base + gl < a.P;
+    const int idx = live ? base + gl : a.P - 1;  // clamped: all lanes take part in the reductions
+    BwdIn in;
+    bwd_gather(a, idx, in, false);
+    if (!STAGED) {
+        const size_t w3 = (size_t)a.M * 3;
+        const float* row = a.shs ? a.shs + idx * w3 : nullptr;
+        float* drow = (a.shs && a.dL_dsh) ? a.dL_dsh + idx * w3 : nullptr;
+        bwd_views_group<LPG>(A, idx, live, v, in, row, row ? row + 3 : nullptr, drow, drow ? drow + 3 : nullptr,
+                             a.M, a.acc & ACC_SH, a.acc & ACC_SH);
+        if (live && a.dL_dsh && !(a.acc & ACC_SH))  // columns past the SH coefficients (M > 16 or no SH)
+            for (int k = (a.shs ? 48 : 0) + v; k < a.M * 3; k += LPG) a.dL_dsh[idx * w3 + k] = 0.f;
+        return;
+    }
+    staged_sh<G>(a, s_sh, base, min(G, a.P - base), gl, [&](float* c0, float* cr, int kw) {
+        bwd_views_group<LPG>(A, idx, live, v, in, c0, cr, c0, cr, kw, false, false);
+    });
+}
+
+static bool staged_layout(const PreprocessBwdArgs& a)
+{
+    const bool interleaved = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
+                             ((uintptr_t)a.dL_dsh % 16) == 0;
+    return interleaved || (a.dc && a.dL_ddc);
 }
 
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
 {
-    PreprocessBwdViewsArgs A;
-    A.a = a;
-    A.V = 0;
-    return launch_bwd<false>(A, s);
+    if (a.P <= 0) return hipSuccess;
+    const dim3 grid((a.P + 255) / 256), block(256);
+    if (staged_layout(a))
+        hipLaunchKernelGGL((preprocess_bwd_kernel<true>), grid, block, staged_lds_bytes(256), s, a);
+    else
+        hipLaunchKernelGGL((preprocess_bwd_kernel<false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+template <int LPG>
+static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
+{
+    constexpr int G = 256 / LPG;
+    const dim3 grid((A.a.P + G - 1) / G), block(256);
+    if (staged_layout(A.a))
+        hipLaunchKernelGGL((preprocess_bwd_views_kernel<LPG, true>), grid, block, staged_lds_bytes(G), s, A);
+    else
+        hipLaunchKernelGGL((preprocess_bwd_views_kernel<LPG, false>), grid, block, 0, s, A);
+    return hipGetLastError();
 }
 
 hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
     if (A.V < 1 || A.V > MAX_VIEWS) return hipErrorInvalidValue;
-    return launch_bwd<true>(A, s);
+    if (A.a.P <= 0) return hipSuccess;
+    if (A.V <= 2) return launch_views<2>(A, s);
+    if (A.V <= 4) return launch_views<4>(A, s);
+    if (A.V <= 8) return launch_views<8>(A, s);
+    return launch_views<16>(A, s);
 }
 
 }  // namespace gsr

@@ -51,6 +51,13 @@ def _load():
     lib.gsr_backward_views.argtypes = [_i, _i, _i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                        _vp, _vp, _vp, _vp, _vp, _b, _b, ctypes.c_uint, _vp]
+    lib.gsr_backward_render.argtypes = [_i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _b, _vp]
+    lib.gsr_backward_preprocess_views.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f,
+                                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _vp, _vp,
+                                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _b, ctypes.c_uint, _vp]
+    lib.gsr_forward_views.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
+                                      _vp, _vp, _vp, _vp, _b, _b, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _vp, _vp,
+                                      _vp]
     lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
     lib.gsr_adam_update_multi.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
@@ -197,6 +204,83 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return L, out_color, radii, geom, binning, img, out_invdepth
 
 
+def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                              cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy, image_height,
+                              image_width, sh, degree, campos, prefiltered, antialiasing, debug, dc=None, out=None):
+    """rasterize_gaussians over a batch of V views of the same Gaussians (gsr_forward_views: the
+    views' binning prefixes run side by side on internal streams).  Per-view lists of camera
+    arguments; `out` = (colors (V,3,H,W), radii (V,P), invdepths (V,1,H,W)) -- written in full.
+    Returns per-view lists (num_rendered, geomBuffer, binningBuffer, imageBuffer); each view's
+    results are bit-identical to rasterize_gaussians on that view."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P, H, W = means3D.size(0), int(image_height), int(image_width)
+    V = len(viewmatrices)
+    colors_out, radii_out, inv_out = out
+    for t, shape, dt in ((colors_out, (V, 3, H, W), torch.float32), (radii_out, (V, P), torch.int32),
+                         (inv_out, (V, 1, H, W), torch.float32)):
+        if tuple(t.shape) != shape or t.dtype != dt or t.device != dev or not t.is_contiguous():
+            raise RuntimeError(f"out: expected a contiguous {dt} tensor of shape {shape} on {dev}")
+    if P == 0:
+        colors_out.zero_()
+        radii_out.zero_()
+        inv_out.zero_()
+        e = torch.empty((0,), dtype=torch.uint8, device=dev)
+        return [0] * V, [e] * V, [e] * V, [e] * V
+    M, has_dc = _sh_split(sh, dc)
+    if has_dc and (dc.dim() != 3 or dc.size(0) != P or dc.size(1) != 1 or dc.size(2) != 3):
+        raise RuntimeError("dc must have dimensions (num_points, 1, 3)")
+    keep = []
+
+    def p(t, name):
+        ptr, tt = _ptr(t, name, dev)
+        keep.append(tt)
+        return ptr
+
+    def cont(ts, name):
+        res = []
+        for t in ts:
+            _, tt = _ptr(t, name, dev)
+            keep.append(tt)
+            res.append(tt)
+        return res
+
+    gsz, isz = lib.gsr_geometry_buffer_size(P), lib.gsr_image_buffer_size(W, H)
+    geoms = [torch.empty((gsz,), dtype=torch.uint8, device=dev) for _ in range(V)]
+    imgs = [torch.empty((isz,), dtype=torch.uint8, device=dev) for _ in range(V)]
+    hint = _binning_hint.get(dev)
+    cap = lib.gsr_binning_buffer_size(min(int(hint * 1.25) + 65536, 0x7FFFFFFF)) if hint is not None else 0
+    bins = [torch.empty((cap,), dtype=torch.uint8, device=dev) if cap else None for _ in range(V)]
+    bg_p, means_p = p(background, "bg"), p(means3D, "means3D")
+    colors_p, op_p = p(colors, "colors_precomp"), p(opacity, "opacities")
+    sc_p, rot_p, cov_p = p(scales, "scales"), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp")
+    sh_p = p(sh, "sh")
+    dc_p = p(dc, "dc") if has_dc else None
+    views, projs, cams = cont(viewmatrices, "viewmatrix"), cont(projmatrices, "projmatrix"), cont(campos, "campos")
+    stream = _stream(dev)
+    nr = (_i * V)()
+    rendered = (_i * V)()
+    _check(lib.gsr_forward_views(
+        V, P, int(degree), M, bg_p, W, H, means_p, dc_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p,
+        cov_p, _ptr_array(views), _ptr_array(projs), _ptr_array(cams), (_f * V)(*[float(t) for t in tan_fovx]),
+        (_f * V)(*[float(t) for t in tan_fovy]), bool(prefiltered), bool(antialiasing), _ptr_array(geoms),
+        _ptr_array(imgs), _ptr_array(bins), (_sz * V)(*([cap] * V)), _ptr_array([colors_out[v] for v in range(V)]),
+        _ptr_array([inv_out[v] for v in range(V)]), _ptr_array([radii_out[v] for v in range(V)]), bool(debug),
+        stream, nr, rendered))
+    Ls = [int(nr[v]) for v in range(V)]
+    _binning_hint[dev] = max(Ls)
+    for v in range(V):
+        need = lib.gsr_binning_buffer_size(Ls[v])
+        if rendered[v]:
+            bins[v] = bins[v][:need]  # a view: the backward re-derives the layout from num_rendered
+        else:  # first call on this device, or the scene grew past the headroom
+            bins[v] = torch.empty((need,), dtype=torch.uint8, device=dev)
+            _check(lib.gsr_forward_render(geoms[v].data_ptr(), bins[v].data_ptr(), imgs[v].data_ptr(), P, Ls[v],
+                                          bg_p, W, H, colors_p, colors_out[v].data_ptr(), inv_out[v].data_ptr(),
+                                          radii_out[v].data_ptr(), bool(debug), stream))
+    return Ls, geoms, bins, imgs
+
+
 # accumulate= keys -> gsr.h GSR_ACC_* bits
 ACC_BITS = {"means3D": 1, "dc": 2, "sh": 4, "opacities": 8, "scales": 16, "rotations": 32, "cov3D_precomp": 64,
             "colors_precomp": 128}
@@ -299,24 +383,9 @@ def _ptr_array(ts):
     return (_vp * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
 
 
-def rasterize_gaussians_backward_views(background, means3D, radii, colors, opacities, scales, rotations,
-                                       scale_modifier, cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy,
-                                       dL_dout_colors, dL_dout_invdepths, sh, degree, campos, geomBuffers, Rs,
-                                       binningBuffers, imageBuffers, antialiasing, debug, dc=None, accumulate=None):
-    """Backward of a batch of V views (gsr_backward_views): per-view lists of the forward's state
-    (radii (P,), camera, buffers, num_rendered) and dL_dout_colors (V,3,H,W), dL_dout_invdepths
-    (V,1,H,W) or None.  Returns (dL_dmeans2D (V,P,3), dL_dcolors, dL_dopacity, dL_dmeans3D,
-    dL_dcov3D, [dL_ddc,] dL_dsh, dL_dscales, dL_drotations): the screen-space gradient per view,
-    everything else summed over the views; `accumulate` as in rasterize_gaussians_backward."""
-    _require_gpu(means3D)
-    dev = means3D.device
-    P = means3D.size(0)
-    V = len(geomBuffers)
-    H, W = dL_dout_colors.size(2), dL_dout_colors.size(3)
-    M, has_dc = _sh_split(sh, dc)
-    has_inv = dL_dout_invdepths is not None and dL_dout_invdepths.numel() != 0
-    if dL_dout_colors.shape != (V, 3, H, W) or (has_inv and dL_dout_invdepths.shape != (V, 1, H, W)):
-        raise RuntimeError("dL_dout_colors must be (V,3,H,W) and dL_dout_invdepths (V,1,H,W)")
+def _views_grads(P, M, V, has_dc, accumulate, dev):
+    """Outputs of a multi-view backward: (V,P,3) screen-space gradients and the summed parameter
+    gradients (fresh buffers, or the caller's `accumulate` targets), plus the GSR_ACC_* mask."""
     acc = dict(accumulate or {})
     for k, t in acc.items():
         n = {"means3D": 3 * P, "dc": 3 * P, "sh": 3 * M * P, "opacities": P, "scales": 3 * P, "rotations": 4 * P,
@@ -337,6 +406,40 @@ def rasterize_gaussians_backward_views(background, means3D, radii, colors, opaci
          "scales": acc.get("scales", parts[4]).view(P, 3), "rotations": acc.get("rotations", parts[5]).view(P, 4),
          "cov3D_precomp": acc.get("cov3D_precomp", parts[6]).view(P, 6),
          "colors_precomp": acc.get("colors_precomp", parts[7]).view(P, 3)}
+    mask = 0
+    for k in acc:
+        mask |= ACC_BITS[k]
+    return dL_dmeans2D, r, acc, mask
+
+
+def _views_result(dL_dmeans2D, r, acc, has_dc):
+    r = {k: (None if k in acc else v) for k, v in r.items()}
+    if has_dc:
+        return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["dc"], r["sh"],
+                r["scales"], r["rotations"])
+    return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["sh"],
+            r["scales"], r["rotations"])
+
+
+def rasterize_gaussians_backward_views(background, means3D, radii, colors, opacities, scales, rotations,
+                                       scale_modifier, cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy,
+                                       dL_dout_colors, dL_dout_invdepths, sh, degree, campos, geomBuffers, Rs,
+                                       binningBuffers, imageBuffers, antialiasing, debug, dc=None, accumulate=None):
+    """Backward of a batch of V views (gsr_backward_views): per-view lists of the forward's state
+    (radii (P,), camera, buffers, num_rendered) and dL_dout_colors (V,3,H,W), dL_dout_invdepths
+    (V,1,H,W) or None.  Returns (dL_dmeans2D (V,P,3), dL_dcolors, dL_dopacity, dL_dmeans3D,
+    dL_dcov3D, [dL_ddc,] dL_dsh, dL_dscales, dL_drotations): the screen-space gradient per view,
+    everything else summed over the views; `accumulate` as in rasterize_gaussians_backward."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    V = len(geomBuffers)
+    H, W = dL_dout_colors.size(2), dL_dout_colors.size(3)
+    M, has_dc = _sh_split(sh, dc)
+    has_inv = dL_dout_invdepths is not None and dL_dout_invdepths.numel() != 0
+    if dL_dout_colors.shape != (V, 3, H, W) or (has_inv and dL_dout_invdepths.shape != (V, 1, H, W)):
+        raise RuntimeError("dL_dout_colors must be (V,3,H,W) and dL_dout_invdepths (V,1,H,W)")
+    dL_dmeans2D, r, acc, mask = _views_grads(P, M, V, has_dc, accumulate, dev)
     keep = []
 
     def p(t, name):
@@ -358,9 +461,6 @@ def rasterize_gaussians_backward_views(background, means3D, radii, colors, opaci
     dpix = [dL_dout_colors[v].contiguous() for v in range(V)]
     dinv = [dL_dout_invdepths[v].contiguous() for v in range(V)] if has_inv else None
     keep.extend(dpix)
-    mask = 0
-    for k in acc:
-        mask |= ACC_BITS[k]
     _check(lib.gsr_backward_views(
         V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), p(background, "bg"), W, H, p(means3D, "means3D"),
         p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"), p(opacities, "opacities"),
@@ -372,12 +472,66 @@ def rasterize_gaussians_backward_views(background, means3D, radii, colors, opaci
         r["colors_precomp"].data_ptr(), r["opacities"].data_ptr(), r["means3D"].data_ptr(),
         r["cov3D_precomp"].data_ptr(), r["dc"].data_ptr() if has_dc else None, r["sh"].data_ptr() if M else None,
         r["scales"].data_ptr(), r["rotations"].data_ptr(), bool(antialiasing), bool(debug), mask, _stream(dev)))
-    r = {k: (None if k in acc else v) for k, v in r.items()}
-    if has_dc:
-        return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["dc"], r["sh"],
-                r["scales"], r["rotations"])
-    return (dL_dmeans2D, r["colors_precomp"], r["opacities"], r["means3D"], r["cov3D_precomp"], r["sh"],
-            r["scales"], r["rotations"])
+    return _views_result(dL_dmeans2D, r, acc, has_dc)
+
+
+def rasterize_gaussians_render_backward(background, P, R, geomBuffer, binningBuffer, imageBuffer, dL_dout_color,
+                                        dL_dout_invdepth, debug):
+    """BACKWARD::render of one view (gsr_backward_render): its per-(tile, Gaussian) gradient
+    records into binningBuffer, for rasterize_gaussians_preprocess_backward_views later."""
+    dev = dL_dout_color.device
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    has_inv = dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0
+    bg_p, bg = _ptr(background, "bg", dev)
+    dpix, dpix_t = _ptr(dL_dout_color, "dL_dout_color", dev)
+    dinv, dinv_t = _ptr(dL_dout_invdepth, "dL_dout_invdepth", dev) if has_inv else (None, None)
+    _check(lib.gsr_backward_render(int(P), int(R), bg_p, W, H, geomBuffer.data_ptr(),
+                                   binningBuffer.data_ptr() if binningBuffer.numel() else None,
+                                   imageBuffer.data_ptr(), dpix, dinv, bool(debug), _stream(dev)))
+    return has_inv
+
+
+def rasterize_gaussians_preprocess_backward_views(means3D, radii, colors, opacities, scales, rotations,
+                                                  scale_modifier, cov3D_precomp, viewmatrices, projmatrices,
+                                                  tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                                                  geomBuffers, Rs, binningBuffers, has_invdepth, antialiasing, debug,
+                                                  dc=None, accumulate=None):
+    """BACKWARD::preprocess of V views whose render backward already ran
+    (gsr_backward_preprocess_views); returns what rasterize_gaussians_backward_views returns."""
+    _require_gpu(means3D)
+    dev = means3D.device
+    P = means3D.size(0)
+    V = len(geomBuffers)
+    M, has_dc = _sh_split(sh, dc)
+    dL_dmeans2D, r, acc, mask = _views_grads(P, M, V, has_dc, accumulate, dev)
+    keep = []
+
+    def p(t, name):
+        ptr, tt = _ptr(t, name, dev)
+        keep.append(tt)
+        return ptr
+
+    def cont(ts, name):
+        out = []
+        for t in ts:
+            _, tt = _ptr(t, name, dev)
+            keep.append(tt)
+            out.append(tt)
+        return out
+
+    views, projs, cams = cont(viewmatrices, "viewmatrix"), cont(projmatrices, "projmatrix"), cont(campos, "campos")
+    _check(lib.gsr_backward_preprocess_views(
+        V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), int(image_width), int(image_height),
+        p(means3D, "means3D"), p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"),
+        p(opacities, "opacities"), p(scales, "scales"), float(scale_modifier), p(rotations, "rotations"),
+        p(cov3D_precomp, "cov3D_precomp"), _ptr_array(views), _ptr_array(projs), _ptr_array(cams),
+        (_f * V)(*[float(x) for x in tan_fovx]), (_f * V)(*[float(x) for x in tan_fovy]), _ptr_array(radii),
+        _ptr_array(geomBuffers), _ptr_array([b if b.numel() else None for b in binningBuffers]), bool(has_invdepth),
+        _ptr_array([dL_dmeans2D[v] for v in range(V)]), r["colors_precomp"].data_ptr(), r["opacities"].data_ptr(),
+        r["means3D"].data_ptr(), r["cov3D_precomp"].data_ptr(), r["dc"].data_ptr() if has_dc else None,
+        r["sh"].data_ptr() if M else None, r["scales"].data_ptr(), r["rotations"].data_ptr(), bool(antialiasing),
+        bool(debug), mask, _stream(dev)))
+    return _views_result(dL_dmeans2D, r, acc, has_dc)
 
 
 def _adam_check(param, param_grad, exp_avg, exp_avg_sq, N, M, dev):

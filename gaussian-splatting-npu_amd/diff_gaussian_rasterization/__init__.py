@@ -21,7 +21,7 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam",
-           "accumulate_grads_in_place", "MultiViewRasterizer", "rasterize_views"]
+           "accumulate_grads_in_place", "deferred_backward", "MultiViewRasterizer", "rasterize_views"]
 
 _state = threading.local()
 
@@ -64,6 +64,113 @@ def _accumulation_target(t):
     return g
 
 
+class _DeferredBatch:
+    """Views rendered inside deferred_backward: their render backward has run, their
+    BACKWARD::preprocess waits for flush()."""
+
+    def __init__(self):
+        self.views = []
+        self.lock = threading.Lock()
+
+    def add(self, view):
+        with self.lock:
+            self.views.append(view)
+
+    def flush(self):
+        with self.lock:
+            views, self.views = self.views, []
+        # views share one set of Gaussian inputs and image/flag settings per batched launch
+        groups = []
+        for v in views:
+            key = v["key"]
+            if groups and groups[-1][0] == key and len(groups[-1][1]) < 16:
+                groups[-1][1].append(v)
+            else:
+                groups.append((key, [v]))
+        for _, g in groups:
+            self._launch(g)
+
+    @staticmethod
+    def _launch(views):
+        v0 = views[0]
+        s0 = v0["settings"]
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, sh, opacities, dc) = v0["inputs"]
+        (c_col, c_m3, c_sc, c_rot, c_cov, c_sh, c_op, c_dc) = v0["caller_inputs"]
+        dev = means3D.device
+        stream = torch.cuda.current_stream(dev)
+        for v in views:  # each view's render backward ran on its forward's stream
+            stream.wait_event(v["event"])
+        inputs = {"means3D": c_m3, "dc": c_dc, "sh": c_sh, "opacities": c_op, "scales": c_sc, "rotations": c_rot,
+                  "cov3D_precomp": c_cov, "colors_precomp": c_col}
+        accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in inputs.items()) if g is not None}
+        if "dc" in accumulate and (dc is None or dc.numel() == 0):
+            del accumulate["dc"]
+        fence = _acc_fence.get(dev)
+        if accumulate and fence is not None:
+            stream.wait_event(fence)
+        for g in accumulate.values():
+            g.record_stream(stream)
+        grads = _C.rasterize_gaussians_preprocess_backward_views(
+            means3D, [v["radii"] for v in views], colors_precomp, opacities, scales, rotations, s0.scale_modifier,
+            cov3Ds_precomp, [v["settings"].viewmatrix for v in views], [v["settings"].projmatrix for v in views],
+            [v["settings"].tanfovx for v in views], [v["settings"].tanfovy for v in views], s0.image_height,
+            s0.image_width, sh, s0.sh_degree, [v["settings"].campos for v in views], [v["geom"] for v in views],
+            [v["num_rendered"] for v in views], [v["binning"] for v in views], any(v["has_inv"] for v in views),
+            s0.antialiasing, s0.debug, dc=dc, accumulate=accumulate)
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        _acc_fence[dev] = ev
+        if len(grads) == 9:
+            g2d, g_col, g_op, g_m3, g_cov, g_dc, g_sh, g_sc, g_rot = grads
+        else:
+            g2d, g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot = grads
+            g_dc = None
+        # A leaf without a .grad (and without hooks) takes its gradient buffer as .grad, as autograd's
+        # AccumulateGrad would (the parameter gradients stay views of ONE buffer: multiview's
+        # in-place all-reduce); the rest goes through autograd: activations (exp, sigmoid,
+        # normalize, cat) between the parameters and the rasterizer inputs, leaves with hooks.
+        tensors, gts = [], []
+        pairs = [(c_m3, g_m3), (c_sh, g_sh), (c_col, g_col), (c_op, g_op), (c_sc, g_sc), (c_rot, g_rot),
+                 (c_cov, g_cov), (c_dc, g_dc)]
+        pairs += [(v["means2D"], g2d[j]) for j, v in enumerate(views)]
+        for t, g in pairs:
+            if g is None or t is None or t.numel() == 0 or not t.requires_grad:
+                continue
+            g = g.view(t.shape)
+            if t.is_leaf and t.grad is None and not t._backward_hooks and \
+                    not getattr(t, "_post_accumulate_grad_hooks", None) and g.device == t.device:
+                t.grad = g
+            else:
+                tensors.append(t)
+                gts.append(g)
+        if tensors:
+            torch.autograd.backward(tensors, gts)
+
+
+@contextlib.contextmanager
+def deferred_backward():
+    """Rasterizer calls (GaussianRasterizer) whose forward runs inside this context defer the
+    per-Gaussian half of their backward: a view's backward runs only its BACKWARD::render (the
+    per-(tile, Gaussian) records, gsr_backward_render) as soon as its image gradient exists, and
+    when the context exits ONE BACKWARD::preprocess pass over the Gaussians
+    (gsr_backward_preprocess_views) produces the gradients of all the views at once, summed --
+    the multi-view step of MultiViewRasterizer with the views' forward and backward passes still
+    free to interleave (view v's render backward beside view v+1's forward on another stream).
+    The summed gradients reach the inputs at exit: added in place to an existing .grad of a leaf
+    input (as accumulate_grads_in_place), otherwise through autograd (activations between the
+    parameters and the rasterizer, means2D's screen-space gradient per view).  Until then the
+    inputs' .grad (and means2D.grad) do not hold these views' contributions.  Equal to the views'
+    ordinary backward passes up to fp32 summation order."""
+    batch = _DeferredBatch()
+    prev = getattr(_state, "deferred", None)
+    _state.deferred = batch
+    try:
+        yield batch
+    finally:
+        _state.deferred = prev
+    batch.flush()
+
+
 class GaussianRasterizationSettings(NamedTuple):
     image_height: int
     image_width: int
@@ -82,6 +189,17 @@ class GaussianRasterizationSettings(NamedTuple):
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                         raster_settings, dc=None):
+    batch = getattr(_state, "deferred", None)
+    inputs = (means3D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, dc)
+    if batch is not None and torch.is_grad_enabled() and any(
+            t is not None and t.requires_grad for t in inputs + (means2D,)):
+        # deferred_backward: the autograd node sees detached Gaussian inputs (its backward returns
+        # nothing for them, and the graph behind them -- activations -- stays untouched until the
+        # batch's exit runs it once); means2D (or a stand-in) carries the view's backward call
+        anchor = means2D if means2D.requires_grad else torch.zeros((0,), requires_grad=True)
+        det = [None if t is None else t.detach() for t in inputs]
+        return _RasterizeGaussians.apply(det[0], anchor, det[1], det[2], det[3], det[4], det[5], det[6],
+                                         raster_settings, det[7], (batch, inputs, means2D))
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                                      cov3Ds_precomp, raster_settings, dc)
 
@@ -94,7 +212,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                raster_settings, dc=None):
+                raster_settings, dc=None, deferred=None):
         s = raster_settings
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepths = _C.rasterize_gaussians(
             s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
@@ -102,6 +220,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             s.campos, s.prefiltered, s.antialiasing, s.debug, dc=dc)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        ctx.deferred = deferred  # (batch, the caller's inputs, the caller's means2D): deferred_backward
         # in-place accumulation (accumulate_grads_in_place): the inputs whose .grad the backward
         # may add into, kept by reference (leaves: the same tensors save_for_backward keeps)
         ctx.acc_inputs = None
@@ -127,6 +246,27 @@ class _RasterizeGaussians(torch.autograd.Function):
                                          device=means3D.device)
         if grad_out_depth is None:
             grad_out_depth = torch.Tensor([])  # no invdepth term (rasterize_points.cu:174-182 with zeros)
+        if ctx.deferred is not None:  # deferred_backward: the records now, the rest at the context's exit
+            dev = means3D.device
+            has_inv = _C.rasterize_gaussians_render_backward(
+                s.bg, means3D.size(0), ctx.num_rendered, geomBuffer, binningBuffer, imgBuffer, grad_out_color,
+                grad_out_depth, s.debug)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            batch, caller_inputs, i_m2 = ctx.deferred
+            (i_m3, i_sh, i_col, i_op, i_sc, i_rot, i_cov, i_dc) = caller_inputs
+            ctx.deferred = None
+            # views batched into one launch: the same Gaussian tensors (of the caller) and settings
+            key = (tuple(None if t is None or t.numel() == 0 else id(t) for t in caller_inputs), means3D.data_ptr(),
+                   sh.data_ptr(),
+                   colors_precomp.data_ptr(), opacities.data_ptr(), scales.data_ptr(), rotations.data_ptr(),
+                   cov3Ds_precomp.data_ptr(), None if dc is None else dc.data_ptr(), s.image_height, s.image_width,
+                   float(s.scale_modifier), s.sh_degree, bool(s.antialiasing), bool(s.debug))
+            batch.add({"key": key, "settings": s, "num_rendered": ctx.num_rendered, "radii": radii,
+                       "geom": geomBuffer, "binning": binningBuffer, "event": ev, "has_inv": has_inv, "means2D": i_m2,
+                       "inputs": (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, sh, opacities, dc),
+                       "caller_inputs": (i_col, i_m3, i_sc, i_rot, i_cov, i_sh, i_op, i_dc)})
+            return (None,) * 11
         accumulate = None
         if ctx.acc_inputs is not None:
             accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in ctx.acc_inputs.items())
@@ -157,7 +297,7 @@ class _RasterizeGaussians(torch.autograd.Function):
              grad_scales, grad_rotations) = grads
             grad_dc = None
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
-                grad_rotations, grad_cov3Ds_precomp, None, grad_dc)
+                grad_rotations, grad_cov3Ds_precomp, None, grad_dc, None)
 
 
 class GaussianRasterizer(nn.Module):
@@ -202,16 +342,6 @@ def _check_inputs(shs, colors_precomp, scales, rotations, cov3D_precomp, dc):
         raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
 
 
-_side_streams = {}
-
-
-def _side_stream(dev):
-    st = _side_streams.get(dev)
-    if st is None:
-        st = _side_streams[dev] = torch.cuda.Stream(dev)
-    return st
-
-
 def rasterize_views(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                     raster_settings, dc=None):
     return _RasterizeViews.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
@@ -220,8 +350,9 @@ def rasterize_views(means3D, means2D, sh, colors_precomp, opacities, scales, rot
 
 class _RasterizeViews(torch.autograd.Function):
     """A batch of V camera views of the same Gaussians as ONE autograd node (the
-    views of a data-parallel step).  Forward: each view through the single-view forward (same
-    kernels, bit-identical outputs) into slices of (V,3,H,W) / (V,P) / (V,1,H,W) outputs.
+    views of a data-parallel step).  Forward: _C.rasterize_gaussians_views (the single-view kernels
+    per view, bit-identical outputs, the views' binning prefixes overlapped) into (V,3,H,W) / (V,P)
+    / (V,1,H,W) outputs.
     Backward: _C.rasterize_gaussians_backward_views -- every view's BACKWARD::render, then one
     pass of BACKWARD::preprocess that reads each Gaussian's parameters once and writes their
     gradients summed over the views, where V single-view backward passes would read and write the
@@ -238,27 +369,16 @@ class _RasterizeViews(torch.autograd.Function):
         colors = torch.empty((V, 3, H, W), dtype=torch.float32, device=dev)
         radii = torch.empty((V, P), dtype=torch.int32, device=dev)
         invdepths = torch.empty((V, 1, H, W), dtype=torch.float32, device=dev)
-        state = []
-        # The views alternate between the caller's stream and a second one, so that one view's
-        # binning (preprocess, sorts, scans: small latency-bound launches) runs beside the
-        # previous view's render; the caller's stream then waits for both.
-        main = torch.cuda.current_stream(dev)
-        streams = [main] + ([_side_stream(dev)] if V > 1 else [])
-        for st in streams[1:]:
-            st.wait_stream(main)
-        for v, s in enumerate(raster_settings):
-            st = streams[v % len(streams)]
-            with torch.cuda.stream(st):
-                L, _, _, geom, binning, img, _ = _C.rasterize_gaussians(
-                    s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-                    s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
-                    s.campos, s.prefiltered, s.antialiasing, s.debug, dc=dc, out=(colors[v], radii[v], invdepths[v]))
-            if st is not main:
-                for t in (geom, binning, img):
-                    t.record_stream(main)  # used by the backward on the caller's stream
-            state.append((L, geom, binning, img))
-        for st in streams[1:]:
-            main.wait_stream(st)
+        # gsr_forward_views: the views' binning prefixes (preprocess, sorts, scans: short
+        # latency-bound launch chains) run side by side on the library's internal streams, the
+        # renders on the caller's stream
+        Ls, geoms, bins, imgs = _C.rasterize_gaussians_views(
+            s0.bg, means3D, colors_precomp, opacities, scales, rotations, s0.scale_modifier, cov3Ds_precomp,
+            [s.viewmatrix for s in raster_settings], [s.projmatrix for s in raster_settings],
+            [s.tanfovx for s in raster_settings], [s.tanfovy for s in raster_settings], H, W, sh, s0.sh_degree,
+            [s.campos for s in raster_settings], s0.prefiltered, s0.antialiasing, s0.debug, dc=dc,
+            out=(colors, radii, invdepths))
+        state = list(zip(Ls, geoms, bins, imgs))
         ctx.raster_settings = raster_settings
         ctx.num_rendered = [st[0] for st in state]
         ctx.set_materialize_grads(False)

@@ -271,6 +271,52 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
                        float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
                        gsr_stream_t stream);
 
+/* The two halves of gsr_backward_views, for callers that run each view's backward as soon as its
+ * image gradient exists and the parameter gradients once per batch (diff_gaussian_rasterization.
+ * deferred_backward: view v's render backward beside view v+1's forward on another stream).
+ * gsr_backward_render: BACKWARD::render of one view (rasterizer_impl.cu:399-418) -- its
+ * per-(tile, Gaussian) gradient records into its binning buffer, nothing else.
+ * gsr_backward_preprocess_views: BACKWARD::preprocess (rasterizer_impl.cu:423-449) of V <= 16
+ * such views in one pass over the Gaussians, arguments as gsr_backward_views; has_invdepth: some
+ * view's render backward had an inverse-depth gradient.  Running the first for every view and then
+ * the second equals gsr_backward_views bit for bit. */
+int gsr_backward_render(int P, int R, const float* background, int width, int height, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, const float* dL_invdepths,
+                        bool debug, gsr_stream_t stream);
+int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int width, int height,
+                                  const float* means3D, const float* dc, const float* shs,
+                                  const float* colors_precomp, const float* opacities, const float* scales,
+                                  float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                  const float* const* viewmatrices, const float* const* projmatrices,
+                                  const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                  const int* const* radii, char* const* geom_buffers, char* const* binning_buffers,
+                                  bool has_invdepth, float* const* dL_dmean2D, float* dL_dcolor, float* dL_dopacity,
+                                  float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                                  float* dL_dscale, float* dL_drot, bool antialiasing, bool debug,
+                                  unsigned accumulate, gsr_stream_t stream);
+
+/* Forward of a batch of V <= 16 camera views of the same Gaussians (the forward half of
+ * gsr_backward_views; each view the result of gsr_forward_prealloc_dc with its own state buffers).
+ * Every view's binning prefix (preprocess, depth sort, scan, emission) is enqueued first, view v on
+ * internal high-priority stream v mod 4, so the short latency-bound launch chains of several
+ * views run side by side; then, in view order, its num_rendered is read back (the one host
+ * hand-off per view, rasterizer_impl.cu:283-284), its tile sort runs on the same internal stream
+ * and its render on the caller's stream.  Per-view arrays hold one pointer per view
+ * (viewmatrices, projmatrices, campos, the three state buffers, out_colors (3,H,W), out_invdepths
+ * (1,H,W), radii (P) -- radii may be NULL); tan_fovx, tan_fovy, binning_capacity, num_rendered and
+ * rendered are host arrays.  rendered[v] = 0: view v's binning buffer was NULL or smaller than
+ * gsr_binning_buffer_size(num_rendered[v]) -- the caller allocates that and finishes the view with
+ * gsr_forward_render.  Every result is bit-identical to the single-view call's. */
+int gsr_forward_views(int V, int P, int D, int M, const float* background, int width, int height,
+                      const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                      const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                      const float* cov3D_precomp, const float* const* viewmatrices, const float* const* projmatrices,
+                      const float* const* campos, const float* tan_fovx, const float* tan_fovy, bool prefiltered,
+                      bool antialiasing, char* const* geometry_buffers, char* const* image_buffers,
+                      char* const* binning_buffers, const size_t* binning_capacity, float* const* out_colors,
+                      float* const* out_invdepths, int* const* radii, bool debug, gsr_stream_t stream,
+                      int* num_rendered, int* rendered);
+
 /* Visibility-masked Adam step (the accelerated upstream's `_C.adamUpdate`, called
  * by SparseGaussianAdam.step(visibility, N) from train.py:180-183): for each of the
  * N Gaussians with visible[i] set, its M consecutive elements of param are updated

@@ -153,3 +153,71 @@ def test_multiview_argument_checks():
     with pytest.raises(Exception, match="excatly one"):
         dgr.MultiViewRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros((V, P, 3), device=DEV),
                                    opacities=t["opacities"], scales=t["scales"], rotations=t["rotations"])
+
+
+@pytest.mark.parametrize("mode,antialiasing", [("sh_scales", False), ("colors_cov", False), ("dc", True)])
+def test_deferred_backward_matches_multiview(mode, antialiasing):
+    """deferred_backward (per-view forward + render backward, one batched preprocess backward at
+    the context's exit) against MultiViewRasterizer on the same views: bit-identical parameter and
+    screen-space gradients (the same kernels on the same records)."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, antialiasing, bg) for c in case["cams"]]
+    gc = torch.stack([g[0] for g in case["grads"]]).to(DEV)
+    gi = torch.stack([g[1] for g in case["grads"]]).to(DEV)
+
+    multi = _leaves(case, mode)
+    means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+    c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **multi)
+    torch.autograd.backward([c, i], [gc, gi])
+
+    deferred = _leaves(case, mode)
+    m2 = [torch.zeros((P, 3), device=DEV, requires_grad=True) for _ in range(V)]
+    with dgr.deferred_backward():
+        for v, s in enumerate(settings):
+            cv, rv, iv = dgr.GaussianRasterizer(s)(means2D=m2[v], **deferred)
+            torch.autograd.backward([cv, iv], [gc[v], gi[v]])
+            assert torch.equal(cv.detach(), c[v].detach()) and torch.equal(rv, r[v])
+        assert all(t.grad is None for t in deferred.values()), "gradients arrive at the context's exit"
+    torch.cuda.synchronize()
+    assert torch.equal(torch.stack([m.grad for m in m2]), means2D.grad)
+    for k in multi:
+        assert torch.equal(deferred[k].grad, multi[k].grad), k
+
+
+def test_deferred_backward_activations_streams_accumulation():
+    """The train.py shape: activations between the parameters and the rasterizer (exp, sigmoid,
+    normalize), views alternating between two streams, and a second batch adding into the .grad of
+    the first -- against the ordinary per-view backward passes (fp32 summation order: 1e-5)."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, False, bg) for c in case["cams"]]
+    sc = case["scene"]
+    raw0 = {"xyz": sc["means3D"], "f": sc["shs"], "op": torch.logit(sc["opacities"].clamp(1e-4, 1 - 1e-4)),
+            "scl": torch.log(sc["scales"]), "rot": sc["rotations"] * 1.7}
+
+    def run(deferred):
+        raw = {k: v.to(DEV).clone().requires_grad_(True) for k, v in raw0.items()}
+        streams = [torch.cuda.current_stream(DEV), torch.cuda.Stream(DEV)]
+        for rep in range(2):
+            inputs = {"means3D": raw["xyz"], "shs": raw["f"], "opacities": torch.sigmoid(raw["op"]),
+                      "scales": torch.exp(raw["scl"]), "rotations": torch.nn.functional.normalize(raw["rot"])}
+            streams[1].wait_stream(streams[0])
+            with (dgr.deferred_backward() if deferred else torch.enable_grad()):
+                for v, s in enumerate(settings):
+                    with torch.cuda.stream(streams[v % 2]):
+                        m2 = torch.zeros((P, 3), device=DEV, requires_grad=True)
+                        cv, _, iv = dgr.GaussianRasterizer(s)(means2D=m2, **inputs)
+                        # the views share the activations: the ordinary path backs through them per view
+                        torch.autograd.backward([cv, iv], [case["grads"][v][0].to(DEV), case["grads"][v][1].to(DEV)],
+                                                retain_graph=not deferred)
+                streams[0].wait_stream(streams[1])
+        torch.cuda.synchronize()
+        return {k: v.grad.cpu().numpy() for k, v in raw.items()}
+
+    a, b = run(False), run(True)
+    for k in a:
+        ok, rel = common.allclose_rel(b[k], a[k], rtol=1e-5, atol=1e-9)
+        assert ok, f"d{k}: deferred vs per-view rel {rel:.3e}"
