@@ -353,7 +353,9 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
     {
         ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s));
+        // + the index-order exclusive scan of the tile counts: each Gaussian's first gradient-record slot
+        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s, a.tiles_touched,
+                                      at<uint32_t>(gb, g.off[GEOM_EMIT_START])));
     }
     DEBUG_SYNC(s);
 
@@ -457,7 +459,7 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
         char* w = bb + b.off[BIN_GRAD_INST];
         const size_t q = align_up(4 * n, 256);
         uint32_t* tile_keys = reinterpret_cast<uint32_t*>(w);
-        uint32_t* gids = reinterpret_cast<uint32_t*>(w + q);
+        uint2* pairs = reinterpret_cast<uint2*>(w + 8 * q);  // (record slot, Gaussian id) per instance
         uint32_t* k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
         uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
         uint32_t* v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
@@ -466,7 +468,7 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
                                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
-                                          at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx, tile_keys, gids, emit_start,
+                                          at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx, tile_keys, pairs, emit_start,
                                           at<uint32_t>(bb, b.off[BIN_VALID]),
                                           at<uint2>(ib, im.off[IMG_RANGES]), T, s));
         }
@@ -475,7 +477,7 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
         const int bit = (int)higher_msb(gx * gy);
         {
             ProfScope ps_(PK_TILE_SORT, s);
-            HIP_TRY(radix_sort(L, bit, tile_keys, gids, k0, v0, k1, v1, slot, point_list, sorted_tiles,
+            HIP_TRY(radix_sort(L, bit, tile_keys, pairs, k0, v0, k1, v1, slot, point_list, sorted_tiles,
                                bb + b.off[BIN_RADIX_SCRATCH], s));
         }
         DEBUG_SYNC(s);

@@ -169,12 +169,14 @@ enum GeomArray {
                           // (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic; cullK scaled by log2(e)/2
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
-    GEOM_EMIT_START,      // u32[P] first emission slot of each Gaussian
+    GEOM_EMIT_START,      // u32[P] first gradient-record slot of each Gaussian (index-order exclusive scan
+                          // of tiles_touched)
     GEOM_RECT,            // u16x4[P] tile rect {x0, y0, x1, y1} (getRect), zero if culled
     GEOM_SORTED_RECT,     // u16x4[P] the rects in depth order (last depth-sort pass)
     GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
-    GEOM_SCAN_SCRATCH,    // u64[scan chunks + 1] look-back status words + chunk ticket (zeroed by preprocess)
+    GEOM_SCAN_SCRATCH,    // u64[2 scan chunks + 1] look-back status words of the two scans + chunk ticket
+                          // (zeroed by preprocess)
     GEOM_COUNT
 };
 
@@ -193,7 +195,7 @@ enum BinArray {
     BIN_SORTED_TILES,     // u32[L] tile id of sorted position
     BIN_SLOT,             // u32[L] emission slot of sorted position
     BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
-                          // it hosts the emission arrays and sort ping-pong buffers (32 B/instance)
+                          // it hosts the emission arrays and sort ping-pong buffers (40 B/instance)
     BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
     BIN_VALID,            // u32[ceil(L/32)] bit per emission slot: its gradient record was written (backward)
     BIN_COUNT
@@ -213,7 +215,7 @@ inline GeomLayout geom_layout(int P)
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 48 * p,
                                 4 * p, 4 * p, 4 * p, 8 * p, 8 * p, 16 * p + 1024, radix_status_bytes(P, 4),
-                                8 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
+                                8 * (2 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS) + 1)};
     GeomLayout l;
     size_t o = 0;
     for (int i = 0; i < GEOM_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
@@ -244,7 +246,7 @@ __host__ __device__ inline size_t tile_sort_status_bytes(size_t n)
 
 __host__ __device__ inline BinLayout bin_layout_dev(size_t n)
 {
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, tile_sort_status_bytes(n), 4 * ((n + 31) / 32)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, tile_sort_status_bytes(n), 4 * ((n + 31) / 32)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
@@ -255,7 +257,7 @@ __host__ __device__ inline BinLayout bin_layout_dev(size_t n)
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 2048, radix_status_bytes(L, 4), 4 * ((n + 31) / 32)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, radix_status_bytes(L, 4), 4 * ((n + 31) / 32)};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

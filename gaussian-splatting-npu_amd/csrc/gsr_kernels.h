@@ -109,8 +109,9 @@ struct PreprocessBwdArgs {
     // per-instance gradient records and the gather map
     const float* grad_inst;         // f32x12[L], emission order
     const uint32_t* valid;          // one bit per slot: records not flagged were never written (no contribution)
-    // (records are stored at emission slots: Gaussian i's are [emit_start[i], +tiles_touched[i]))
-    const uint32_t* emit_start;     // first emission slot of Gaussian i
+    // (Gaussian i's records are slots [emit_start[i], +tiles_touched[i]), emit_start the index-order
+    // exclusive scan of tiles_touched)
+    const uint32_t* emit_start;     // first record slot of Gaussian i
     const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
     int has_invdepth;
     const float4* conic_opacity;    // GEOM_CONIC_OPACITY (the rendered, AA-scaled opacity in .w)
@@ -178,20 +179,24 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
 // look-back over `status` (scan_status_words(n) u64 words, zero on entry: preprocess clears them).
 // The total goes to *total_out (pinned host memory is fine).
 int scan_status_words(int n);
+// With in2/out2: a second, independent scan of n items in the same launch, EXCLUSIVE sums into out2.
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
-                                 uint32_t* total_out, hipStream_t s);
+                                 uint32_t* total_out, hipStream_t s, const uint32_t* in2 = nullptr,
+                                 uint32_t* out2 = nullptr);
 
-hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
+hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
                       uint32_t* sorted_counts = nullptr);
-// Also clears the valid bit mask (the backward's record flags) and ranges[0..T) for tile_ranges.
+// Emission: tile_keys[i] and pairs[i] = (gradient-record slot, Gaussian id) of every instance, in
+// depth order (rec_start: index-order exclusive scan of the tile counts).  Also clears the valid
+// bit mask (the backward's record flags) and ranges[0..T) for tile_ranges.
 hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
-                                       const uint2* sorted_rects, uint32_t gx, uint32_t* emit_start, char* bb,
+                                       const uint2* sorted_rects, uint32_t gx, const uint32_t* rec_start, char* bb,
                                        size_t capacity, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
-                                 uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, uint32_t* valid, uint2* ranges, int T, hipStream_t s);
+                                 uint32_t gx, uint32_t* tile_keys, uint2* pairs, const uint32_t* rec_start,
+                                 uint32_t* valid, uint2* ranges, int T, hipStream_t s);
 // ranges must be zero on entry unless L == 0 (emit_instances clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,

@@ -315,16 +315,27 @@ __device__ __forceinline__ uint32_t scan_lookback(uint64_t* status, int c, int l
     return excl;
 }
 
+// Two scans in one launch: chunks [0, nchunks) scan `in` (inclusive, into `out`; the total goes
+// to total_out), chunks [nchunks, 2 nchunks) scan `in2` into `out2` (EXCLUSIVE), if given.  The
+// ticket hands out all chunks of the first scan before the second's; each scan looks back over
+// its own status words.
 __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, const uint32_t* gather, int n,
                                                             int nchunks, uint64_t* status, uint32_t* out,
-                                                            uint32_t* total_out)
+                                                            uint32_t* total_out, const uint32_t* in2, uint32_t* out2)
 {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_chunk, s_excl;
-    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + nchunks);
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + 2 * nchunks);
     if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
     __syncthreads();
-    const int c = (int)s_chunk;
+    const bool second = (int)s_chunk >= nchunks;
+    const int c = second ? (int)s_chunk - nchunks : (int)s_chunk;
+    if (second) {
+        in = in2;
+        gather = nullptr;
+        out = out2;
+        status += nchunks;
+    }
     // each thread owns 16 consecutive items; every load issued before the first use
     const size_t base = (size_t)c * SCAN_ITEMS + (size_t)threadIdx.x * 16;
     uint32_t v[16];
@@ -358,29 +369,33 @@ __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, 
             if (c > 0)
                 __hip_atomic_store(status + c, SCAN_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            if (c == nchunks - 1)
+            if (c == nchunks - 1 && !second)
                 __hip_atomic_store(total_out, excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_excl = excl;
         }
     }
     __syncthreads();
     ex += s_excl;
+    const uint32_t incl = second ? 0u : 1u;  // the second scan stores exclusive sums
     if (base + 16 <= (size_t)n && ((uintptr_t)out & 15) == 0) {  // 4 x 16-byte stores
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            uint4 q;
-            q.x = (ex += v[4 * k]);
-            q.y = (ex += v[4 * k + 1]);
-            q.z = (ex += v[4 * k + 2]);
-            q.w = (ex += v[4 * k + 3]);
-            reinterpret_cast<uint4*>(out + base)[k] = q;
+            uint32_t o[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint32_t nx = ex + v[4 * k + e];
+                o[e] = incl ? nx : ex;
+                ex = nx;
+            }
+            reinterpret_cast<uint4*>(out + base)[k] = make_uint4(o[0], o[1], o[2], o[3]);
         }
     } else {
 #pragma unroll
         for (int k = 0; k < 16; k++) {
-            ex += v[k];
+            const uint32_t nx = ex + v[k];
             const size_t i = base + k;
-            if (i < (size_t)n) out[i] = ex;
+            if (i < (size_t)n) out[i] = incl ? nx : ex;
+            ex = nx;
         }
     }
 }
@@ -413,14 +428,15 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
     return hipGetLastError();
 }
 
-int scan_status_words(int n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS + 1; }  // + the ticket
+int scan_status_words(int n) { return 2 * ((n + SCAN_ITEMS - 1) / SCAN_ITEMS) + 1; }  // two scans + the ticket
 
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
-                                 uint32_t* total_out, hipStream_t s)
+                                 uint32_t* total_out, hipStream_t s, const uint32_t* in2, uint32_t* out2)
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    hipLaunchKernelGGL(scan_lookback_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, nb, status, out, total_out);
+    hipLaunchKernelGGL(scan_lookback_kernel, dim3(in2 ? 2 * nb : nb), dim3(256), 0, s, in, gather, n, nb, status, out,
+                       total_out, in2, out2);
     return hipGetLastError();
 }
 

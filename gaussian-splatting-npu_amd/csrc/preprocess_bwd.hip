@@ -43,14 +43,11 @@ constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +
 // (L/8 bytes: it stays in L2), so a Gaussian's flags are one or two words; its flagged records are
 // then read B at a time in slot order (bitwise reproducible sums).
 template <int B = REC_BATCH>
-__device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
-                                               const uint32_t* valid, const float* grad_inst, int idx,
-                                               float (&g)[GF_NUM])
+__device__ __forceinline__ void gather_range(uint32_t e0, uint32_t e1, const uint32_t* valid, const float* grad_inst,
+                                             float (&g)[GF_NUM])
 {
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
-    const uint32_t e0 = emit_start[idx];
-    const uint32_t e1 = e0 + tiles_touched[idx];  // 0 tiles for culled Gaussians
     for (uint32_t w0 = e0 & ~31u; w0 < e1; w0 += 32) {
         uint32_t bits = valid[w0 >> 5];
         if (w0 < e0) bits &= ~0u << (e0 - w0);
@@ -84,6 +81,15 @@ __device__ __forceinline__ void gather_records(const uint32_t* emit_start, const
             }
         }
     }
+}
+
+template <int B = REC_BATCH>
+__device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
+                                               const uint32_t* valid, const float* grad_inst, int idx,
+                                               float (&g)[GF_NUM])
+{
+    const uint32_t e0 = emit_start[idx];
+    gather_range<B>(e0, e0 + tiles_touched[idx], valid, grad_inst, g);  // 0 tiles for culled Gaussians
 }
 
 // The per-Gaussian parameters (and, accumulating, the outputs' old values); with `view` also the
@@ -577,11 +583,6 @@ constexpr int SH_STRIDE = 49;  // LDS dwords per row (odd)
 // from the summed dL/dcov3D (linear in it).  The parameters (236 B per Gaussian at degree 3) are
 // read and their gradients written once per batch instead of once per view, and the V views'
 // dependent gathers (records) are in flight side by side instead of one after another.
-__device__ __forceinline__ ViewCam cam_of(const BwdView& v)
-{
-    return {v.view, v.proj, v.campos, v.focal_x, v.focal_y, v.tan_fovx, v.tan_fovy};
-}
-
 // x from another lane of its DPP row (CTRL: a dpp_ctrl code)
 template <int CTRL>
 __device__ __forceinline__ float dpp_mov(float x)
@@ -607,6 +608,50 @@ __device__ __forceinline__ float group_sum(float x)
 #endif
 constexpr int VIEW_REC_BATCH = GSR_VIEW_REC_BATCH;
 
+// A lane's view inputs, loaded in the kernel's prologue (unconditionally, clamped), so that their
+// round trip overlaps the SH staging and the record gather is the only dependent one after it.
+struct ViewIn {
+    int radius;
+    float4 co;
+    uint8_t cl;
+    uint32_t e0, n;  // record slots [e0, e0 + n)
+};
+
+__device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int idx, int v, ViewIn& vi)
+{
+    const BwdView& bv = A.v[v < A.V ? v : 0];
+    vi.radius = bv.radii[idx];
+    vi.co = bv.conic_opacity[idx];
+    vi.cl = bv.clamped[idx];
+    vi.e0 = bv.emit_start[idx];
+    vi.n = bv.tiles_touched[idx];
+}
+
+// The batch's cameras in LDS (view 16, proj 16, campos 3, focal_x, focal_y, tan_fovx, tan_fovy),
+// read by the lanes of each view instead of through two dependent global loads per lane.
+constexpr int CAM_FLOATS = 40;
+__device__ __forceinline__ void cams_to_lds(const PreprocessBwdViewsArgs& A, float (*s_cam)[CAM_FLOATS])
+{
+    for (int t = threadIdx.x; t < A.V * CAM_FLOATS; t += blockDim.x) {
+        const int v = t / CAM_FLOATS, j = t - v * CAM_FLOATS;
+        const BwdView& bv = A.v[v];
+        float x = 0.f;
+        if (j < 16) x = bv.view[j];
+        else if (j < 32) x = bv.proj[j - 16];
+        else if (j < 35) x = bv.campos[j - 32];
+        else if (j == 35) x = bv.focal_x;
+        else if (j == 36) x = bv.focal_y;
+        else if (j == 37) x = bv.tan_fovx;
+        else if (j == 38) x = bv.tan_fovy;
+        s_cam[v][j] = x;
+    }
+}
+
+__device__ __forceinline__ ViewCam cam_of_lds(const float* c)
+{
+    return {c, c + 16, c + 32, c[35], c[36], c[37], c[38]};
+}
+
 // One lane's share of a Gaussian of the batch.  c0: SH coefficient 0 (3 floats), cr: coefficient
 // k >= 1 at cr[3 (k - 1)]; d0 / dr the same for dL/dsh (may alias c0 / cr: every lane of the group
 // reads coefficient k before its sum is written), kw the number of coefficients to write (zeros from
@@ -614,24 +659,18 @@ constexpr int VIEW_REC_BATCH = GSR_VIEW_REC_BATCH;
 // run the same code on a clamped index, write nothing, and keep every lane in the reductions).
 template <int LPG>
 __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A, int idx, bool live, int v,
-                                                const BwdIn& in, const float* c0, const float* cr, float* d0,
-                                                float* dr, int kw, bool acc_dc, bool acc_sh)
+                                                const BwdIn& in, const ViewIn& vi, const float* cam,
+                                                const float* c0, const float* cr, float* d0, float* dr, int kw,
+                                                bool acc_dc, bool acc_sh)
 {
     const PreprocessBwdArgs& a = A.a;
     const size_t i = (size_t)idx;
     const bool has_view = live && v < A.V;
     const BwdView& bv = A.v[v < A.V ? v : 0];
-    bool vis = false;
-    float4 co = make_float4(0.f, 0.f, 0.f, 0.f);
-    uint8_t cl = 0;
+    const bool vis = has_view && vi.radius > 0;
     float gs[GF_NUM];
-    if (has_view) {
-        vis = bv.radii[idx] > 0;
-        co = bv.conic_opacity[idx];
-        cl = bv.clamped[idx];
-    }
     if (vis) {
-        gather_records<VIEW_REC_BATCH>(bv.emit_start, bv.tiles_touched, bv.valid, bv.grad_inst, idx, gs);
+        gather_range<VIEW_REC_BATCH>(vi.e0, vi.e0 + vi.n, bv.valid, bv.grad_inst, gs);
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
@@ -640,7 +679,7 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     cov3d_of(a, in, cov3D);
     ViewGrad o;
     if (vis) {
-        view_grad(a, cam_of(bv), gs, co, cl, in.mean, in.opacity, cov3D, o);
+        view_grad(a, cam_of_lds(cam), gs, vi.co, vi.cl, in.mean, in.opacity, cov3D, o);
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) o.g[q] = 0.f;
@@ -830,20 +869,26 @@ __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const Preproc
     const int base = blockIdx.x * G;
     const bool live = base + gl < a.P;
     const int idx = live ? base + gl : a.P - 1;  // clamped: all lanes take part in the reductions
+    __shared__ float s_cam[MAX_VIEWS][CAM_FLOATS];
     BwdIn in;
     bwd_gather(a, idx, in, false);
+    ViewIn vi;
+    view_load(A, idx, v, vi);  // in flight during the camera and SH staging
+    cams_to_lds(A, s_cam);
+    const float* cam = s_cam[v < A.V ? v : 0];
     if (!STAGED) {
+        __syncthreads();
         const size_t w3 = (size_t)a.M * 3;
         const float* row = a.shs ? a.shs + idx * w3 : nullptr;
         float* drow = (a.shs && a.dL_dsh) ? a.dL_dsh + idx * w3 : nullptr;
-        bwd_views_group<LPG>(A, idx, live, v, in, row, row ? row + 3 : nullptr, drow, drow ? drow + 3 : nullptr,
-                             a.M, a.acc & ACC_SH, a.acc & ACC_SH);
+        bwd_views_group<LPG>(A, idx, live, v, in, vi, cam, row, row ? row + 3 : nullptr, drow,
+                             drow ? drow + 3 : nullptr, a.M, a.acc & ACC_SH, a.acc & ACC_SH);
         if (live && a.dL_dsh && !(a.acc & ACC_SH))  // columns past the SH coefficients (M > 16 or no SH)
             for (int k = (a.shs ? 48 : 0) + v; k < a.M * 3; k += LPG) a.dL_dsh[idx * w3 + k] = 0.f;
         return;
     }
     staged_sh<G>(a, s_sh, base, min(G, a.P - base), gl, [&](float* c0, float* cr, int kw) {
-        bwd_views_group<LPG>(A, idx, live, v, in, c0, cr, c0, cr, kw, false, false);
+        bwd_views_group<LPG>(A, idx, live, v, in, vi, cam, c0, cr, c0, cr, kw, false, false);
     });
 }
 

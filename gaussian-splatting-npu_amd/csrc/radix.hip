@@ -154,8 +154,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(uint32_t*
 struct SortPassArgs {
     int n, shift, nbits, nchunks;
     const uint32_t* keys_in;
-    const uint32_t* vals_in;   // payload in; null: .x = input index (and .y = gids[index] when paired)
-    const uint32_t* gids;      // paired sorts: second payload word of the first pass
+    const uint32_t* vals_in;   // payload in; null (unpaired sorts' first pass): the input index
     uint32_t* keys_out;        // intermediate pass: keys_out[dst], vals_out[dst] (u32 or u32x2)
     uint32_t* vals_out;
     // final pass (keys_out == null): out_x[dst] = v.x, out_y[dst] = v.y, sorted_keys[dst] = key
@@ -220,14 +219,13 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
-    if (a.vals_in) {
+    if (PAIR || a.vals_in) {  // PAIR: the caller's pairs in the first pass
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
     } else {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
-            if constexpr (PAIR) val[i] = make_uint2((uint32_t)gidx(i), a.gids[gidx(i)]);
-            else val[i] = (uint32_t)gidx(i);
+            if constexpr (!PAIR) val[i] = (uint32_t)gidx(i);
         }
     }
 #pragma unroll
@@ -301,30 +299,34 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
     }
 }
 
-// Emission in depth order: instance slots [off(k-1), off(k)) of depth rank k belong to
-// Gaussian g = sorted_ids[k]; tiles y-major then x inside its rect (rasterizer_impl.cu:98-109).
+// Emission in depth order: instances [off(k-1), off(k)) of depth rank k belong to Gaussian
+// g = sorted_ids[k]; tiles y-major then x inside its rect (rasterizer_impl.cu:98-109).  Each
+// instance carries (slot, g): its gradient-record slot rec_start[g] + j (j-th tile of g), with
+// rec_start the index-order exclusive scan of the tile counts -- a Gaussian's records are
+// contiguous and Gaussians' record ranges follow their index, so the per-Gaussian gather of the
+// backward (preprocess_bwd, thread i <-> Gaussian i) reads consecutive lines across a wave.
 // One wave per 64 consecutive ranks: the lanes first publish their rects (read in depth order:
 // the depth sort laid them out, no gathers by Gaussian id) in LDS, then the wave fills its whole
-// slot range 64 consecutive slots at a time (coalesced stores), each lane finding the owner of
-// its slot by a binary search over the 64 rect starts.
+// instance range 64 consecutive instances at a time (coalesced stores), each lane finding the
+// owner of its instance by a binary search over the 64 rect starts.
 // Early form (bb != null): launched before the host has read num_rendered back, so the output
 // arrays are resolved here from the device-side total (offsets_d[P-1]) with the binning layout
 // the host will use; if that layout does not fit in `capacity` bytes, nothing is written (the
 // host then allocates the exact size and emits again).
 __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
                                                              const uint32_t* offsets_d, const uint2* sorted_rects,
-                                                             uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                                             uint32_t* emit_start, uint32_t* valid, uint2* ranges,
+                                                             uint32_t gx, uint32_t* tile_keys, uint2* pairs,
+                                                             const uint32_t* rec_start, uint32_t* valid, uint2* ranges,
                                                              int T, char* bb, size_t capacity)
 {
-    __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64];
+    __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64], s_rec[4][64];
     if (bb) {
         const size_t n = offsets_d[P - 1];
         const BinLayout b = bin_layout_dev(n);
         if (n == 0 || b.off[BIN_COUNT] + 256 > capacity) return;  // gsr_binning_buffer_size = total + 256
         const size_t q = align_up(4 * n, 256);
         tile_keys = reinterpret_cast<uint32_t*>(bb + b.off[BIN_GRAD_INST]);
-        gids = reinterpret_cast<uint32_t*>(bb + b.off[BIN_GRAD_INST] + q);
+        pairs = reinterpret_cast<uint2*>(bb + b.off[BIN_GRAD_INST] + 8 * q);
         valid = reinterpret_cast<uint32_t*>(bb + b.off[BIN_VALID]);
     }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -338,10 +340,10 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
     const uint32_t prev = offsets_d[max(kc - 1, 0)];
     const uint2 rc = sorted_rects[kc];
     const uint32_t wend = offsets_d[min(k0 + 63, P - 1)];
+    const uint32_t r0 = rec_start[g];
     uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1;
     if (k < P) {
         start = k == 0 ? 0u : prev;
-        emit_start[g] = start;
         x0 = rc.x & 0xFFFFu;
         y0 = rc.x >> 16;
         wd = max((rc.y & 0xFFFFu) - x0, 1u);
@@ -351,6 +353,7 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
     s_y0[w][lane] = y0;
     s_w[w][lane] = wd;
     s_g[w][lane] = g;
+    s_rec[w][lane] = r0;
     const uint32_t wbeg = (uint32_t)__shfl((int)start, 0, 64);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -365,7 +368,7 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
         const uint32_t wj = s_w[w][j];
         const uint32_t yy = local / wj, xx = local - yy * wj;
         tile_keys[sl] = (s_y0[w][j] + yy) * gx + (s_x0[w][j] + xx);
-        gids[sl] = s_g[w][j];
+        pairs[sl] = make_uint2(s_rec[w][j] + local, s_g[w][j]);
         if ((sl & 31u) == 0u) valid[sl >> 5] = 0u;  // the backward flags the records it writes
     }
 }
@@ -428,15 +431,16 @@ size_t radix_status_bytes(int n, int npass)
 static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 2048 && RS_MAXBINS == 256,
               "tile_sort_status_bytes (gsr_common.h) restates radix_status_bytes for 2,048-key chunks");
 
-// Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, and
-// with `gids` also gids[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
-// gids); the last pass writes out_x[dst] = i, out_y[dst] = gids[i] and sorted_keys[dst] = key
-// (any of them may be null); without gids it can also lay out rects[i] and their tile counts
-// in sorted order.  All writes are contiguous runs: no scattered stores.
-hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t* gids, uint32_t* k0, uint32_t* v0,
+// Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, or with
+// `pairs` the u32x2 pairs[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
+// pairs); the last pass writes out_x[dst] = i (pairs[i].x), out_y[dst] = pairs[i].y and
+// sorted_keys[dst] = key (any of them may be null); without pairs it can also lay out rects[i]
+// and their tile counts in sorted order.  All writes are contiguous runs: no scattered stores.
+hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects, uint2* sorted_rects, uint32_t* sorted_counts)
 {
+    const bool pair = pairs != nullptr;
     if (n <= 0) return hipSuccess;
     const int nchunks = (int)rs_chunks(n);
     uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
@@ -444,7 +448,7 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
     if (nbits < 1) nbits = 1;
     const int npass = (nbits + 7) / 8;
     const uint32_t* kin = keys_in;
-    const uint32_t* vin = nullptr;
+    const uint32_t* vin = reinterpret_cast<const uint32_t*>(pairs);
     int shift = 0;
     for (int p = 0; p < npass; p++) {
         const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
@@ -468,23 +472,22 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
         a.nchunks = nchunks;
         a.keys_in = kin;
         a.vals_in = vin;
-        a.gids = gids;
         a.keys_out = last ? nullptr : ((p & 1) ? k1 : k0);
         a.vals_out = last ? nullptr : ((p & 1) ? v1 : v0);
         a.out_x = out_x;
         a.out_y = out_y;
         a.sorted_keys = sorted_keys;
-        a.rects = (last && !gids) ? rects : nullptr;
+        a.rects = (last && !pair) ? rects : nullptr;
         a.sorted_rects = sorted_rects;
         a.sorted_counts = sorted_counts;
         a.row_prefix = counts;
         a.totals = totals;
         const dim3 g((unsigned)nchunks), b(RS_THREADS);
         if (shrt) {
-            if (gids) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, true>), g, b, 0, s, a);
+            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, true>), g, b, 0, s, a);
             else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, false>), g, b, 0, s, a);
         } else {
-            if (gids) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, a);
+            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, a);
             else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false>), g, b, 0, s, a);
         }
         kin = a.keys_out;
@@ -495,22 +498,22 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint32_t*
 }
 
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
-                                 uint32_t gx, uint32_t* tile_keys, uint32_t* gids,
-                                 uint32_t* emit_start, uint32_t* valid, uint2* ranges, int T, hipStream_t s)
+                                 uint32_t gx, uint32_t* tile_keys, uint2* pairs, const uint32_t* rec_start,
+                                 uint32_t* valid, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       sorted_rects, gx, tile_keys, gids, emit_start, valid, ranges, T, nullptr, (size_t)0);
+                       sorted_rects, gx, tile_keys, pairs, rec_start, valid, ranges, T, nullptr, (size_t)0);
     return hipGetLastError();
 }
 
 hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
-                                       const uint2* sorted_rects, uint32_t gx, uint32_t* emit_start, char* bb,
+                                       const uint2* sorted_rects, uint32_t gx, const uint32_t* rec_start, char* bb,
                                        size_t capacity, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0 || !bb) return hipSuccess;
     hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       sorted_rects, gx, nullptr, nullptr, emit_start, nullptr, ranges, T, bb, capacity);
+                       sorted_rects, gx, nullptr, nullptr, rec_start, nullptr, ranges, T, bb, capacity);
     return hipGetLastError();
 }
 
