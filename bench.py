@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--no-deferred", dest="deferred", action="store_false",
                     help="every view's full backward on its own (default: per-view render backward, ONE batched "
                          "preprocess backward per step, dgr.deferred_backward)")
+    ap.add_argument("--order", choices=("interleave", "lookahead", "forward-first"), default="interleave",
+                    help="issue order of the step's views: forward+backward per view, the next view's forward "
+                         "before this view's backward, or every forward before every backward")
     ap.add_argument("--no-fused-accumulation", action="store_true",
                     help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
@@ -254,18 +257,38 @@ def main():
             ar_events.append((e0, e1, nbytes))
 
     def views_loop(n_st):
-        for i, (s, (gc, gi)) in enumerate(zip(cams, grads)):
+        def forward(i):
             st = streams[i % n_st]
             with torch.cuda.stream(st):
-                rast = dgr.GaussianRasterizer(raster_settings=s)
-                means2D = means2Ds[i]
+                rast = dgr.GaussianRasterizer(raster_settings=cams[i])
                 # views after the first add their gradients into the parameters' .grad inside the
                 # backward kernel (dgr.accumulate_grads_in_place) instead of autograd's separate add
                 with dgr.accumulate_grads_in_place(not args.no_fused_accumulation):
-                    color, radii, inv = rast(means3D=params["means3D"], means2D=means2D, shs=params["shs"],
+                    color, radii, inv = rast(means3D=params["means3D"], means2D=means2Ds[i], shs=params["shs"],
                                              opacities=params["opacities"], scales=params["scales"],
                                              rotations=params["rotations"])
-                torch.autograd.backward([color, inv], [gc, gi])
+            return st, color, inv
+
+        def backward(i, out):
+            st, color, inv = out
+            with torch.cuda.stream(st):
+                torch.autograd.backward([color, inv], list(grads[i]))
+
+        n = len(cams)
+        if args.order == "interleave":  # forward, backward, next view
+            for i in range(n):
+                backward(i, forward(i))
+        elif args.order == "lookahead":  # the next view's forward is issued before this view's backward
+            prev = forward(0)
+            for i in range(1, n):
+                cur = forward(i)
+                backward(i - 1, prev)
+                prev = cur
+            backward(n - 1, prev)
+        else:  # every forward, then every backward
+            outs = [forward(i) for i in range(n)]
+            for i in range(n):
+                backward(i, outs[i])
         for st in streams[1:n_st]:
             main_stream.wait_stream(st)
 

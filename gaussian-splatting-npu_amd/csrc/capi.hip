@@ -4,6 +4,7 @@
 // stream-ordered D2H of num_rendered, and error reporting.  No exceptions
 // cross the ABI; every launch goes to the caller's stream.
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -85,6 +86,9 @@ constexpr int PREFIX_STREAMS = 4;  // views whose binning prefixes run side by s
 struct PrefixStream {
     hipStream_t s[PREFIX_STREAMS] = {};
     hipEvent_t fork = nullptr, join = nullptr;
+    // side work of a prefix (the index-order scan) beside its critical path
+    hipStream_t aux = nullptr;
+    hipEvent_t aux_in = nullptr, aux_out = nullptr;
 };
 constexpr int MAX_DEVICES = 64;
 thread_local PrefixStream g_prefix[MAX_DEVICES];
@@ -120,6 +124,50 @@ int prefix_fork(hipStream_t caller, int n, hipStream_t* out)
 }
 
 int prefix_begin(hipStream_t caller, hipStream_t* out) { return prefix_fork(caller, 1, out); }
+
+int current_device()
+{
+    int dev = 0;
+    return hipGetDevice(&dev) == hipSuccess ? dev : 0;
+}
+
+// The auxiliary stream of the current device, forked from `s` (s itself when the prefix streams
+// are off); aux_join makes `s` wait for everything enqueued on it so far.
+int aux_fork(hipStream_t s, hipStream_t* out)
+{
+    *out = s;
+    if (g_prefix_off) return GSR_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail_hip(e, __LINE__);
+    if (dev < 0 || dev >= MAX_DEVICES) return GSR_OK;
+    PrefixStream& ps = g_prefix[dev];
+    if (!ps.aux) {
+        int least = 0, greatest = 0;
+        if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipStreamCreateWithPriority(&ps.aux, hipStreamNonBlocking, greatest)) != hipSuccess)
+            return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.aux_in, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.aux_out, hipEventDisableTiming)) != hipSuccess)
+            return fail_hip(e, __LINE__);
+    }
+    if ((e = hipEventRecord(ps.aux_in, s)) != hipSuccess) return fail_hip(e, __LINE__);
+    if ((e = hipStreamWaitEvent(ps.aux, ps.aux_in, 0)) != hipSuccess) return fail_hip(e, __LINE__);
+    *out = ps.aux;
+    return GSR_OK;
+}
+
+int aux_join(hipStream_t s, hipStream_t aux)
+{
+    if (aux == s) return GSR_OK;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return fail_hip(e, __LINE__);
+    PrefixStream& ps = g_prefix[dev];
+    if ((e = hipEventRecord(ps.aux_out, aux)) != hipSuccess) return fail_hip(e, __LINE__);
+    if ((e = hipStreamWaitEvent(s, ps.aux_out, 0)) != hipSuccess) return fail_hip(e, __LINE__);
+    return GSR_OK;
+}
 
 // the caller's stream waits for everything enqueued on the prefix stream so far
 int prefix_end(hipStream_t caller, hipStream_t prefix)
@@ -264,17 +312,16 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
 }
 
 
-// Forward, first half: preprocess, depth sort and the tile-count scan are enqueued; *h_out is the
-// pinned word block the scan publishes num_rendered into (forward_geometry_wait reads it).
-static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width,
-                                   int height, const float* means3D, const float* dc, const float* shs,
-                                   const float* colors_precomp, const float* opacities, const float* scales,
-                                   float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                                   const float* viewmatrix, const float* projmatrix, const float* cam_pos,
-                                   float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
-                                   bool debug, gsr_stream_t stream, uint32_t** h_out, int slot = 0)
+// The arguments of one view's preprocess (argument checks; the view's pinned read-back slot is
+// reset: *h_out its host words, *hdev_out their device address).
+static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width,
+                                 int height, const float* means3D, const float* dc, const float* shs,
+                                 const float* colors_precomp, const float* opacities, const float* scales,
+                                 float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                 const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                                 float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
+                                 int slot, PreprocessArgs* out, uint32_t** h_out, uint32_t** hdev_out)
 {
-    hipStream_t s = (hipStream_t)stream;
     if (width <= 0 || height <= 0) return fail(GSR_ERR_INVALID, "image size must be positive");
     if (!colors_precomp && !dc && (!shs || M <= 0))
         return fail(GSR_ERR_INVALID, "Please provide exactly one of either SHs or precomputed colors!");
@@ -299,8 +346,7 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     uint32_t* h_dev = nullptr;
     HIP_TRY(hipHostGetDevicePointer((void**)&h_dev, h, 0));
 
-    // 1. preprocess (forward.cu:154-272)
-    PreprocessArgs a;
+    PreprocessArgs& a = *out;
     a.P = P; a.D = D; a.M = dc ? M + 1 : M; a.W = width; a.H = height;  // kernels count the dc coefficient
     a.dc = dc;
     a.means3D = means3D; a.scales = scales; a.scale_modifier = scale_modifier; a.rotations = rotations;
@@ -321,15 +367,32 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     a.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
     a.host_flags = h_dev;
     a.scan_status = at<uint64_t>(gb, g.off[GEOM_SCAN_SCRATCH]);
-    a.scan_status_words = scan_status_words(P);
+    a.scan_status_words = 2 * scan_status_words(P);  // the depth-order and the index-order scan
     a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     a.dkey = at<uint32_t>(gb, g.off[GEOM_DKEY]);
     a.rect = at<uint2>(gb, g.off[GEOM_RECT]);
+    *h_out = h;
+    *hdev_out = h_dev;
+    return GSR_OK;
+}
+
+// After preprocess: the record-slot scan, the depth sort and the tile-count scan of one view.
+static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint32_t* h_dev, hipStream_t s,
+                                 bool debug, bool use_aux = true)
+{
+    const GeomLayout g = geom_layout(P);
+    // 1b. each Gaussian's first gradient-record slot: index-order exclusive scan of the tile counts
+    //     (records in Gaussian order: preprocess_bwd's per-Gaussian gathers are contiguous), on the
+    //     auxiliary stream beside the depth sort; emission (which reads it) waits for it
+    hipStream_t aux = s;
     {
-        ProfScope ps_(PK_PREPROCESS, s);
-        HIP_TRY(launch_preprocess(a, s));
+        // (one auxiliary stream per device: views whose prefixes run side by side on several
+        // prefix streams scan inline instead of coupling their streams through it)
+        int rc = use_aux ? aux_fork(s, &aux) : GSR_OK;
+        if (rc) return rc;
+        HIP_TRY(launch_inclusive_scan(a.tiles_touched, nullptr, at<uint32_t>(gb, g.off[GEOM_EMIT_START]), P,
+                                      a.scan_status + scan_status_words(P), nullptr, aux, true));
     }
-    DEBUG_SYNC(s);
 
     // 2. stable depth sort of the Gaussians (first half of the reference's tile|depth key sort)
     uint32_t* sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
@@ -353,14 +416,42 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
     {
         ProfScope ps_(PK_SCAN, s);
-        // + the index-order exclusive scan of the tile counts: each Gaussian's first gradient-record slot
-        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s, a.tiles_touched,
-                                      at<uint32_t>(gb, g.off[GEOM_EMIT_START])));
+        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s));
+    }
+    {
+        const int rc = aux_join(s, aux);
+        if (rc) return rc;
     }
     DEBUG_SYNC(s);
-
-    *h_out = h;
     return GSR_OK;
+}
+
+// Forward, first half: preprocess, depth sort and the tile-count scan are enqueued; *h_out is the
+// pinned word block the scan publishes num_rendered into (forward_geometry_wait reads it).
+static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width,
+                                   int height, const float* means3D, const float* dc, const float* shs,
+                                   const float* colors_precomp, const float* opacities, const float* scales,
+                                   float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                   const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                                   float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
+                                   bool debug, gsr_stream_t stream, uint32_t** h_out, int slot = 0,
+                                   bool use_aux = true)
+{
+    hipStream_t s = (hipStream_t)stream;
+    PreprocessArgs a;
+    uint32_t* h_dev = nullptr;
+    int rc = forward_geometry_args(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                   colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                   viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                   radii, slot, &a, h_out, &h_dev);
+    if (rc) return rc;
+    // 1. preprocess (forward.cu:154-272)
+    {
+        ProfScope ps_(PK_PREPROCESS, s);
+        HIP_TRY(launch_preprocess(a, s));
+    }
+    DEBUG_SYNC(s);
+    return forward_geometry_sort(a, geometry_buffer, P, h_dev, s, debug, use_aux);
 }
 
 static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rendered)
@@ -633,43 +724,55 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     const GeomLayout g = geom_layout(P);
     const ImageLayout im = image_layout(width, height);
 
-    // Prefix stream k carries views k, k + n, k + 2n, ...: each view's first half (preprocess, depth
-    // sort, scan, early emission), and after its num_rendered is read back its second half (tile
-    // sort, ranges, order), then the first half of the stream's next view.  Up to n views' short
-    // latency-bound launch chains are in flight side by side, and no view's tile sort queues
-    // behind a later view's preprocess.  The renders go to the caller's stream in view order.
     uint32_t* h[MAX_VIEWS];
-    auto first_half = [&](int v) -> int {
-        char* gb = geometry_buffers[v];
-        char* ib = image_buffers[v];
-        if (!gb || !ib) return fail(GSR_ERR_ALLOC, "null state buffer");
+    // 1. ONE preprocess launch per 8 views on prefix stream 0 (the Gaussians' parameters and SH rows
+    //    read once for all of them), then view v's depth sort, scans and early emission on prefix
+    //    stream v mod n: the short latency-bound launch chains of the views run side by side.
+    PreprocessArgs pa[MAX_VIEWS];
+    uint32_t* hdev[MAX_VIEWS];
+    for (int v = 0; v < V && !rc; v++) {
+        if (!geometry_buffers[v] || !image_buffers[v]) return fail(GSR_ERR_ALLOC, "null state buffer");
         if (!out_colors[v] || !out_invdepths[v]) return fail(GSR_ERR_INVALID, "null per-view output");
+        rc = forward_geometry_args(geometry_buffers[v], image_buffers[v], P, D, M, width, height, means3D, dc, shs,
+                                   colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                   viewmatrices[v], projmatrices[v], campos[v], tan_fovx[v], tan_fovy[v], prefiltered,
+                                   antialiasing, radii ? radii[v] : nullptr, v, &pa[v], &h[v], &hdev[v]);
+    }
+    if (rc) return rc;
+    {
+        ProfScope ps_(PK_PREPROCESS, ps[0]);
+        HIP_TRY(launch_preprocess_views(pa, V, ps[0]));
+    }
+    DEBUG_SYNC(ps[0]);
+    if (n > 1) {
+        PrefixStream& pst = g_prefix[0 <= current_device() && current_device() < MAX_DEVICES ? current_device() : 0];
+        HIP_TRY(hipEventRecord(pst.fork, ps[0]));
+        for (int k = 1; k < n; k++) HIP_TRY(hipStreamWaitEvent(ps[k], pst.fork, 0));
+    }
+    for (int v = 0; v < V && !rc; v++) {
         const hipStream_t s = ps[v % n];
-        const int r = forward_geometry_launch(gb, ib, P, D, M, width, height, means3D, dc, shs, colors_precomp,
-                                              opacities, scales, scale_modifier, rotations, cov3D_precomp,
-                                              viewmatrices[v], projmatrices[v], campos[v], tan_fovx[v], tan_fovy[v],
-                                              prefiltered, antialiasing, radii ? radii[v] : nullptr, debug, s, &h[v], v);
-        if (r) return r;
+        char* gb = geometry_buffers[v];
+        rc = forward_geometry_sort(pa[v], gb, P, hdev[v], s, debug, n == 1);
+        if (rc) break;
         if (binning_buffers[v] && binning_capacity[v] > 0) {
             ProfScope ps_(PK_EMIT, s);
             HIP_TRY(launch_emit_instances_early(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
                                                 at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                                                 at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx,
                                                 at<uint32_t>(gb, g.off[GEOM_EMIT_START]), binning_buffers[v],
-                                                binning_capacity[v], at<uint2>(ib, im.off[IMG_RANGES]),
+                                                binning_capacity[v], at<uint2>(image_buffers[v], im.off[IMG_RANGES]),
                                                 (int)(gx * gy), s));
         }
-        return GSR_OK;
-    };
-    for (int v = 0; v < n && !rc; v++) rc = first_half(v);
+    }
+    // 2. in view order: num_rendered read back, the view's tile sort on its prefix stream and its
+    //    render on the caller's stream (views whose binning buffer is too small are left to the
+    //    caller: allocate gsr_binning_buffer_size(num_rendered[v]), then gsr_forward_render)
     for (int v = 0; v < V && !rc; v++) {
         const hipStream_t s = ps[v % n];
         int L = 0;
         rc = forward_geometry_wait(h[v], s, &L);
         num_rendered[v] = L;
         if (rc) break;
-        // views whose binning buffer is too small are left to the caller (allocate
-        // gsr_binning_buffer_size(num_rendered[v]), then gsr_forward_render)
         const bool early = binning_buffers[v] && binning_capacity[v] > 0;
         if (early && gsr_binning_buffer_size(L) <= binning_capacity[v]) {
             rc = forward_render_impl(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L, background,
@@ -677,7 +780,6 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
             if (rc) break;
             rendered[v] = 1;
         }
-        if (v + n < V) rc = first_half(v + n);
     }
     for (int k = 0; k < n; k++) {  // everything the prefix streams wrote is ordered before the caller's next work
         const int rj = prefix_end(caller, ps[k]);

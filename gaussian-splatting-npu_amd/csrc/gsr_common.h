@@ -175,8 +175,8 @@ enum GeomArray {
     GEOM_SORTED_RECT,     // u16x4[P] the rects in depth order (last depth-sort pass)
     GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
-    GEOM_SCAN_SCRATCH,    // u64[2 scan chunks + 1] look-back status words of the two scans + chunk ticket
-                          // (zeroed by preprocess)
+    GEOM_SCAN_SCRATCH,    // 2 x u64[scan chunks + 1] look-back status words + chunk ticket of the two
+                          // scans (depth order, index order; zeroed by preprocess)
     GEOM_COUNT
 };
 
@@ -215,7 +215,7 @@ inline GeomLayout geom_layout(int P)
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 48 * p,
                                 4 * p, 4 * p, 4 * p, 8 * p, 8 * p, 16 * p + 1024, radix_status_bytes(P, 4),
-                                8 * (2 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS) + 1)};
+                                16 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
     GeomLayout l;
     size_t o = 0;
     for (int i = 0; i < GEOM_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -174,15 +174,18 @@ hipError_t launch_adam_update(const AdamArgs& a, hipStream_t s);
 hipError_t launch_adam_update_multi(const AdamArgs* groups, int n_groups, hipStream_t s);
 
 hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s);
+// V views of the same Gaussians (a[v] differ in camera and output buffers only), PREPROCESS_BATCH
+// views per launch: each launch reads the Gaussians' parameters once.
+constexpr int PREPROCESS_BATCH = 8;
+hipError_t launch_preprocess_views(const PreprocessArgs* a, int V, hipStream_t s);
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s);
 // Inclusive scan of in[gather[i]] (gather may be null): one launch, chained chunks with decoupled
 // look-back over `status` (scan_status_words(n) u64 words, zero on entry: preprocess clears them).
 // The total goes to *total_out (pinned host memory is fine).
 int scan_status_words(int n);
-// With in2/out2: a second, independent scan of n items in the same launch, EXCLUSIVE sums into out2.
+// exclusive: exclusive sums instead; total_out may be null.
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
-                                 uint32_t* total_out, hipStream_t s, const uint32_t* in2 = nullptr,
-                                 uint32_t* out2 = nullptr);
+                                 uint32_t* total_out, hipStream_t s, bool exclusive = false);
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,

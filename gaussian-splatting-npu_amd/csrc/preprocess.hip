@@ -197,17 +197,32 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
 // SH coefficients are 192 of the 236 bytes read per Gaussian at degree 3.  STAGED: the block's
 // 256 x 3M floats arrive through LDS with coalesced 16-byte loads (rows padded to an odd number
 // of dwords, so the per-thread row walks are bank-conflict-free) instead of every lane striding
-// 3M floats through global memory.
-template <bool STAGED>
-__global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, int lds_stride)
+// 3M floats through global memory.  NV > 1: the block's Gaussians for up to NV views of the same
+// Gaussians (a batch of views, gsr_forward_views): their parameters and SH rows are read from HBM
+// once, each view's outputs go to its own buffers (A.a[v]).
+template <int NV>
+struct PreprocessBatch {
+    PreprocessArgs a[NV];
+    int V;
+};
+
+template <bool STAGED, int NV>
+__global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBatch<NV> A, int lds_stride)
 {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const PreprocessArgs& a = A.a[0];  // the Gaussian inputs (the same in every view)
     const int base = blockIdx.x * 256;
     const int idx = base + (int)threadIdx.x;
-    if (idx < a.scan_status_words) a.scan_status[idx] = 0;  // the scan runs after this kernel
+    const int V = NV == 1 ? 1 : A.V;
+    for (int v = 0; v < V; v++)
+        if (idx < A.a[v].scan_status_words) A.a[v].scan_status[idx] = 0;  // the scans run after this kernel
+    auto views = [&](const float* sh0, const float* sh) {
+        if (idx >= a.P) return;
+        for (int v = 0; v < V; v++) preprocess_one(A.a[v], idx, sh0, sh);
+    };
     if (!STAGED) {
         const float* row = a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr;
-        if (idx < a.P) preprocess_one(a, idx, row, row);
+        views(row, row);
         return;
     }
     if (a.dc && a.M <= 16) {  // separate dc, verbatim: dc rows at 0, rest rows (stride 3(M-1)) at 768
@@ -216,7 +231,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
         lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
         if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
         __syncthreads();
-        if (idx < a.P) preprocess_one(a, idx, s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x - 3);
+        views(s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x - 3);
         return;
     }
     if (a.dc) {  // separate dc, wide rest rows: coefficient 0 into columns 0-2, the rest after it (16 used)
@@ -226,7 +241,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
                                           (a.M - 1) * 3, n);
         __syncthreads();
         const float* row = s_sh + threadIdx.x * lds_stride;
-        if (idx < a.P) preprocess_one(a, idx, row, row);
+        views(row, row);
         return;
     }
     const int W3 = a.M * 3;  // multiple of 4 on this path
@@ -240,7 +255,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(PreprocessArgs a, i
     }
     __syncthreads();
     const float* row = s_sh + threadIdx.x * lds_stride;
-    if (idx < a.P) preprocess_one(a, idx, row, row);
+    views(row, row);
 }
 
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,
@@ -315,27 +330,18 @@ __device__ __forceinline__ uint32_t scan_lookback(uint64_t* status, int c, int l
     return excl;
 }
 
-// Two scans in one launch: chunks [0, nchunks) scan `in` (inclusive, into `out`; the total goes
-// to total_out), chunks [nchunks, 2 nchunks) scan `in2` into `out2` (EXCLUSIVE), if given.  The
-// ticket hands out all chunks of the first scan before the second's; each scan looks back over
-// its own status words.
+// Inclusive (or, with `exclusive`, exclusive) scan of in[gather[i]] into out; the total goes to
+// total_out (may be null).
 __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, const uint32_t* gather, int n,
                                                             int nchunks, uint64_t* status, uint32_t* out,
-                                                            uint32_t* total_out, const uint32_t* in2, uint32_t* out2)
+                                                            uint32_t* total_out, bool exclusive)
 {
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_chunk, s_excl;
-    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + 2 * nchunks);
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + nchunks);
     if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
     __syncthreads();
-    const bool second = (int)s_chunk >= nchunks;
-    const int c = second ? (int)s_chunk - nchunks : (int)s_chunk;
-    if (second) {
-        in = in2;
-        gather = nullptr;
-        out = out2;
-        status += nchunks;
-    }
+    const int c = (int)s_chunk;
     // each thread owns 16 consecutive items; every load issued before the first use
     const size_t base = (size_t)c * SCAN_ITEMS + (size_t)threadIdx.x * 16;
     uint32_t v[16];
@@ -369,14 +375,14 @@ __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, 
             if (c > 0)
                 __hip_atomic_store(status + c, SCAN_INC | (uint64_t)(excl + total), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-            if (c == nchunks - 1 && !second)
+            if (c == nchunks - 1 && total_out)
                 __hip_atomic_store(total_out, excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             s_excl = excl;
         }
     }
     __syncthreads();
     ex += s_excl;
-    const uint32_t incl = second ? 0u : 1u;  // the second scan stores exclusive sums
+    const bool incl = !exclusive;
     if (base + 16 <= (size_t)n && ((uintptr_t)out & 15) == 0) {  // 4 x 16-byte stores
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -400,25 +406,48 @@ __global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, 
     }
 }
 
-hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
+template <int NV>
+static hipError_t launch_preprocess_batch(const PreprocessBatch<NV>& A, hipStream_t s)
 {
+    const PreprocessArgs& a = A.a[0];
     if (a.P <= 0) return hipSuccess;
     const int W3 = a.M * 3;
     const bool staged = a.shs && !a.colors_precomp && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
                         ((uintptr_t)a.shs % 16) == 0;
+    const dim3 grid((a.P + 255) / 256), block(256);
     if (a.dc && !a.colors_precomp) {  // separate dc: always staged (any M, any alignment)
         const int stride = (min(a.M, 16) * 3) | 1;
         const size_t lds = a.M <= 16 ? (768 + 256 * (size_t)(a.M - 1) * 3) * sizeof(float)
                                      : 256 * stride * sizeof(float);
-        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256), lds, s, a, stride);
+        hipLaunchKernelGGL((preprocess_fwd_kernel<true, NV>), grid, block, lds, s, A, stride);
     } else if (staged) {
         const int stride = W3 | 1;
-        hipLaunchKernelGGL(preprocess_fwd_kernel<true>, dim3((a.P + 255) / 256), dim3(256),
-                           256 * stride * sizeof(float), s, a, stride);
+        hipLaunchKernelGGL((preprocess_fwd_kernel<true, NV>), grid, block, 256 * stride * sizeof(float), s, A,
+                           stride);
     } else {
-        hipLaunchKernelGGL(preprocess_fwd_kernel<false>, dim3((a.P + 255) / 256), dim3(256), 0, s, a, 0);
+        hipLaunchKernelGGL((preprocess_fwd_kernel<false, NV>), grid, block, 0, s, A, 0);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_preprocess(const PreprocessArgs& a, hipStream_t s)
+{
+    PreprocessBatch<1> A;
+    A.a[0] = a;
+    A.V = 1;
+    return launch_preprocess_batch(A, s);
+}
+
+hipError_t launch_preprocess_views(const PreprocessArgs* a, int V, hipStream_t s)
+{
+    for (int v0 = 0; v0 < V; v0 += PREPROCESS_BATCH) {
+        PreprocessBatch<PREPROCESS_BATCH> A;
+        A.V = min(PREPROCESS_BATCH, V - v0);
+        for (int v = 0; v < A.V; v++) A.a[v] = a[v0 + v];
+        const hipError_t e = launch_preprocess_batch(A, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 hipError_t launch_mark_visible(int P, const float* means3D, const float* view, bool* present, hipStream_t s)
@@ -428,15 +457,15 @@ hipError_t launch_mark_visible(int P, const float* means3D, const float* view, b
     return hipGetLastError();
 }
 
-int scan_status_words(int n) { return 2 * ((n + SCAN_ITEMS - 1) / SCAN_ITEMS) + 1; }  // two scans + the ticket
+int scan_status_words(int n) { return (n + SCAN_ITEMS - 1) / SCAN_ITEMS + 1; }  // + the ticket
 
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
-                                 uint32_t* total_out, hipStream_t s, const uint32_t* in2, uint32_t* out2)
+                                 uint32_t* total_out, hipStream_t s, bool exclusive)
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    hipLaunchKernelGGL(scan_lookback_kernel, dim3(in2 ? 2 * nb : nb), dim3(256), 0, s, in, gather, n, nb, status, out,
-                       total_out, in2, out2);
+    hipLaunchKernelGGL(scan_lookback_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, nb, status, out, total_out,
+                       exclusive);
     return hipGetLastError();
 }
 

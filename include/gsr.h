@@ -297,9 +297,10 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
 
 /* Forward of a batch of V <= 16 camera views of the same Gaussians (the forward half of
  * gsr_backward_views; each view the result of gsr_forward_prealloc_dc with its own state buffers).
- * Every view's binning prefix (preprocess, depth sort, scan, emission) is enqueued first, view v on
- * internal high-priority stream v mod 4, so the short latency-bound launch chains of several
- * views run side by side; then, in view order, its num_rendered is read back (the one host
+ * One preprocess launch per 8 views reads the Gaussians' parameters once for all of them; then
+ * every view's depth sort, scans and emission are enqueued, view v on internal high-priority
+ * stream v mod 4, so the short latency-bound launch chains of several views run side by side;
+ * then, in view order, its num_rendered is read back (the one host
  * hand-off per view, rasterizer_impl.cu:283-284), its tile sort runs on the same internal stream
  * and its render on the caller's stream.  Per-view arrays hold one pointer per view
  * (viewmatrices, projmatrices, campos, the three state buffers, out_colors (3,H,W), out_invdepths
