@@ -99,7 +99,8 @@ def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1):
         # depth keys in, sorted ids out; rects gathered and laid out in depth order, tile counts out
         "depth_sort": P * 28,
         "scan": P * 8,                                          # depth-ordered tile counts in, offsets out
-        "emit_instances": P * 20 + L * 9,                       # ids, offsets, rects, emit_start; (tile, id, flag)
+        # ids, offsets, rects, record starts in; (tile, (record slot, id)) per instance + valid bits out
+        "emit_instances": P * 20 + L * 12 + L // 8,
         "tile_sort": L * 24,                                    # (tile, slot, id) in and out
         "tile_ranges": L * 4 + T * 8,
         "tile_order": T * 12,                                   # per-tile work in, launch order out
@@ -120,11 +121,12 @@ def lib_sha256():
 
 
 def pmc_traffic(args, timeout=240):
-    """HBM traffic per launch of every rasterizer kernel, measured now on this build: two
-    rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: together they exceed the 4 TCC counters
-    of one pass) over this script's own workload (`--pmc-child`: the same views, 1 warm-up + 1
-    step), each a child process under a time limit; bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per
-    MI355X_MICROARCH.md §HBM, per launch (tools/pmc_summary.py).  None if rocprofv3 is absent or a
+    """HBM traffic and VALU wave-instructions per launch of every rasterizer kernel, measured now
+    on this build: three rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE -- together they exceed
+    the 4 TCC counters of one pass -- and SQ_INSTS_VALU) over this script's own workload
+    (`--pmc-child`: the same views, 1 warm-up + 1 step), each a child process under a time limit;
+    bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per MI355X_MICROARCH.md §HBM, per launch
+    (tools/pmc_summary.py).  Returns (traffic, valu) dicts, or None if rocprofv3 is absent or a
     pass fails."""
     exe = shutil.which("rocprofv3")
     if not exe:
@@ -139,7 +141,7 @@ def pmc_traffic(args, timeout=240):
         child.append("--antialiasing")
     env = dict(os.environ, TMPDIR=tmp)
     try:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        for counter in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
             r = subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(tmp, counter),
                                 "-o", "run", "--"] + child, env=env, cwd=ROOT, timeout=timeout,
                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -151,7 +153,8 @@ def pmc_traffic(args, timeout=240):
                 pmc_summary.main(tmp)
             finally:
                 sys.stdout = old
-        return json.load(open(os.path.join(tmp, "pmc_traffic.json")))["bytes_per_launch"]
+        return (json.load(open(os.path.join(tmp, "pmc_traffic.json")))["bytes_per_launch"],
+                json.load(open(os.path.join(tmp, "pmc_valu.json")))["winst_per_launch"])
     except Exception:
         return None
     finally:
@@ -369,11 +372,14 @@ def main():
     roofline = None
     if kern:
         ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if args.deferred else 1)
-        dom = max(kern, key=lambda k: kern[k]["avg_ms"])
+        # the dominant kernel: the largest share of the step (mean launch time x launches per step)
+        dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
         sha = lib_sha256()
         traffic, traffic_src, traffic_all = None, None, None
         measured = None if (args.no_pmc or world > 1) else pmc_traffic(args)
+        valu_measured = measured[1] if measured else None
+        measured = measured[0] if measured else None
         if measured and dom in measured:
             traffic, traffic_src, traffic_all = measured[dom], "rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (this run)", \
                 measured
@@ -389,19 +395,20 @@ def main():
             except Exception:
                 traffic_src = "unavailable"
         valu = None  # secondary roofline: render kernels are VALU-issue bound, not HBM bound
-        vf = os.path.join(ROOT, "profiles", "pmc_valu.json")
-        try:
-            vi = json.load(open(vf))
-            if vi.get("lib_sha256") == sha:
-                vi = vi["winst_per_launch"]
-                valu = {k: {"winst_per_launch": vi[k],
-                            "achieved_Ginst_s": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
-                            "frac": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
-                        for k in kern if k in vi}
-                valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": "profiles/pmc_valu.json (SQ_INSTS_VALU, same build)",
-                        "kernels": valu}
-        except Exception:
-            valu = None
+        vi, vsrc = valu_measured, "rocprofv3 --pmc SQ_INSTS_VALU (this run)"
+        if not vi:
+            try:
+                st = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu.json")))
+                if st.get("lib_sha256") == sha:
+                    vi, vsrc = st["winst_per_launch"], "profiles/pmc_valu.json (SQ_INSTS_VALU, same build)"
+            except Exception:
+                vi = None
+        if vi:
+            valu = {k: {"winst_per_launch": vi[k],
+                        "achieved_Ginst_s": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
+                        "frac": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
+                    for k in kern if k in vi}
+            valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": vsrc, "kernels": valu}
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": traffic_src, "traffic_stale": traffic is None and traffic_src is not None

@@ -15,7 +15,7 @@ import sys
 SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_lookback_kernel": "scan",
          "emit_instances_kernel": "emit_instances", "tile_ranges_kernel": "tile_ranges",
          "tile_order_kernel": "tile_order", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
-         "preprocess_bwd_kernel": "preprocess_bwd",
+         "preprocess_bwd_kernel": "preprocess_bwd", "preprocess_bwd_views_kernel": "preprocess_bwd",
          # the depth sort and the tile sort share these kernels: reported together, per step
          "radix_count_kernel": "radix_sorts", "radix_rowscan_kernel": "radix_sorts",
          "radix_rowscan_lds_kernel": "radix_sorts",
