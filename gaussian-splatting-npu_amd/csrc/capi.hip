@@ -603,6 +603,7 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
     r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.out_color = out_color;
     r.invdepth = depth;
+    r.hit = L > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
     {
         ProfScope ps_(PK_RENDER_FWD, s);
         HIP_TRY(launch_render_fwd(r, T, s));
@@ -837,6 +838,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
     r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     r.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
+    r.hit = R > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
     if (R > 0) {
         {
             ProfScope ps_(PK_TILE_ORDER, s);
@@ -934,6 +936,7 @@ int gsr_backward_render(int P, int R, const float* background, int width, int he
     r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);
     r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
     r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
+    r.hit = at<uint8_t>(bb, b.off[BIN_HIT]);
     {
         ProfScope ps_(PK_TILE_ORDER, s);
         HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,

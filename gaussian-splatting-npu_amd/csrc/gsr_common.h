@@ -198,6 +198,8 @@ enum BinArray {
                           // it hosts the emission arrays and sort ping-pong buffers (40 B/instance)
     BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
     BIN_VALID,            // u32[ceil(L/32)] bit per emission slot: its gradient record was written (backward)
+    BIN_HIT,              // u8[L] per sorted position: quadrants (bit w = 8x8 quadrant w) with a pixel the
+                          // entry contributed to in the forward (render_fwd), read by render_bwd
     BIN_COUNT
 };
 
@@ -246,7 +248,7 @@ __host__ __device__ inline size_t tile_sort_status_bytes(size_t n)
 
 __host__ __device__ inline BinLayout bin_layout_dev(size_t n)
 {
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, tile_sort_status_bytes(n), 4 * ((n + 31) / 32)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, tile_sort_status_bytes(n), 4 * ((n + 31) / 32), n};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
@@ -257,7 +259,7 @@ __host__ __device__ inline BinLayout bin_layout_dev(size_t n)
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, radix_status_bytes(L, 4), 4 * ((n + 31) / 32)};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, radix_status_bytes(L, 4), 4 * ((n + 31) / 32), n};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

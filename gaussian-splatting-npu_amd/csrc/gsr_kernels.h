@@ -52,6 +52,7 @@ struct RenderFwdArgs {
     float* out_color;
     float* invdepth;
     float4* accum;  // IMG_ACCUM: {C_r, C_g, C_b, invdepth} before the background
+    uint8_t* hit;   // BIN_HIT: contributing quadrants of every processed list entry (out)
 };
 
 struct RenderBwdArgs {
@@ -70,6 +71,7 @@ struct RenderBwdArgs {
     const uint32_t* slot;       // emission slot of each sorted position
     uint32_t* valid;            // bit (slot & 31) of valid[slot >> 5] set for every record written (cleared by emit)
     float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
+    const uint8_t* hit;         // BIN_HIT (render_fwd): the quadrants each entry contributed to
 };
 
 // Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  With u = G dL/dalpha

@@ -227,6 +227,15 @@ __global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, c
     }
 }
 
+// quadrant bits of batch entry e from the per-wave round masks
+__device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64], int e)
+{
+    uint32_t h = 0;
+#pragma unroll
+    for (int w = 0; w < 4; w++) h |= (uint32_t)((s_hitw[w][e >> 6] >> (e & 63)) & 1ull) << w;
+    return h;
+}
+
 __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 {
 #pragma clang fp contract(fast)
@@ -243,6 +252,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 
     __shared__ float4 s_rec[BATCH * 3];
     __shared__ uint8_t s_mask[BATCH];
+    // per wave and 64-entry round of a batch: bit i = entry (round, i) contributed to some pixel of
+    // the wave's quadrant (kept in scalar registers during the round, stored once per round)
+    __shared__ uint64_t s_hitw[4][BATCH / 64];
 
     bool done = !inside;
     float T = 1.0f;
@@ -251,8 +263,13 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
 
     // list ids are fetched one batch ahead, so a batch waits for its record gather only
     uint32_t next_id = todo > 0 ? a.point_list[range.x + min(tid, todo - 1)] : 0u;
+    int flushed = 0;  // entries [0, flushed) have their contribution bits in a.hit
     for (int base = 0; base < todo; base += BATCH) {
         if (__syncthreads_and(done)) break;
+        if (base > 0) {  // the previous batch's contribution bits (every wave has finished it)
+            a.hit[range.x + base - BATCH + tid] = (uint8_t)hit_bits(s_hitw, tid);
+            flushed = base;
+        }
         const int k = base + tid;
         const uint32_t id = next_id;
         next_id = a.point_list[range.x + min(k + BATCH, todo - 1)];
@@ -264,6 +281,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
         s_rec[2 * BATCH + tid] = r2;
         const uint32_t m = k < todo ? quad_mask(r0, r1, tx, ty) : 0u;
         s_mask[tid] = (uint8_t)m;
+        if (tid < 4 * (BATCH / 64)) (&s_hitw[0][0])[tid] = 0ull;
         __syncthreads();
         const int n = min(BATCH, todo - base);
         // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
@@ -273,6 +291,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
             const int jr = r * 64 + lane;
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
+            uint64_t hitbits = 0;  // wave-uniform
             // two entries per iteration with ping-pong record registers (no rotation copies)
             auto take = [&]() -> int {
                 const int jj = rem ? r * 64 + (int)__builtin_ctzll(rem) : -1;
@@ -288,6 +307,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
                     done = true;
                     contrib = false;
                 }
+                if (__ballot(contrib) != 0ull) hitbits |= 1ull << (j & 63);
                 if (contrib) {
                     C0 += col.x * alpha * T;
                     C1 += col.y * alpha * T;
@@ -313,6 +333,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
                 blend(jb, bxy, bco, bcol);
                 if (j < 0 || __all(done)) break;
             }
+            if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
         }
     }
 
@@ -320,6 +341,9 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
     const uint32_t wl = wave_max_u32(last_contributor);
     if (lane == 0) s_lc[wid] = wl;
     __syncthreads();
+    // the last processed batch's contribution bits (entries past it are never read: the
+    // backward stops at the tile's largest n_contrib, all of whose entries were processed)
+    if (flushed + tid < todo && tid < BATCH) a.hit[range.x + flushed + tid] = (uint8_t)hit_bits(s_hitw, tid);
     if (tid == 0) a.tile_work[tile] = max(max(s_lc[0], s_lc[1]), max(s_lc[2], s_lc[3]));
 
     if (inside) {
@@ -535,32 +559,32 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     __shared__ float4 s_rec[3][64];
     __shared__ uint8_t s_list[64];
 
-    // Entries that contribute to no pixel (list positions >= tmax, or culled for every quadrant)
-    // get no record: valid[slot] stays 0 and preprocess_bwd skips them.
+    // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
+    // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
+    // pixel) are evaluated; entries that contributed nowhere (and list positions >= tmax) get no
+    // record: valid[slot] stays 0 and preprocess_bwd skips them.
 
-    // list ids and slots are fetched one batch ahead; record loads are unconditional (clamped)
+    // list ids, slots and contribution bits are fetched one batch ahead; record loads are
+    // unconditional (clamped)
     const int last = (int)tmax - 1;
-    uint32_t next_id = 0, next_slot = 0;
+    uint32_t next_id = 0, next_slot = 0, next_hit = 0;
     if (tmax > 0) {
         next_id = a.point_list[range.x + min(lane, last)];
         next_slot = a.slot[range.x + min(lane, last)];
+        next_hit = a.hit[range.x + min(lane, last)];
     }
     for (int p0 = 0; p0 < (int)tmax; p0 += 64) {
         const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
-        const uint32_t id = next_id, myslot = next_slot;
+        const uint32_t id = next_id, myslot = next_slot, hit = next_hit;
         next_id = a.point_list[range.x + min(pos_l + 64, last)];
         next_slot = a.slot[range.x + min(pos_l + 64, last)];
+        next_hit = a.hit[range.x + min(pos_l + 64, last)];
         const float4* r = a.splat + 3 * (size_t)id;
         const float4 r0 = r[0], r1 = r[1], r2 = r[2];
         s_rec[0][lane] = r0;
         s_rec[1][lane] = r1;
         s_rec[2][lane] = r2;
-        uint32_t m = 0;
-        if (pos_l < (int)tmax) {
-            m = quad_mask(r0, r1, tx, ty);
-            m &= (uint32_t)((uint32_t)pos_l < qmax[0]) | ((uint32_t)((uint32_t)pos_l < qmax[1]) << 1) |
-                 ((uint32_t)((uint32_t)pos_l < qmax[2]) << 2) | ((uint32_t)((uint32_t)pos_l < qmax[3]) << 3);
-        }
+        const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         const uint64_t b = __ballot(m != 0);
         const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
         if (m != 0) s_list[before] = (uint8_t)lane;
