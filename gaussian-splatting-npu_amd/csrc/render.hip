@@ -236,7 +236,7 @@ __device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64
     return h;
 }
 
-__global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) render_fwd_kernel(RenderFwdArgs a)
 {
 #pragma clang fp contract(fast)
     const uint32_t tile = a.tile_order[blockIdx.x];
@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(256) render_fwd_kernel(RenderFwdArgs a)
                     done = true;
                     contrib = false;
                 }
-                if (__ballot(contrib) != 0ull) hitbits |= 1ull << (j & 63);
+                hitbits |= (uint64_t)(__ballot(contrib) != 0ull) << (j & 63);  // scalar, branch-free
                 if (contrib) {
                     C0 += col.x * alpha * T;
                     C1 += col.y * alpha * T;
