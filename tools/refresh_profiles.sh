@@ -12,4 +12,4 @@ bash tools/profile_pmc.sh "$TAG/pmc" > "$OUT/pmc.log" 2>&1 || { tail -20 "$OUT/p
 cp "gpurun_out/$TAG/pmc/pmc_traffic.json" "gpurun_out/$TAG/pmc/pmc_valu.json" profiles/
 timeout -k 10 400 python -u bench.py > "$OUT/bench.log" 2>&1 || { tail -20 "$OUT/bench.log"; exit 1; }
 grep '^{' "$OUT/bench.log" | cut -c1-200
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-aux > "$OUT/rocprof.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-aux --no-pmc > "$OUT/rocprof.log" 2>&1
