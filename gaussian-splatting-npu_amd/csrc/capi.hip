@@ -1228,4 +1228,25 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
     return GSR_OK;
 }
 
+size_t gsr_debug_depth_sort_workspace_size(int n)
+{
+    const size_t q = align_up(4 * (size_t)(n > 0 ? n : 0), 256);
+    return 4 * q + align_up(radix_status_bytes(n, 4), 256);
+}
+
+int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* workspace, gsr_stream_t stream)
+{
+    if (n < 0 || (n > 0 && (!keys || !out_ids || !workspace))) return fail(GSR_ERR_INVALID, "bad depth-sort arguments");
+    if (n == 0) return GSR_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const size_t q = align_up(4 * (size_t)n, 256);
+    uint32_t* k0 = reinterpret_cast<uint32_t*>(workspace);
+    uint32_t* v0 = reinterpret_cast<uint32_t*>(workspace + q);
+    uint32_t* k1 = reinterpret_cast<uint32_t*>(workspace + 2 * q);
+    uint32_t* v1 = reinterpret_cast<uint32_t*>(workspace + 3 * q);
+    // the forward's call (forward_geometry_sort) without the rect gather
+    HIP_TRY(radix_sort(n, DEPTH_BITS, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr, workspace + 4 * q, s));
+    return GSR_OK;
+}
+
 }  // extern "C"

@@ -61,6 +61,9 @@ def _load():
     lib.gsr_adam_update.argtypes = [_vp, _vp, _vp, _vp, _vp, _f, _f, _f, _f, _i, _i, _vp]
     lib.gsr_adam_update_multi.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp]
     lib.gsr_debug_sorted_keys.argtypes = [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]
+    lib.gsr_debug_depth_sort_workspace_size.argtypes = [_i]
+    lib.gsr_debug_depth_sort_workspace_size.restype = _sz
+    lib.gsr_debug_depth_sort.argtypes = [_vp, _i, _vp, _vp, _vp]
     for n in ("gsr_geometry_layout", "gsr_binning_layout"):
         getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
     lib.gsr_image_layout.argtypes = [_i, _i, ctypes.POINTER(_sz), _i]
@@ -620,6 +623,20 @@ def sorted_keys(geomBuffer, binningBuffer, imgBuffer, P, L, W, H):
                                      imgBuffer.data_ptr(), P, L, W, H, keys.data_ptr() if L else None,
                                      vals.data_ptr() if L else None, ranges.data_ptr(), _stream(dev)))
     return keys, vals, ranges
+
+
+def depth_sort(keys):
+    """The forward's depth sort on its own (parity helper): the stable order of the u32 keys
+    (int32 tensor of bit patterns; -1 = culled, sorted last)."""
+    n = keys.numel()
+    ids = torch.empty((n,), dtype=torch.int32, device=keys.device)
+    if n == 0:
+        return ids
+    ws = torch.empty((lib.gsr_debug_depth_sort_workspace_size(n),), dtype=torch.uint8, device=keys.device)
+    keys = keys.contiguous()
+    _check(lib.gsr_debug_depth_sort(keys.data_ptr(), n, ids.data_ptr(), ws.data_ptr(),
+                                    _stream(keys.device)))
+    return ids
 
 
 def fusedssim(C1, C2, img1, img2):

@@ -349,6 +349,14 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
                           uint64_t* keys_out, uint32_t* vals_out, uint32_t* ranges_out,
                           gsr_stream_t stream);
 
+/* Debug / parity helper: the forward's depth sort alone (the first half of the
+ * rasterizer_impl.cu:306-311 key sort): out_ids = the stable order of n u32 keys
+ * (the forward's depth keys: float bit patterns, 0xFFFFFFFF = culled, sorted
+ * last).
+ * workspace: gsr_debug_depth_sort_workspace_size(n) device bytes. */
+size_t gsr_debug_depth_sort_workspace_size(int n);
+int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* workspace, gsr_stream_t stream);
+
 /* Byte offsets of the arrays inside each opaque state buffer (n entries
  * written, count of arrays returned; entry [count] is the total size).  For
  * parity tests and debugging only; the layout is private to this library. */
