@@ -277,6 +277,7 @@ inline BinLayout bin_layout(int L)
 // of 256 rows starts at a multiple of 1 KB, so alignment of the array is alignment of the
 // block), dropping (in) / zero-filling (out) columns at or beyond `ncols`.
 // ---------------------------------------------------------------------------
+constexpr int LDS_IN_BATCH = 6;
 __device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, int ncols, const float* src, int w,
                                             int n)
 {
@@ -285,8 +286,7 @@ __device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, in
     if (((uintptr_t)src & 15) == 0) {
         const int nv4 = total >> 2;
         const float4* s4 = reinterpret_cast<const float4*>(src);
-        for (int f = threadIdx.x; f < nv4; f += blockDim.x) {
-            const float4 v = s4[f];
+        auto put = [&](int f, const float4 v) {
             const float vv[4] = {v.x, v.y, v.z, v.w};
             int g = (4 * f) / w, j = 4 * f - g * w;
 #pragma unroll
@@ -294,7 +294,18 @@ __device__ __forceinline__ void lds_rows_in(float* lds, int stride, int col0, in
                 if (col0 + j < ncols) lds[g * stride + col0 + j] = vv[q];
                 if (++j == w) { j = 0; g++; }
             }
+        };
+        // LDS_IN_BATCH loads in flight per thread before their stores (not one round trip each)
+        const int bd = (int)blockDim.x;
+        int f = threadIdx.x;
+        for (; f + (LDS_IN_BATCH - 1) * bd < nv4; f += LDS_IN_BATCH * bd) {
+            float4 v[LDS_IN_BATCH];
+#pragma unroll
+            for (int u = 0; u < LDS_IN_BATCH; u++) v[u] = s4[f + u * bd];
+#pragma unroll
+            for (int u = 0; u < LDS_IN_BATCH; u++) put(f + u * bd, v[u]);
         }
+        for (; f < nv4; f += bd) put(f, s4[f]);
         e0 = nv4 << 2;
     }
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) {
@@ -367,9 +378,18 @@ __device__ __forceinline__ void lds_copy_in(float* lds, const float* src, int to
 {
     int e0 = 0;
     if (((uintptr_t)src & 15) == 0 && ((uintptr_t)lds & 15) == 0) {
-        const int nv4 = total >> 2;
-        for (int f = threadIdx.x; f < nv4; f += blockDim.x)
-            reinterpret_cast<float4*>(lds)[f] = reinterpret_cast<const float4*>(src)[f];
+        const int nv4 = total >> 2, bd = (int)blockDim.x;
+        const float4* s4 = reinterpret_cast<const float4*>(src);
+        float4* l4 = reinterpret_cast<float4*>(lds);
+        int f = threadIdx.x;
+        for (; f + (LDS_IN_BATCH - 1) * bd < nv4; f += LDS_IN_BATCH * bd) {
+            float4 v[LDS_IN_BATCH];
+#pragma unroll
+            for (int u = 0; u < LDS_IN_BATCH; u++) v[u] = s4[f + u * bd];
+#pragma unroll
+            for (int u = 0; u < LDS_IN_BATCH; u++) l4[f + u * bd] = v[u];
+        }
+        for (; f < nv4; f += bd) l4[f] = s4[f];
         e0 = nv4 << 2;
     }
     for (int e = e0 + threadIdx.x; e < total; e += blockDim.x) lds[e] = src[e];

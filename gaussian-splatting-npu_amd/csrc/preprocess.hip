@@ -85,8 +85,41 @@ __device__ __forceinline__ f3 computeColorFromSH(const f3 pos, int deg, const fl
     return {res[0], res[1], res[2]};
 }
 
+// A Gaussian's own inputs (the same in every view), loaded before the block's SH staging barrier
+// so their round trip overlaps the staging.
+struct GaussIn {
+    f3 p;
+    float4 rot;
+    float scl[3];
+    float opacity;
+    float cov3D[6];  // cov3D_precomp only
+};
+
+__device__ __forceinline__ GaussIn load_gauss(const PreprocessArgs& a, int idx)
+{
+    GaussIn g;
+    g.p = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
+    g.rot = make_float4(0.f, 0.f, 0.f, 0.f);
+    g.scl[0] = g.scl[1] = g.scl[2] = 0.f;
+#pragma unroll
+    for (int k = 0; k < 6; k++) g.cov3D[k] = 0.f;
+    if (!a.cov3D_precomp) {
+        const float* rp = a.rotations + 4 * (size_t)idx;
+        g.rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
+        const float* sp = a.scales + 3 * (size_t)idx;
+        g.scl[0] = sp[0]; g.scl[1] = sp[1]; g.scl[2] = sp[2];
+    } else {
+        const float* c = a.cov3D_precomp + (size_t)idx * 6;
+#pragma unroll
+        for (int k = 0; k < 6; k++) g.cov3D[k] = c[k];
+    }
+    g.opacity = a.opacities[idx];
+    return g;
+}
+
 // One Gaussian; `sh` points at its SH coefficients (global memory or its LDS staging row).
-__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const float* sh0, const float* sh)
+__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx, const GaussIn& gi, const float* sh0,
+                                               const float* sh)
 {
 
     // culled: these four are written here and only here (a visible Gaussian writes them once, below)
@@ -97,17 +130,8 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
         a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
     };
 
-    // Issue every per-Gaussian load up front (one memory round trip instead of one per phase).
-    const f3 p_orig = {a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]};
-    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
-    float scl[3] = {0.f, 0.f, 0.f};
-    if (!a.cov3D_precomp) {
-        const float* rp = a.rotations + 4 * (size_t)idx;
-        rot = make_float4(rp[0], rp[1], rp[2], rp[3]);
-        const float* sp = a.scales + 3 * (size_t)idx;
-        scl[0] = sp[0]; scl[1] = sp[1]; scl[2] = sp[2];
-    }
-    const float opacity_in = a.opacities[idx];
+    const f3 p_orig = gi.p;
+    const float opacity_in = gi.opacity;
     // in_frustum (auxiliary.h:151-176)
     const f3 p_view = transformPoint4x3(p_orig, a.view);
     if (p_view.z <= 0.2f) {
@@ -123,11 +147,10 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     // array forced the local copy into scratch (32 B/lane; 0.099 -> 0.094 ms without it).
     float cov3D[6];
     if (a.cov3D_precomp) {
-        const float* c = a.cov3D_precomp + (size_t)idx * 6;
 #pragma unroll
-        for (int k = 0; k < 6; k++) cov3D[k] = c[k];
+        for (int k = 0; k < 6; k++) cov3D[k] = gi.cov3D[k];
     } else {
-        computeCov3D(scl, a.scale_modifier, rot, cov3D);  // recomputed by preprocess_bwd, not stored
+        computeCov3D(gi.scl, a.scale_modifier, gi.rot, cov3D);  // recomputed by preprocess_bwd, not stored
     }
 
     f3 cov = computeCov2D(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3D, a.view);
@@ -216,9 +239,12 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
     const int V = NV == 1 ? 1 : A.V;
     for (int v = 0; v < V; v++)
         if (idx < A.a[v].scan_status_words) A.a[v].scan_status[idx] = 0;  // the scans run after this kernel
+    // the Gaussian's own inputs first: their loads are in flight during the SH staging
+    GaussIn gi;
+    if (idx < a.P) gi = load_gauss(a, idx);
     auto views = [&](const float* sh0, const float* sh) {
         if (idx >= a.P) return;
-        for (int v = 0; v < V; v++) preprocess_one(A.a[v], idx, sh0, sh);
+        for (int v = 0; v < V; v++) preprocess_one(A.a[v], idx, gi, sh0, sh);
     };
     if (!STAGED) {
         const float* row = a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr;
@@ -247,12 +273,23 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
     const int W3 = a.M * 3;  // multiple of 4 on this path
     const int nv4 = min(256, a.P - base) * (W3 / 4);
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
-    for (int f = threadIdx.x; f < nv4; f += 256) {
+    auto put = [&](int f, const float4 v) {
         const int g = (f * 4) / W3, w = (f * 4) - g * W3;
-        const float4 v = src[f];
         float* d = &s_sh[g * lds_stride + w];
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    };
+    // 12 loads in flight per thread (a whole block at degree 3) before the first LDS store: one
+    // loop iteration per load would wait out 12 round trips
+    constexpr int U = 12;
+    int f = threadIdx.x;
+    for (; f + (U - 1) * 256 < nv4; f += U * 256) {
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = src[f + u * 256];
+#pragma unroll
+        for (int u = 0; u < U; u++) put(f + u * 256, v[u]);
     }
+    for (; f < nv4; f += 256) put(f, src[f]);
     __syncthreads();
     const float* row = s_sh + threadIdx.x * lds_stride;
     views(row, row);

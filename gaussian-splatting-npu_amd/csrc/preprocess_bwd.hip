@@ -801,12 +801,22 @@ __device__ __forceinline__ void staged_sh(const PreprocessBwdArgs& a, float* s_s
         return;
     }
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
-    for (int f = threadIdx.x; f < n * 12; f += blockDim.x) {
+    auto put = [&](int f, const float4 v) {
         const int g = f / 12, j = f - g * 12;
-        const float4 v = src[f];
         float* d = &s_sh[g * SH_STRIDE + 4 * j];
         d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    };
+    // LDS_IN_BATCH loads in flight per thread before their stores (not one round trip each)
+    const int bd = (int)blockDim.x;
+    int f = threadIdx.x;
+    for (; f + (LDS_IN_BATCH - 1) * bd < n * 12; f += LDS_IN_BATCH * bd) {
+        float4 v[LDS_IN_BATCH];
+#pragma unroll
+        for (int u = 0; u < LDS_IN_BATCH; u++) v[u] = src[f + u * bd];
+#pragma unroll
+        for (int u = 0; u < LDS_IN_BATCH; u++) put(f + u * bd, v[u]);
     }
+    for (; f < n * 12; f += bd) put(f, src[f]);
     __syncthreads();
     float* row = s_sh + r * SH_STRIDE;
     work(row, row + 3, 16);
