@@ -256,7 +256,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) r
     // the wave's quadrant (kept in scalar registers during the round, stored once per round)
     __shared__ uint64_t s_hitw[4][BATCH / 64];
 
-    bool done = !inside;
+    float live = inside ? 1.0f : 0.0f;  // 0 once the pixel is finished (or outside the image)
     float T = 1.0f;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
     uint32_t last_contributor = 0;
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) r
     uint32_t next_id = todo > 0 ? a.point_list[range.x + min(tid, todo - 1)] : 0u;
     int flushed = 0;  // entries [0, flushed) have their contribution bits in a.hit
     for (int base = 0; base < todo; base += BATCH) {
-        if (__syncthreads_and(done)) break;
+        if (__syncthreads_and(live == 0.0f)) break;
         if (base > 0) {  // the previous batch's contribution bits (every wave has finished it)
             a.hit[range.x + base - BATCH + tid] = (uint8_t)hit_bits(s_hitw, tid);
             flushed = base;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) r
         // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
         // per 64 entries, then a scalar bit scan; each record is read one entry ahead of use.
         for (int r = 0; r < BATCH / 64; r++) {
-            if (__all(done)) break;
+            if (__all(live == 0.0f)) break;
             const int jr = r * 64 + lane;
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
@@ -298,24 +298,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) r
                 rem &= rem - 1;
                 return jj;
             };
+            // Branch-free blend: every test is a compare feeding a select (no exec-mask branch, no
+            // scalar mask algebra -- the scalar unit, shared by the CU's four SIMDs, is the busier
+            // issue port in this loop).  a = 0 for a finished pixel (live = 0) or power > 0; an
+            // entry that would take T below 1e-4 finishes the pixel without blending
+            // (forward.cu:356-376); ae = the alpha actually blended (0 or a).
             auto blend = [&](int j, const float4 xy, const float4 co, const float4 col) {
                 const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
                 const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
-                bool contrib = !done && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T * (1 - alpha);
-                if (contrib && test_T < 0.0001f) {  // forward.cu:366-370
-                    done = true;
-                    contrib = false;
-                }
-                hitbits |= (uint64_t)(__ballot(contrib) != 0ull) << (j & 63);  // scalar, branch-free
-                if (contrib) {
-                    C0 += col.x * alpha * T;
-                    C1 += col.y * alpha * T;
-                    C2 += col.z * alpha * T;
-                    ID += col.w * alpha * T;
-                    T = test_T;
-                    last_contributor = (uint32_t)(base + j + 1);
-                }
+                const float a = (p2 > 0.0f ? 0.0f : alpha) * live;
+                const bool contrib = a >= 1.0f / 255.0f;
+                const float test_T = T * (1 - a);
+                const bool stop = (contrib ? test_T : 1.0f) < 0.0001f;
+                live = stop ? 0.0f : live;
+                const float ae = stop ? 0.0f : (contrib ? a : 0.0f);
+                const bool blended = ae > 0.0f;
+                hitbits |= __ballot(blended) ? (1ull << (j & 63)) : 0ull;  // scalar select
+                const float aT = ae * T;  // 0 leaves the sums unchanged
+                C0 += col.x * aT;
+                C1 += col.y * aT;
+                C2 += col.z * aT;
+                ID += col.w * aT;
+                T = blended ? test_T : T;
+                last_contributor = blended ? (uint32_t)(base + j + 1) : last_contributor;
             };
             int j = take();
             float4 axy = s_rec[j], aco = s_rec[BATCH + j], acol = s_rec[2 * BATCH + j];
@@ -324,14 +329,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) r
                 const int lb = jb >= 0 ? jb : j;
                 const float4 bxy = s_rec[lb], bco = s_rec[BATCH + lb], bcol = s_rec[2 * BATCH + lb];
                 blend(j, axy, aco, acol);
-                if (jb < 0 || __all(done)) break;
+                if (jb < 0 || __all(live == 0.0f)) break;
                 j = take();
                 const int la = j >= 0 ? j : jb;
                 axy = s_rec[la];
                 aco = s_rec[BATCH + la];
                 acol = s_rec[2 * BATCH + la];
                 blend(jb, bxy, bco, bcol);
-                if (j < 0 || __all(done)) break;
+                if (j < 0 || __all(live == 0.0f)) break;
             }
             if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
         }
