@@ -828,6 +828,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
     r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     r.W = width; r.H = height; r.grid_x = gx;
+    r.T = (int)(gx * gy);
     r.bg = background;
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
@@ -926,6 +927,7 @@ int gsr_backward_render(int P, int R, const float* background, int width, int he
     r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
     r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
     r.W = width; r.H = height; r.grid_x = gx;
+    r.T = T;
     r.bg = background;
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);

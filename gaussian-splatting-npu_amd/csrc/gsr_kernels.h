@@ -61,6 +61,7 @@ struct RenderBwdArgs {
     const uint32_t* point_list;
     int W, H;
     uint32_t grid_x;
+    int T;  // tiles
     const float* bg;
     const float4* splat;
     const float* final_Ts;

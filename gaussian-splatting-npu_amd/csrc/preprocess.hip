@@ -223,6 +223,11 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
 // 3M floats through global memory.  NV > 1: the block's Gaussians for up to NV views of the same
 // Gaussians (a batch of views, gsr_forward_views): their parameters and SH rows are read from HBM
 // once, each view's outputs go to its own buffers (A.a[v]).
+// Threads (Gaussians) per preprocess workgroup.  64 lets the next view's preprocess slip into
+// single-wave holes beside a running render_bwd, but once render_bwd frees 4-wave holes
+// (BWD_TPW) 256 measures as fast (same-box A/B 2,302 vs 2,325 Mpix/s).
+constexpr int PF_TPB = 256;
+
 template <int NV>
 struct PreprocessBatch {
     PreprocessArgs a[NV];
@@ -230,11 +235,11 @@ struct PreprocessBatch {
 };
 
 template <bool STAGED, int NV>
-__global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBatch<NV> A, int lds_stride)
+__global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const PreprocessBatch<NV> A, int lds_stride)
 {
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const PreprocessArgs& a = A.a[0];  // the Gaussian inputs (the same in every view)
-    const int base = blockIdx.x * 256;
+    const int base = blockIdx.x * PF_TPB;
     const int idx = base + (int)threadIdx.x;
     const int V = NV == 1 ? 1 : A.V;
     for (int v = 0; v < V; v++)
@@ -251,9 +256,9 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
         views(row, row);
         return;
     }
-    if (a.dc && a.M <= 16) {  // separate dc, verbatim: dc rows at 0, rest rows (stride 3(M-1)) at 768
-        const int n = min(256, a.P - base), wr = (a.M - 1) * 3;
-        float* s_rest = s_sh + 768;
+    if (a.dc && a.M <= 16) {  // separate dc, verbatim: dc rows at 0, rest rows (stride 3(M-1)) after them
+        const int n = min(PF_TPB, a.P - base), wr = (a.M - 1) * 3;
+        float* s_rest = s_sh + 3 * PF_TPB;
         lds_copy_in(s_sh, a.dc + (size_t)base * 3, n * 3);
         if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
         __syncthreads();
@@ -261,7 +266,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
         return;
     }
     if (a.dc) {  // separate dc, wide rest rows: coefficient 0 into columns 0-2, the rest after it (16 used)
-        const int n = min(256, a.P - base), ncols = min(a.M, 16) * 3;
+        const int n = min(PF_TPB, a.P - base), ncols = min(a.M, 16) * 3;
         lds_rows_in(s_sh, lds_stride, 0, ncols, a.dc + (size_t)base * 3, 3, n);
         if (a.shs && a.M > 1) lds_rows_in(s_sh, lds_stride, 3, ncols, a.shs + (size_t)base * (a.M - 1) * 3,
                                           (a.M - 1) * 3, n);
@@ -271,7 +276,7 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
         return;
     }
     const int W3 = a.M * 3;  // multiple of 4 on this path
-    const int nv4 = min(256, a.P - base) * (W3 / 4);
+    const int nv4 = min(PF_TPB, a.P - base) * (W3 / 4);
     const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * W3);
     auto put = [&](int f, const float4 v) {
         const int g = (f * 4) / W3, w = (f * 4) - g * W3;
@@ -282,14 +287,14 @@ __global__ void __launch_bounds__(256) preprocess_fwd_kernel(const PreprocessBat
     // loop iteration per load would wait out 12 round trips
     constexpr int U = 12;
     int f = threadIdx.x;
-    for (; f + (U - 1) * 256 < nv4; f += U * 256) {
+    for (; f + (U - 1) * PF_TPB < nv4; f += U * PF_TPB) {
         float4 v[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) v[u] = src[f + u * 256];
+        for (int u = 0; u < U; u++) v[u] = src[f + u * PF_TPB];
 #pragma unroll
-        for (int u = 0; u < U; u++) put(f + u * 256, v[u]);
+        for (int u = 0; u < U; u++) put(f + u * PF_TPB, v[u]);
     }
-    for (; f < nv4; f += 256) put(f, src[f]);
+    for (; f < nv4; f += PF_TPB) put(f, src[f]);
     __syncthreads();
     const float* row = s_sh + threadIdx.x * lds_stride;
     views(row, row);
@@ -451,15 +456,15 @@ static hipError_t launch_preprocess_batch(const PreprocessBatch<NV>& A, hipStrea
     const int W3 = a.M * 3;
     const bool staged = a.shs && !a.colors_precomp && W3 > 0 && W3 % 4 == 0 && W3 <= 64 &&
                         ((uintptr_t)a.shs % 16) == 0;
-    const dim3 grid((a.P + 255) / 256), block(256);
+    const dim3 grid((a.P + PF_TPB - 1) / PF_TPB), block(PF_TPB);
     if (a.dc && !a.colors_precomp) {  // separate dc: always staged (any M, any alignment)
         const int stride = (min(a.M, 16) * 3) | 1;
-        const size_t lds = a.M <= 16 ? (768 + 256 * (size_t)(a.M - 1) * 3) * sizeof(float)
-                                     : 256 * stride * sizeof(float);
+        const size_t lds = a.M <= 16 ? ((size_t)PF_TPB * 3 + PF_TPB * (size_t)(a.M - 1) * 3) * sizeof(float)
+                                     : PF_TPB * stride * sizeof(float);
         hipLaunchKernelGGL((preprocess_fwd_kernel<true, NV>), grid, block, lds, s, A, stride);
     } else if (staged) {
         const int stride = W3 | 1;
-        hipLaunchKernelGGL((preprocess_fwd_kernel<true, NV>), grid, block, 256 * stride * sizeof(float), s, A,
+        hipLaunchKernelGGL((preprocess_fwd_kernel<true, NV>), grid, block, PF_TPB * stride * sizeof(float), s, A,
                            stride);
     } else {
         hipLaunchKernelGGL((preprocess_fwd_kernel<false, NV>), grid, block, 0, s, A, 0);

@@ -496,14 +496,25 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 // contiguous floats each) at their emission slots and flag them valid; entries that survive
 // no quadrant get no record.  No atomics:
 // per-(tile, Gaussian) sums are bitwise reproducible.
+// Tiles (independent waves) per workgroup.  A retiring 4-wave workgroup frees one wave slot on
+// each SIMD of its CU -- the footprint of a 256-thread binning-prefix workgroup of the next view
+// (depth sort, scans, emission, tile sort), which then runs beside this launch instead of
+// waiting for its last wave; single-wave workgroups left no such hole (a freed slot was refilled
+// by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
+// 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
+constexpr int BWD_TPW = 4;
+
 template <bool HAS_INV>
-__global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
+__global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(RenderBwdArgs a)
 {
 #pragma clang fp contract(fast)
     constexpr int G = 3;  // Gaussians per transposed reduction (3 x 10 gradient terms <= 32 values)
-    const uint32_t tile = a.tile_order[blockIdx.x];
+    const int wv = BWD_TPW == 1 ? 0 : (int)(threadIdx.x >> 6);
+    const int ti = (int)blockIdx.x * BWD_TPW + wv;
+    if (ti >= a.T) return;  // waves are independent: no workgroup barrier below
+    const uint32_t tile = a.tile_order[ti];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
-    const int lane = threadIdx.x;
+    const int lane = (int)(threadIdx.x & 63);
     const uint2 range = a.ranges[tile];
     const size_t HW = (size_t)a.H * a.W;
     const float px0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
@@ -561,8 +572,10 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(RenderBwdArgs a)
     }
     const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
 
-    __shared__ float4 s_rec[3][64];
-    __shared__ uint8_t s_list[64];
+    __shared__ float4 s_recw[BWD_TPW][3][64];
+    __shared__ uint8_t s_listw[BWD_TPW][64];
+    float4 (&s_rec)[3][64] = s_recw[wv];
+    uint8_t (&s_list)[64] = s_listw[wv];
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
@@ -681,10 +694,12 @@ hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
+    if (a.T != T) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)((T + BWD_TPW - 1) / BWD_TPW)), block(64 * BWD_TPW);
     if (a.dL_invdepths)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, dim3(T), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(render_bwd_kernel<true>, grid, block, 0, s, a);
     else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, dim3(T), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(render_bwd_kernel<false>, grid, block, 0, s, a);
     return hipGetLastError();
 }
 
