@@ -72,11 +72,13 @@ def parse():
                     help="render the views of a step one after the other on one stream")
     ap.add_argument("--no-prefix-stream", action="store_true",
                     help="run the forward's binning prefix on the caller's stream, not the library's priority stream")
-    ap.add_argument("--batch-views", action="store_true",
-                    help="render this rank's views as one MultiViewRasterizer batch (one backward preprocess pass)")
+    ap.add_argument("--per-view", dest="batch_views", action="store_false",
+                    help="render the views one GaussianRasterizer call at a time (alternating over two streams, "
+                         "deferred_backward) instead of the default: this rank's views as ONE MultiViewRasterizer "
+                         "batch (binning prefix batched over the views, one backward preprocess pass)")
     ap.add_argument("--no-deferred", dest="deferred", action="store_false",
-                    help="every view's full backward on its own (default: per-view render backward, ONE batched "
-                         "preprocess backward per step, dgr.deferred_backward)")
+                    help="--per-view: every view's full backward on its own (default: per-view render backward, "
+                         "ONE batched preprocess backward per step, dgr.deferred_backward)")
     ap.add_argument("--order", choices=("interleave", "lookahead", "forward-first"), default="interleave",
                     help="issue order of the step's views: forward+backward per view, the next view's forward "
                          "before this view's backward, or every forward before every backward")
@@ -242,15 +244,12 @@ def main():
                                    opacities=params["opacities"], scales=params["scales"],
                                    rotations=params["rotations"])
             torch.autograd.backward([color, inv], [gc_batch, gi_batch])
-            nbytes = multiview.allreduce_grads(params)
-            if record_allreduce:
-                raise RuntimeError("--batch-views: all-reduce events not recorded")
-            return
-        n_st = len(streams) if overlap else 1
-        for st in streams[1:n_st]:
-            st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
-        with (dgr.deferred_backward() if args.deferred else contextlib.nullcontext()):
-            views_loop(n_st)
+        else:
+            n_st = len(streams) if overlap else 1
+            for st in streams[1:n_st]:
+                st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
+            with (dgr.deferred_backward() if args.deferred else contextlib.nullcontext()):
+                views_loop(n_st)
         if record_allreduce:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -371,7 +370,11 @@ def main():
 
     roofline = None
     if kern:
-        ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if args.deferred else 1)
+        batched_bwd = args.batch_views or args.deferred
+        ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if batched_bwd else 1)
+        if args.batch_views:  # the batched binning prefix: one launch per VIEW_BATCH (8) views
+            for k in ("preprocess_fwd", "depth_sort", "scan", "emit_instances", "tile_sort", "tile_ranges"):
+                ab[k] *= min(len(cams), 8)
         # the dominant kernel: the largest share of the step (mean launch time x launches per step)
         dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
@@ -456,9 +459,14 @@ def main():
         "config": {"workload": workload, "P": P, "width": W, "height": H, "views_per_step": views_step,
                    "views_per_rank": len(views), "num_rendered": L, "num_rendered_per_view": Ls,
                    "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}",
-                   "execution": ("views alternating over 2 HIP streams" if args.overlap else "views on one stream")
-                   + ("; per view forward + render backward, one batched preprocess backward per step "
-                      "(deferred_backward)" if args.deferred else "; per view forward + full backward")},
+                   "execution": ("one MultiViewRasterizer batch: the binning prefix of all views batched "
+                                 "(one launch per stage, grid.y = view), then every view's render forward, every "
+                                 "view's render backward, one preprocess backward for the batch"
+                                 if args.batch_views else
+                                 ("views alternating over 2 HIP streams" if args.overlap else "views on one stream")
+                                 + ("; per view forward + render backward, one batched preprocess backward per "
+                                    "step (deferred_backward)" if args.deferred
+                                    else "; per view forward + full backward"))},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "aux": aux,

@@ -518,6 +518,31 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
                                height, out_color, depth, debug, stream, false, ps);
 }
 
+// render_fwd's arguments for a view whose binning is complete
+static RenderFwdArgs render_fwd_args(char* gb, char* bb, char* ib, int P, int L, const float* background, int width,
+                                     int height, float* out_color, float* depth)
+{
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const BinLayout b = bin_layout(L);
+    RenderFwdArgs r;
+    r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    r.tile_work = at<uint32_t>(ib, im.off[IMG_TILE_WORK]);
+    r.point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
+    r.W = width; r.H = height;
+    r.grid_x = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+    r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
+    r.bg = background;
+    r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
+    r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
+    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
+    r.out_color = out_color;
+    r.invdepth = depth;
+    r.hit = L > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
+    return r;
+}
+
 // Forward, second half.  `emitted`: the early emission (gsr_forward_prealloc_dc) already wrote the
 // instances into this binning buffer.
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
@@ -590,20 +615,7 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
         if (rc) return rc;
     }
     s = caller;
-    RenderFwdArgs r;
-    r.ranges = ranges;
-    r.tile_order = tile_order;
-    r.tile_work = at<uint32_t>(ib, im.off[IMG_TILE_WORK]);
-    r.point_list = point_list;
-    r.W = width; r.H = height; r.grid_x = gx;
-    r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
-    r.bg = background;
-    r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
-    r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
-    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
-    r.out_color = out_color;
-    r.invdepth = depth;
-    r.hit = L > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
+    const RenderFwdArgs r = render_fwd_args(gb, bb, ib, P, L, background, width, height, out_color, depth);
     {
         ProfScope ps_(PK_RENDER_FWD, s);
         HIP_TRY(launch_render_fwd(r, T, s));
@@ -696,6 +708,31 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     return GSR_OK;
 }
 
+// Tile-sort job of one view whose instances were emitted into binning buffer bb (layout of L):
+// the emission arrays and ping-pong buffers live in the not yet used gradient-record region.
+static SortJob tile_sort_job(char* bb, int L)
+{
+    const BinLayout b = bin_layout(L);
+    const size_t q = align_up(4 * (size_t)L, 256);
+    char* w = bb + b.off[BIN_GRAD_INST];
+    SortJob j;
+    j.n = L;
+    j.keys_in = reinterpret_cast<const uint32_t*>(w);                  // tile keys (emission)
+    j.pairs = reinterpret_cast<const uint2*>(w + 8 * q);               // (record slot, Gaussian id)
+    j.k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
+    j.k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
+    j.v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
+    j.v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
+    j.out_x = at<uint32_t>(bb, b.off[BIN_SLOT]);
+    j.out_y = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
+    j.sorted_keys = at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
+    j.scratch = bb + b.off[BIN_RADIX_SCRATCH];
+    j.rects = nullptr;
+    j.sorted_rects = nullptr;
+    j.sorted_counts = nullptr;
+    return j;
+}
+
 int gsr_forward_views(int V, int P, int D, int M, const float* background, int width, int height,
                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
@@ -716,77 +753,128 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     }
     if (P <= 0) return P < 0 ? fail(GSR_ERR_INVALID, "P must be >= 0") : GSR_OK;
     hipStream_t caller = (hipStream_t)stream;
-    const int n = V < PREFIX_STREAMS ? V : PREFIX_STREAMS;
-    hipStream_t ps[PREFIX_STREAMS];
-    int rc = prefix_fork(caller, n, ps);
-    if (rc) return rc;
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    const int T = (int)(gx * gy);
     const GeomLayout g = geom_layout(P);
     const ImageLayout im = image_layout(width, height);
 
     uint32_t* h[MAX_VIEWS];
-    // 1. ONE preprocess launch per 8 views on prefix stream 0 (the Gaussians' parameters and SH rows
-    //    read once for all of them), then view v's depth sort, scans and early emission on prefix
-    //    stream v mod n: the short latency-bound launch chains of the views run side by side.
     PreprocessArgs pa[MAX_VIEWS];
     uint32_t* hdev[MAX_VIEWS];
-    for (int v = 0; v < V && !rc; v++) {
+    for (int v = 0; v < V; v++) {
         if (!geometry_buffers[v] || !image_buffers[v]) return fail(GSR_ERR_ALLOC, "null state buffer");
         if (!out_colors[v] || !out_invdepths[v]) return fail(GSR_ERR_INVALID, "null per-view output");
-        rc = forward_geometry_args(geometry_buffers[v], image_buffers[v], P, D, M, width, height, means3D, dc, shs,
-                                   colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
-                                   viewmatrices[v], projmatrices[v], campos[v], tan_fovx[v], tan_fovy[v], prefiltered,
-                                   antialiasing, radii ? radii[v] : nullptr, v, &pa[v], &h[v], &hdev[v]);
+        const int rc = forward_geometry_args(geometry_buffers[v], image_buffers[v], P, D, M, width, height, means3D, dc,
+                                             shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                                             cov3D_precomp, viewmatrices[v], projmatrices[v], campos[v], tan_fovx[v],
+                                             tan_fovy[v], prefiltered, antialiasing, radii ? radii[v] : nullptr, v,
+                                             &pa[v], &h[v], &hdev[v]);
+        if (rc) return rc;
     }
+    // The binning prefix of all V views, batched: every stage is one launch over all views
+    // (grid.y = view), on one high-priority prefix stream; the renders follow on the caller's.
+    hipStream_t ps = nullptr;
+    int rc = prefix_begin(caller, &ps);
     if (rc) return rc;
     {
-        ProfScope ps_(PK_PREPROCESS, ps[0]);
-        HIP_TRY(launch_preprocess_views(pa, V, ps[0]));
+        ProfScope ps_(PK_PREPROCESS, ps);
+        HIP_TRY(launch_preprocess_views(pa, V, ps));  // the parameters and SH rows read once per 8 views
     }
-    DEBUG_SYNC(ps[0]);
-    if (n > 1) {
-        PrefixStream& pst = g_prefix[0 <= current_device() && current_device() < MAX_DEVICES ? current_device() : 0];
-        HIP_TRY(hipEventRecord(pst.fork, ps[0]));
-        for (int k = 1; k < n; k++) HIP_TRY(hipStreamWaitEvent(ps[k], pst.fork, 0));
-    }
-    for (int v = 0; v < V && !rc; v++) {
-        const hipStream_t s = ps[v % n];
+    DEBUG_SYNC(ps);
+    ScanJob rec[MAX_VIEWS], off[MAX_VIEWS];
+    SortJob dsort[MAX_VIEWS];
+    EmitJob emit[MAX_VIEWS];
+    int ne = 0;
+    for (int v = 0; v < V; v++) {
         char* gb = geometry_buffers[v];
-        rc = forward_geometry_sort(pa[v], gb, P, hdev[v], s, debug, n == 1);
-        if (rc) break;
-        if (binning_buffers[v] && binning_capacity[v] > 0) {
-            ProfScope ps_(PK_EMIT, s);
-            HIP_TRY(launch_emit_instances_early(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
-                                                at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
-                                                at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx,
-                                                at<uint32_t>(gb, g.off[GEOM_EMIT_START]), binning_buffers[v],
-                                                binning_capacity[v], at<uint2>(image_buffers[v], im.off[IMG_RANGES]),
-                                                (int)(gx * gy), s));
-        }
+        const PreprocessArgs& a = pa[v];
+        // each Gaussian's first gradient-record slot (index-order exclusive scan of the tile counts)
+        rec[v] = {a.tiles_touched, at<uint32_t>(gb, g.off[GEOM_EMIT_START]), P, a.scan_status + scan_status_words(P),
+                  nullptr};
+        char* tmp = gb + g.off[GEOM_DSORT_TMP];
+        const size_t q = align_up(4 * (size_t)P, 256);
+        dsort[v] = {P, a.dkey, nullptr, reinterpret_cast<uint32_t*>(tmp), reinterpret_cast<uint32_t*>(tmp + q),
+                    reinterpret_cast<uint32_t*>(tmp + 2 * q), reinterpret_cast<uint32_t*>(tmp + 3 * q),
+                    at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH], a.rect,
+                    at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])};
+        uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+        off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
+        if (binning_buffers[v] && binning_capacity[v] > 0)
+            emit[ne++] = {P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), offsets, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
+                          at<uint32_t>(gb, g.off[GEOM_EMIT_START]), nullptr, nullptr, nullptr,
+                          at<uint2>(image_buffers[v], im.off[IMG_RANGES]), binning_buffers[v], binning_capacity[v]};
     }
-    // 2. in view order: num_rendered read back, the view's tile sort on its prefix stream and its
-    //    render on the caller's stream (views whose binning buffer is too small are left to the
-    //    caller: allocate gsr_binning_buffer_size(num_rendered[v]), then gsr_forward_render)
+    HIP_TRY(launch_scan_batch(rec, V, true, ps));
+    {
+        ProfScope ps_(PK_DEPTH_SORT, ps);
+        HIP_TRY(radix_sort_batch(dsort, V, DEPTH_BITS, ps));
+    }
+    {
+        ProfScope ps_(PK_SCAN, ps);
+        HIP_TRY(launch_scan_batch(off, V, false, ps));
+    }
+    if (ne) {  // before the read-back: resolves its arrays from the device-side totals
+        ProfScope ps_(PK_EMIT, ps);
+        HIP_TRY(launch_emit_batch(emit, ne, gx, T, ps));
+    }
+    DEBUG_SYNC(ps);
+    // the one host hand-off: every view's num_rendered (rasterizer_impl.cu:283-284)
+    int L[MAX_VIEWS];
     for (int v = 0; v < V && !rc; v++) {
-        const hipStream_t s = ps[v % n];
-        int L = 0;
-        rc = forward_geometry_wait(h[v], s, &L);
-        num_rendered[v] = L;
-        if (rc) break;
-        const bool early = binning_buffers[v] && binning_capacity[v] > 0;
-        if (early && gsr_binning_buffer_size(L) <= binning_capacity[v]) {
-            rc = forward_render_impl(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L, background,
-                                     width, height, out_colors[v], out_invdepths[v], debug, stream, L > 0, s);
-            if (rc) break;
-            rendered[v] = 1;
+        rc = forward_geometry_wait(h[v], ps, &L[v]);
+        num_rendered[v] = L[v];
+    }
+    if (rc) {
+        prefix_end(caller, ps);
+        return rc;
+    }
+    // views whose binning buffer holds them: tile sort, tile ranges and tile order, batched (the
+    // others are left to the caller: allocate gsr_binning_buffer_size(num_rendered[v]), then
+    // gsr_forward_render)
+    int fit[MAX_VIEWS], nf = 0;
+    SortJob tsort[MAX_VIEWS];
+    RangesJob rj[MAX_VIEWS];
+    OrderJob oj[MAX_VIEWS];
+    int ns = 0;
+    for (int v = 0; v < V; v++) {
+        if (!binning_buffers[v] || binning_capacity[v] == 0 || gsr_binning_buffer_size(L[v]) > binning_capacity[v])
+            continue;
+        char* bb = binning_buffers[v];
+        char* ib = image_buffers[v];
+        const BinLayout b = bin_layout(L[v]);
+        if (L[v] > 0) tsort[ns++] = tile_sort_job(bb, L[v]);
+        rj[nf] = {L[v], L[v] > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr, at<uint2>(ib, im.off[IMG_RANGES])};
+        oj[nf] = {at<uint2>(ib, im.off[IMG_RANGES]), nullptr, at<uint32_t>(ib, im.off[IMG_TILE_ORDER])};
+        fit[nf++] = v;
+    }
+    if (ns) {
+        ProfScope ps_(PK_TILE_SORT, ps);
+        HIP_TRY(radix_sort_batch(tsort, ns, (int)higher_msb((uint32_t)T), ps));
+    }
+    if (nf) {
+        {
+            ProfScope ps_(PK_RANGES, ps);
+            HIP_TRY(launch_tile_ranges_batch(rj, nf, T, ps));
         }
+        ProfScope ps_(PK_TILE_ORDER, ps);
+        HIP_TRY(launch_tile_order_batch(oj, nf, T, ps));
     }
-    for (int k = 0; k < n; k++) {  // everything the prefix streams wrote is ordered before the caller's next work
-        const int rj = prefix_end(caller, ps[k]);
-        if (!rc) rc = rj;
+    DEBUG_SYNC(ps);
+    rc = prefix_end(caller, ps);
+    if (rc) return rc;
+    for (int k = 0; k < nf; k++) {
+        const int v = fit[k];
+        const RenderFwdArgs r = render_fwd_args(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L[v],
+                                                background, width, height, out_colors[v], out_invdepths[v]);
+        {
+            ProfScope ps_(PK_RENDER_FWD, caller);
+            HIP_TRY(launch_render_fwd(r, T, caller));
+        }
+        DEBUG_SYNC(caller);
+        rendered[v] = 1;
     }
-    return rc;
+    return GSR_OK;
 }
 
 int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int width, int height,

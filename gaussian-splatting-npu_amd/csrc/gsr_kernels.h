@@ -190,6 +190,71 @@ int scan_status_words(int n);
 hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uint32_t* out, int n, uint64_t* status,
                                  uint32_t* total_out, hipStream_t s, bool exclusive = false);
 
+// Batched prefix launches (gsr_forward_views): up to VIEW_BATCH views per launch, view =
+// blockIdx.y, each with its own arrays and sizes (workgroups past a view's size exit at once).
+// One launch per step over all views replaces V launches of a few hundred workgroups each: the
+// latency-bound prefix kernels of one 1M-Gaussian view fill a fraction of the chip.
+constexpr int VIEW_BATCH = 8;
+template <typename A>
+struct ViewBatch {
+    A v[VIEW_BATCH];
+    int n;
+};
+
+struct ScanJob {  // launch_inclusive_scan's arguments for one view
+    const uint32_t* in;
+    uint32_t* out;
+    int n;
+    uint64_t* status;
+    uint32_t* total_out;
+};
+hipError_t launch_scan_batch(const ScanJob* jobs, int V, bool exclusive, hipStream_t s);
+
+struct SortJob {  // radix_sort's arguments for one view
+    int n;
+    const uint32_t* keys_in;
+    const uint2* pairs;
+    uint32_t *k0, *v0, *k1, *v1;
+    uint32_t *out_x, *out_y, *sorted_keys;
+    char* scratch;
+    const uint2* rects;
+    uint2* sorted_rects;
+    uint32_t* sorted_counts;
+};
+// V independent stable sorts over the same bit width, pass by pass in shared launches.
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s);
+
+struct EmitJob {  // emission of one view (bb != null: the early form, arrays resolved on the device)
+    int P;
+    const uint32_t* sorted_ids;
+    const uint32_t* offsets_d;
+    const uint2* sorted_rects;
+    const uint32_t* rec_start;
+    uint32_t* tile_keys;
+    uint2* pairs;
+    uint32_t* valid;
+    uint2* ranges;
+    char* bb;
+    size_t capacity;
+};
+hipError_t launch_emit_batch(const EmitJob* jobs, int V, uint32_t gx, int T, hipStream_t s);
+
+struct RangesJob {
+    int L;
+    const uint32_t* sorted_tiles;
+    uint2* ranges;
+};
+// views with L == 0 get their ranges zeroed (no emission cleared them)
+hipError_t launch_tile_ranges_batch(const RangesJob* jobs, int V, int T, hipStream_t s);
+
+struct OrderJob {
+    const uint2* ranges;
+    const uint32_t* work;
+    uint32_t* order;
+};
+// every job with ranges (the forward's order) or every job with work (the backward's)
+hipError_t launch_tile_order_batch(const OrderJob* jobs, int V, int T, hipStream_t s);
+
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,

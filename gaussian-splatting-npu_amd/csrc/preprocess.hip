@@ -374,10 +374,25 @@ __device__ __forceinline__ uint32_t scan_lookback(uint64_t* status, int c, int l
 
 // Inclusive (or, with `exclusive`, exclusive) scan of in[gather[i]] into out; the total goes to
 // total_out (may be null).
-__global__ void __launch_bounds__(256) scan_lookback_kernel(const uint32_t* in, const uint32_t* gather, int n,
-                                                            int nchunks, uint64_t* status, uint32_t* out,
-                                                            uint32_t* total_out, bool exclusive)
+struct ScanKArgs {
+    const uint32_t* in;
+    const uint32_t* gather;
+    int n, nchunks;
+    uint64_t* status;
+    uint32_t* out;
+    uint32_t* total_out;
+};
+__global__ void __launch_bounds__(256) scan_lookback_kernel(const ViewBatch<ScanKArgs> B, bool exclusive)
 {
+    const ScanKArgs& J = B.v[blockIdx.y];
+    const int nchunks = J.nchunks;
+    if ((int)blockIdx.x >= nchunks) return;  // past this view's chunks (uniform, before taking a ticket)
+    const uint32_t* in = J.in;
+    const uint32_t* gather = J.gather;
+    const int n = J.n;
+    uint64_t* status = J.status;
+    uint32_t* out = J.out;
+    uint32_t* total_out = J.total_out;
     __shared__ uint32_t lds4[4];
     __shared__ uint32_t s_chunk, s_excl;
     uint32_t* ticket = reinterpret_cast<uint32_t*>(status + nchunks);
@@ -506,9 +521,32 @@ hipError_t launch_inclusive_scan(const uint32_t* in, const uint32_t* gather, uin
 {
     if (n <= 0) return hipSuccess;
     const int nb = (n + SCAN_ITEMS - 1) / SCAN_ITEMS;
-    hipLaunchKernelGGL(scan_lookback_kernel, dim3(nb), dim3(256), 0, s, in, gather, n, nb, status, out, total_out,
-                       exclusive);
+    ViewBatch<ScanKArgs> B;
+    B.n = 1;
+    B.v[0] = {in, gather, n, nb, status, out, total_out};
+    hipLaunchKernelGGL(scan_lookback_kernel, dim3(nb), dim3(256), 0, s, B, exclusive);
     return hipGetLastError();
+}
+
+hipError_t launch_scan_batch(const ScanJob* jobs, int V, bool exclusive, hipStream_t s)
+{
+    for (int v0 = 0; v0 < V; v0 += VIEW_BATCH) {
+        const int nv = min(VIEW_BATCH, V - v0);
+        ViewBatch<ScanKArgs> B;
+        B.n = nv;
+        int maxc = 0;
+        for (int v = 0; v < nv; v++) {
+            const ScanJob& j = jobs[v0 + v];
+            const int nb = j.n > 0 ? (j.n + SCAN_ITEMS - 1) / SCAN_ITEMS : 0;
+            B.v[v] = {j.in, nullptr, j.n, nb, j.status, j.out, j.total_out};
+            maxc = max(maxc, nb);
+        }
+        if (maxc == 0) continue;
+        hipLaunchKernelGGL(scan_lookback_kernel, dim3((unsigned)maxc, (unsigned)nv), dim3(256), 0, s, B, exclusive);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 }  // namespace gsr

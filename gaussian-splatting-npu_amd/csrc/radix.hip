@@ -36,11 +36,19 @@ constexpr int RS_MAXBINS = 256;
 
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
-// (1) counts[d * nchunks + c] = number of elements of chunk c with digit d.
+// (1) counts[d * nchunks + c] = number of elements of chunk c with digit d (view blockIdx.y).
+struct CountJob {
+    const uint32_t* keys;
+    int n, nchunks;
+    uint32_t* counts;
+};
 template <int ITEMS>
-__global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t* keys, int n, int shift, int nbits,
-                                                                int nchunks, uint32_t* counts)
+__global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
+    const CountJob& J = B.v[blockIdx.y];
+    if ((int)blockIdx.x >= J.nchunks) return;  // past this view's chunks (uniform)
+    const uint32_t* keys = J.keys;
+    const int n = J.n;
     __shared__ uint32_t h[4][RS_MAXBINS];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t nb = 1u << nbits, mask = nb - 1u;
@@ -66,13 +74,22 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const uint32_t*
             if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
     }
     __syncthreads();
-    if ((uint32_t)tid < nb) counts[(size_t)tid * nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    if ((uint32_t)tid < nb)
+        J.counts[(size_t)tid * J.nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
 // (2) one workgroup per digit: exclusive scan of counts[d, 0..nchunks) in place; the row total
 // goes to totals[d].
-__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(uint32_t* counts, int nchunks, uint32_t* totals)
+struct RowJob {
+    uint32_t* counts;
+    int nchunks;
+    uint32_t* totals;
+};
+__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBatch<RowJob> B)
 {
+    uint32_t* counts = B.v[blockIdx.y].counts;
+    const int nchunks = B.v[blockIdx.y].nchunks;
+    uint32_t* totals = B.v[blockIdx.y].totals;
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -105,9 +122,11 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(uint32_t* cou
 // serially, and one block-wide scan of the segment sums joins them -- one global round trip and
 // two barriers instead of three barriers per 256 chunks.
 constexpr int RS_ROW_LDS = 12288;
-__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(uint32_t* counts, int nchunks,
-                                                                       uint32_t* totals)
+__global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const ViewBatch<RowJob> RB)
 {
+    uint32_t* counts = RB.v[blockIdx.y].counts;
+    const int nchunks = RB.v[blockIdx.y].nchunks;
+    uint32_t* totals = RB.v[blockIdx.y].totals;
     __shared__ uint32_t s_row[RS_ROW_LDS];
     __shared__ uint32_t s_wave[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -190,8 +209,10 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
 template <int ITEMS, bool PAIR>
-__global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs a)
+__global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
+    const SortPassArgs& a = B.v[blockIdx.y];
+    if ((int)blockIdx.x >= a.nchunks) return;  // past this view's chunks (uniform)
     constexpr int TILE = RS_THREADS * ITEMS;
     using Val = typename std::conditional<PAIR, uint2, uint32_t>::type;
     __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
@@ -313,12 +334,20 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(SortPassArgs 
 // arrays are resolved here from the device-side total (offsets_d[P-1]) with the binning layout
 // the host will use; if that layout does not fit in `capacity` bytes, nothing is written (the
 // host then allocates the exact size and emits again).
-__global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32_t* sorted_ids,
-                                                             const uint32_t* offsets_d, const uint2* sorted_rects,
-                                                             uint32_t gx, uint32_t* tile_keys, uint2* pairs,
-                                                             const uint32_t* rec_start, uint32_t* valid, uint2* ranges,
-                                                             int T, char* bb, size_t capacity)
+__global__ void __launch_bounds__(256) emit_instances_kernel(const ViewBatch<EmitJob> B, uint32_t gx, int T)
 {
+    const EmitJob& J = B.v[blockIdx.y];
+    const int P = J.P;
+    const uint32_t* sorted_ids = J.sorted_ids;
+    const uint32_t* offsets_d = J.offsets_d;
+    const uint2* sorted_rects = J.sorted_rects;
+    const uint32_t* rec_start = J.rec_start;
+    uint32_t* tile_keys = J.tile_keys;
+    uint2* pairs = J.pairs;
+    uint32_t* valid = J.valid;
+    uint2* ranges = J.ranges;
+    char* bb = J.bb;
+    const size_t capacity = J.capacity;
     __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64], s_rec[4][64];
     if (bb) {
         const size_t n = offsets_d[P - 1];
@@ -376,8 +405,12 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(int P, const uint32
 // identifyTileRanges (rasterizer_impl.cu:116-138): four consecutive instances per thread (one
 // 16-byte load); each element's predecessor comes from the same load or, for the first, from the
 // neighbouring lane (the wave's first lane loads it).
-__global__ void __launch_bounds__(256) tile_ranges_kernel(int L, const uint32_t* sorted_tiles, uint2* ranges)
+__global__ void __launch_bounds__(256) tile_ranges_kernel(const ViewBatch<RangesJob> B)
 {
+    const int L = B.v[blockIdx.y].L;
+    const uint32_t* sorted_tiles = B.v[blockIdx.y].sorted_tiles;
+    uint2* ranges = B.v[blockIdx.y].ranges;
+    if ((int)blockIdx.x * 256 * 4 >= L) return;  // past this view's instances (uniform)
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int lane = threadIdx.x & 63;
     const int i0 = 4 * t;
@@ -436,65 +469,114 @@ static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 20
 // pairs); the last pass writes out_x[dst] = i (pairs[i].x), out_y[dst] = pairs[i].y and
 // sorted_keys[dst] = key (any of them may be null); without pairs it can also lay out rects[i]
 // and their tile counts in sorted order.  All writes are contiguous runs: no scattered stores.
+// radix_sort_batch: V such sorts (one per view, same bit width and pairing), each pass's three
+// kernels launched once for all of them (grid.y = view).
+template <typename F>
+static hipError_t for_groups(int V, F f)
+{
+    for (int v0 = 0; v0 < V; v0 += VIEW_BATCH) {
+        const hipError_t e = f(v0, min(VIEW_BATCH, V - v0));
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+static inline uint32_t* sort_counts(const SortJob& j) { return reinterpret_cast<uint32_t*>(j.scratch); }
+static inline uint32_t* sort_totals(const SortJob& j)
+{
+    return reinterpret_cast<uint32_t*>(j.scratch + align_up(rs_chunks(j.n) * RS_MAXBINS * 4 + 256, 256));
+}
+
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s)
+{
+    if (nbits < 1) nbits = 1;
+    const int npass = (nbits + 7) / 8;
+    return for_groups(V, [&](int v0, int nv) -> hipError_t {
+        int maxc = 0;
+        bool pair = false;
+        for (int v = 0; v < nv; v++) {
+            maxc = max(maxc, (int)rs_chunks(jobs[v0 + v].n));
+            pair = jobs[v0 + v].pairs != nullptr;
+        }
+        if (maxc == 0) return hipSuccess;
+        const uint32_t* kin[VIEW_BATCH];
+        const uint32_t* vin[VIEW_BATCH];
+        for (int v = 0; v < nv; v++) {
+            kin[v] = jobs[v0 + v].keys_in;
+            vin[v] = reinterpret_cast<const uint32_t*>(jobs[v0 + v].pairs);
+        }
+        int shift = 0;
+        for (int p = 0; p < npass; p++) {
+            const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
+            const bool last = p == npass - 1;
+            ViewBatch<CountJob> cb;
+            ViewBatch<RowJob> rb;
+            ViewBatch<SortPassArgs> sb;
+            cb.n = rb.n = sb.n = nv;
+            for (int v = 0; v < nv; v++) {
+                const SortJob& j = jobs[v0 + v];
+                const int nchunks = (int)rs_chunks(j.n);
+                cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j)};
+                rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
+                SortPassArgs& a = sb.v[v];
+                a.n = j.n;
+                a.shift = shift;
+                a.nbits = w;
+                a.nchunks = nchunks;
+                a.keys_in = kin[v];
+                a.vals_in = vin[v];
+                a.keys_out = last ? nullptr : ((p & 1) ? j.k1 : j.k0);
+                a.vals_out = last ? nullptr : ((p & 1) ? j.v1 : j.v0);
+                a.out_x = j.out_x;
+                a.out_y = j.out_y;
+                a.sorted_keys = j.sorted_keys;
+                a.rects = (last && !pair) ? j.rects : nullptr;
+                a.sorted_rects = j.sorted_rects;
+                a.sorted_counts = j.sorted_counts;
+                a.row_prefix = sort_counts(j);
+                a.totals = sort_totals(j);
+                kin[v] = a.keys_out;
+                vin[v] = a.vals_out;
+            }
+            const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
+            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS>, g, b, 0, s, cb, shift, w);
+            if (maxc <= RS_ROW_LDS)
+                hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+            else
+                hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, sb);
+            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false>), g, b, 0, s, sb);
+            shift += w;
+        }
+        return hipGetLastError();
+    });
+}
+
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects, uint2* sorted_rects, uint32_t* sorted_counts)
 {
-    const bool pair = pairs != nullptr;
     if (n <= 0) return hipSuccess;
-    const int nchunks = (int)rs_chunks(n);
-    uint32_t* counts = reinterpret_cast<uint32_t*>(scratch);
-    uint32_t* totals = reinterpret_cast<uint32_t*>(scratch + align_up((size_t)nchunks * RS_MAXBINS * 4 + 256, 256));
-    if (nbits < 1) nbits = 1;
-    const int npass = (nbits + 7) / 8;
-    const uint32_t* kin = keys_in;
-    const uint32_t* vin = reinterpret_cast<const uint32_t*>(pairs);
-    int shift = 0;
-    for (int p = 0; p < npass; p++) {
-        const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
-        const bool last = p == npass - 1;
-        const bool shrt = rs_items(n) == RS_ITEMS_SHORT;
-        if (shrt)
-            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS_SHORT>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s,
-                               kin, n, shift, w, nchunks, counts);
-        else
-            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS>, dim3((unsigned)nchunks), dim3(RS_THREADS), 0, s, kin,
-                               n, shift, w, nchunks, counts);
-        if (nchunks <= RS_ROW_LDS)
-            hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks,
-                               totals);
-        else
-            hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w), dim3(RS_THREADS), 0, s, counts, nchunks, totals);
-        SortPassArgs a;
-        a.n = n;
-        a.shift = shift;
-        a.nbits = w;
-        a.nchunks = nchunks;
-        a.keys_in = kin;
-        a.vals_in = vin;
-        a.keys_out = last ? nullptr : ((p & 1) ? k1 : k0);
-        a.vals_out = last ? nullptr : ((p & 1) ? v1 : v0);
-        a.out_x = out_x;
-        a.out_y = out_y;
-        a.sorted_keys = sorted_keys;
-        a.rects = (last && !pair) ? rects : nullptr;
-        a.sorted_rects = sorted_rects;
-        a.sorted_counts = sorted_counts;
-        a.row_prefix = counts;
-        a.totals = totals;
-        const dim3 g((unsigned)nchunks), b(RS_THREADS);
-        if (shrt) {
-            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, true>), g, b, 0, s, a);
-            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS_SHORT, false>), g, b, 0, s, a);
-        } else {
-            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, a);
-            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false>), g, b, 0, s, a);
+    const SortJob j = {n, keys_in, pairs, k0, v0, k1, v1, out_x, out_y, sorted_keys, scratch, rects, sorted_rects,
+                       sorted_counts};
+    return radix_sort_batch(&j, 1, nbits, s);
+}
+
+hipError_t launch_emit_batch(const EmitJob* jobs, int V, uint32_t gx, int T, hipStream_t s)
+{
+    return for_groups(V, [&](int v0, int nv) -> hipError_t {
+        ViewBatch<EmitJob> B;
+        B.n = nv;
+        int maxp = 0;
+        for (int v = 0; v < nv; v++) {
+            B.v[v] = jobs[v0 + v];
+            maxp = max(maxp, B.v[v].P);
         }
-        kin = a.keys_out;
-        vin = a.vals_out;
-        shift += w;
-    }
-    return hipGetLastError();
+        if (maxp <= 0) return hipSuccess;
+        hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)((maxp + 255) / 256), (unsigned)nv), dim3(256), 0, s,
+                           B, gx, T);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
@@ -502,9 +584,8 @@ hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32
                                  uint32_t* valid, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0) return hipSuccess;
-    hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       sorted_rects, gx, tile_keys, pairs, rec_start, valid, ranges, T, nullptr, (size_t)0);
-    return hipGetLastError();
+    const EmitJob j = {P, sorted_ids, offsets_d, sorted_rects, rec_start, tile_keys, pairs, valid, ranges, nullptr, 0};
+    return launch_emit_batch(&j, 1, gx, T, s);
 }
 
 hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
@@ -512,18 +593,40 @@ hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const 
                                        size_t capacity, uint2* ranges, int T, hipStream_t s)
 {
     if (P <= 0 || !bb) return hipSuccess;
-    hipLaunchKernelGGL(emit_instances_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, sorted_ids, offsets_d,
-                       sorted_rects, gx, nullptr, nullptr, rec_start, nullptr, ranges, T, bb, capacity);
-    return hipGetLastError();
+    const EmitJob j = {P, sorted_ids, offsets_d, sorted_rects, rec_start, nullptr, nullptr, nullptr, ranges, bb,
+                       capacity};
+    return launch_emit_batch(&j, 1, gx, T, s);
+}
+
+hipError_t launch_tile_ranges_batch(const RangesJob* jobs, int V, int T, hipStream_t s)
+{
+    for (int v = 0; v < V; v++) {
+        if (jobs[v].L <= 0) {  // no emission ran to clear them
+            const hipError_t e = hipMemsetAsync(jobs[v].ranges, 0, sizeof(uint2) * (size_t)T, s);
+            if (e != hipSuccess) return e;
+        } else if ((uintptr_t)jobs[v].sorted_tiles & 15) {
+            return hipErrorInvalidValue;  // binning arrays are 256-B aligned
+        }
+    }
+    return for_groups(V, [&](int v0, int nv) -> hipError_t {
+        ViewBatch<RangesJob> B;
+        B.n = nv;
+        int maxl = 0;
+        for (int v = 0; v < nv; v++) {
+            B.v[v] = jobs[v0 + v];
+            maxl = max(maxl, B.v[v].L);
+        }
+        if (maxl <= 0) return hipSuccess;
+        const int quads = (maxl + 3) / 4;
+        hipLaunchKernelGGL(tile_ranges_kernel, dim3((unsigned)((quads + 255) / 256), (unsigned)nv), dim3(256), 0, s, B);
+        return hipGetLastError();
+    });
 }
 
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s)
 {
-    if (L <= 0) return hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);  // no emit ran to clear them
-    if ((uintptr_t)sorted_tiles & 15) return hipErrorInvalidValue;  // binning arrays are 256-B aligned
-    const int quads = (L + 3) / 4;
-    hipLaunchKernelGGL(tile_ranges_kernel, dim3((quads + 255) / 256), dim3(256), 0, s, L, sorted_tiles, ranges);
-    return hipGetLastError();
+    const RangesJob j = {L, sorted_tiles, ranges};
+    return launch_tile_ranges_batch(&j, 1, T, s);
 }
 
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,

@@ -136,9 +136,11 @@ constexpr int ORDER_BITS = 6;         // 64 work classes; tiles without work joi
 constexpr int ORDER_PER_THREAD = 8;   // tiles per thread and pass: 8,192 per pass (one pass at 1080p)
 
 template <bool FROM_RANGES>
-__global__ void __launch_bounds__(1024) tile_order_kernel(const uint2* ranges, const uint32_t* work, int T,
-                                                          uint32_t* order)
+__global__ void __launch_bounds__(1024) tile_order_kernel(const ViewBatch<OrderJob> B, int T)
 {
+    const uint2* ranges = B.v[blockIdx.x].ranges;  // one workgroup per view
+    const uint32_t* work = B.v[blockIdx.x].work;
+    uint32_t* order = B.v[blockIdx.x].order;
     __shared__ uint32_t s_cnt[16][1 << ORDER_BITS];  // per-wave class counts, then per-wave starts
     __shared__ uint32_t s_order[1024 * ORDER_PER_THREAD];  // the pass's order, stored out coalesced
     __shared__ uint32_t s_max;
@@ -676,12 +678,28 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(RenderBwdArgs 
     }
 }
 
-hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s)
+hipError_t launch_tile_order_batch(const OrderJob* jobs, int V, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    if (ranges) hipLaunchKernelGGL(tile_order_kernel<true>, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
-    else hipLaunchKernelGGL(tile_order_kernel<false>, dim3(1), dim3(1024), 0, s, ranges, work, T, order);
-    return hipGetLastError();
+    for (int v0 = 0; v0 < V; v0 += VIEW_BATCH) {
+        const int nv = min(VIEW_BATCH, V - v0);
+        ViewBatch<OrderJob> B;
+        B.n = nv;
+        for (int v = 0; v < nv; v++) B.v[v] = jobs[v0 + v];
+        if (B.v[0].ranges)
+            hipLaunchKernelGGL(tile_order_kernel<true>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        else
+            hipLaunchKernelGGL(tile_order_kernel<false>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s)
+{
+    const OrderJob j = {ranges, work, order};
+    return launch_tile_order_batch(&j, 1, T, s);
 }
 
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
