@@ -784,8 +784,6 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     DEBUG_SYNC(ps);
     ScanJob rec[MAX_VIEWS], off[MAX_VIEWS];
     SortJob dsort[MAX_VIEWS];
-    EmitJob emit[MAX_VIEWS];
-    int ne = 0;
     for (int v = 0; v < V; v++) {
         char* gb = geometry_buffers[v];
         const PreprocessArgs& a = pa[v];
@@ -800,10 +798,6 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                     at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])};
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
-        if (binning_buffers[v] && binning_capacity[v] > 0)
-            emit[ne++] = {P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), offsets, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
-                          at<uint32_t>(gb, g.off[GEOM_EMIT_START]), nullptr, nullptr, nullptr,
-                          at<uint2>(image_buffers[v], im.off[IMG_RANGES]), binning_buffers[v], binning_capacity[v]};
     }
     HIP_TRY(launch_scan_batch(rec, V, true, ps));
     {
@@ -813,10 +807,6 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     {
         ProfScope ps_(PK_SCAN, ps);
         HIP_TRY(launch_scan_batch(off, V, false, ps));
-    }
-    if (ne) {  // before the read-back: resolves its arrays from the device-side totals
-        ProfScope ps_(PK_EMIT, ps);
-        HIP_TRY(launch_emit_batch(emit, ne, gx, T, ps));
     }
     DEBUG_SYNC(ps);
     // the one host hand-off: every view's num_rendered (rasterizer_impl.cu:283-284)
@@ -829,11 +819,11 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         prefix_end(caller, ps);
         return rc;
     }
-    // views whose binning buffer holds them: tile sort, tile ranges and tile order, batched (the
-    // others are left to the caller: allocate gsr_binning_buffer_size(num_rendered[v]), then
-    // gsr_forward_render)
+    // views whose binning buffer holds them: emission fused into the tile sort, tile ranges and
+    // tile order, batched (the others are left to the caller: allocate
+    // gsr_binning_buffer_size(num_rendered[v]), then gsr_forward_render)
     int fit[MAX_VIEWS], nf = 0;
-    SortJob tsort[MAX_VIEWS];
+    TileSortJob tsort[MAX_VIEWS];
     RangesJob rj[MAX_VIEWS];
     OrderJob oj[MAX_VIEWS];
     int ns = 0;
@@ -842,15 +832,22 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
             continue;
         char* bb = binning_buffers[v];
         char* ib = image_buffers[v];
+        char* gb = geometry_buffers[v];
         const BinLayout b = bin_layout(L[v]);
-        if (L[v] > 0) tsort[ns++] = tile_sort_job(bb, L[v]);
+        if (L[v] > 0) {
+            const SortJob t = tile_sort_job(bb, L[v]);
+            tsort[ns++] = {P, L[v], at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
+                           at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_EMIT_START]),
+                           gb + g.off[GEOM_DSORT_TMP], t.k0, t.v0, t.k1, t.v1, t.scratch, t.out_x, t.out_y,
+                           t.sorted_keys, at<uint32_t>(bb, b.off[BIN_VALID]), at<uint2>(ib, im.off[IMG_RANGES])};
+        }
         rj[nf] = {L[v], L[v] > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr, at<uint2>(ib, im.off[IMG_RANGES])};
         oj[nf] = {at<uint2>(ib, im.off[IMG_RANGES]), nullptr, at<uint32_t>(ib, im.off[IMG_TILE_ORDER])};
         fit[nf++] = v;
     }
     if (ns) {
         ProfScope ps_(PK_TILE_SORT, ps);
-        HIP_TRY(radix_sort_batch(tsort, ns, (int)higher_msb((uint32_t)T), ps));
+        HIP_TRY(tile_sort_fused_batch(tsort, ns, gx, T, ps));
     }
     if (nf) {
         {

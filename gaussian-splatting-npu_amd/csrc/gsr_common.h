@@ -5,6 +5,7 @@
 // expression order is kept so that, with -ffp-contract=off (this library's
 // default), preprocess outputs are bit-identical to oracle/gsr_oracle.c.
 #pragma once
+#include <algorithm>
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -173,7 +174,8 @@ enum GeomArray {
                           // of tiles_touched)
     GEOM_RECT,            // u16x4[P] tile rect {x0, y0, x1, y1} (getRect), zero if culled
     GEOM_SORTED_RECT,     // u16x4[P] the rects in depth order (last depth-sort pass)
-    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1
+    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1; then the count matrix of the
+                          // fused emission + first tile-sort pass (gsr_forward_views)
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
     GEOM_SCAN_SCRATCH,    // 2 x u64[scan chunks + 1] look-back status words + chunk ticket of the two
                           // scans (depth order, index order; zeroed by preprocess)
@@ -211,12 +213,15 @@ struct ImageLayout { size_t off[IMG_COUNT + 1]; };
 struct BinLayout { size_t off[BIN_COUNT + 1]; };
 
 size_t radix_status_bytes(int n, int npass);
+size_t fused_pass1_scratch_bytes(int P);  // radix.hip: the fused emission pass's count matrix
 
 inline GeomLayout geom_layout(int P)
 {
     size_t p = (size_t)(P > 0 ? P : 0);
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 48 * p,
-                                4 * p, 4 * p, 4 * p, 8 * p, 8 * p, 16 * p + 1024, radix_status_bytes(P, 4),
+                                4 * p, 4 * p, 4 * p, 8 * p, 8 * p,
+                                // (after the depth sort, the fused tile-sort pass's count matrix)
+                                std::max(16 * p + 1024, fused_pass1_scratch_bytes(P)), radix_status_bytes(P, 4),
                                 16 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
     GeomLayout l;
     size_t o = 0;

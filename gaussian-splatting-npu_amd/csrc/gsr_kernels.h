@@ -221,8 +221,30 @@ struct SortJob {  // radix_sort's arguments for one view
     uint2* sorted_rects;
     uint32_t* sorted_counts;
 };
-// V independent stable sorts over the same bit width, pass by pass in shared launches.
-hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s);
+// V independent stable sorts over the same bit width (key bits [shift0, shift0 + nbits)), pass by
+// pass in shared launches.
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0 = 0);
+
+// Emission fused into the tile sort (gsr_forward_views): the instances are generated from the
+// depth-ordered rects inside the first radix pass's count and scatter kernels instead of being
+// written out by an emission kernel and read back by that pass.
+struct TileSortJob {
+    int P, L;
+    const uint32_t* sorted_ids;
+    const uint32_t* offsets;      // inclusive scan of the tile counts in depth order
+    const uint2* sorted_rects;
+    const uint32_t* rec_start;    // first gradient-record slot per Gaussian
+    char* pass1_scratch;          // fused_pass1_scratch_bytes(P): the first pass's count matrix
+    uint32_t *k0, *v0, *k1, *v1;  // ping-pong (v: u32x2)
+    char* scratch;                // radix_status_bytes(L) for the later passes
+    uint32_t* out_slot;           // BIN_SLOT
+    uint32_t* out_ids;            // BIN_POINT_LIST
+    uint32_t* out_tiles;          // BIN_SORTED_TILES
+    uint32_t* valid;              // BIN_VALID, cleared
+    uint2* ranges;                // IMG_RANGES, cleared
+};
+size_t fused_pass1_scratch_bytes(int P);
+hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s);
 
 struct EmitJob {  // emission of one view (bb != null: the early form, arrays resolved on the device)
     int P;

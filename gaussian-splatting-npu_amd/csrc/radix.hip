@@ -402,6 +402,228 @@ __global__ void __launch_bounds__(256) emit_instances_kernel(const ViewBatch<Emi
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Emission fused into the first tile-sort pass.  Chunk c of a view = the instances of its depth
+// ranks [c * FE_RANKS, (c + 1) * FE_RANKS) in emission order (depth rank, then y-major inside the
+// rect: duplicateWithKeys, rasterizer_impl.cu:98-109).  Both kernels stage the chunk's ranks
+// (instance start, rect, and for the scatter the Gaussian id and record start) in LDS and derive
+// every instance -- owner by binary search over the starts, tile from the owner's rect -- instead of
+// reading emitted (tile, slot, id) arrays: the 12 B per instance that emission wrote and the pass
+// read back (twice: count and scatter) never touch HBM.  The scatter ranks a chunk in rounds of
+// RS_THREADS * ITEMS instances (one round on average: ~6 instances per rank), carrying each digit's
+// running output position from round to round, so a chunk of any size stays stable.
+// ---------------------------------------------------------------------------
+constexpr int FE_RANKS = 256;
+
+struct FusedPassArgs {
+    int P, L, nchunks;
+    const uint32_t* sorted_ids;
+    const uint32_t* offsets;
+    const uint2* sorted_rects;
+    const uint32_t* rec_start;
+    uint32_t* counts;  // (bins, nchunks)
+    uint32_t* totals;  // (bins)
+    // outputs: keys_out / vals_out (u32x2) -- or, if this is the only pass, the final arrays
+    uint32_t* keys_out;
+    uint2* vals_out;
+    uint32_t* out_slot;
+    uint32_t* out_ids;
+    uint32_t* out_tiles;
+    uint32_t* valid;
+    uint2* ranges;
+};
+
+struct FeRanks {
+    uint32_t start[FE_RANKS], x0[FE_RANKS], y0[FE_RANKS], w[FE_RANKS], g[FE_RANKS], rec[FE_RANKS];
+    float rw[FE_RANKS];  // 1 / w
+};
+
+// Stages chunk c's ranks; [wbeg, wend) is its instance range.  Ends with a barrier.
+template <bool IDS>
+__device__ __forceinline__ void fe_stage(const FusedPassArgs& J, int c, FeRanks& s, uint32_t& wbeg, uint32_t& wend)
+{
+    const int tid = threadIdx.x;
+    const int k0 = c * FE_RANKS, k = k0 + tid;
+    uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1, g = 0, rec = 0;
+    if (k < J.P) {
+        start = k == 0 ? 0u : J.offsets[k - 1];
+        const uint2 rc = J.sorted_rects[k];
+        x0 = rc.x & 0xFFFFu;
+        y0 = rc.x >> 16;
+        wd = max((rc.y & 0xFFFFu) - x0, 1u);
+        if (IDS) {
+            g = J.sorted_ids[k];
+            rec = J.rec_start[g];
+        }
+    }
+    s.start[tid] = start;
+    s.x0[tid] = x0;
+    s.y0[tid] = y0;
+    s.w[tid] = wd;
+    s.rw[tid] = 1.0f / (float)wd;
+    if (IDS) {
+        s.g[tid] = g;
+        s.rec[tid] = rec;
+    }
+    wbeg = k0 == 0 ? 0u : J.offsets[k0 - 1];
+    wend = J.offsets[min(k0 + FE_RANKS, J.P) - 1];
+    __syncthreads();
+}
+
+// The owner of instance sl (the largest staged rank whose start is <= sl: ranks without instances
+// share their successor's start) and its local index inside the owner's rect.
+__device__ __forceinline__ int fe_owner(const FeRanks& s, uint32_t sl)
+{
+    int j = 0;
+#pragma unroll
+    for (int step = FE_RANKS / 2; step >= 1; step >>= 1)
+        if (s.start[j + step] <= sl) j += step;
+    return j;
+}
+
+__device__ __forceinline__ uint32_t fe_tile(const FeRanks& s, int j, uint32_t sl, uint32_t gx, uint32_t& local)
+{
+    local = sl - s.start[j];
+    const uint32_t wj = s.w[j];
+    // local / wj by a reciprocal estimate (off by at most one for local < 2^24) and one correction
+    // each way, instead of the ~40-instruction integer division
+    uint32_t yy = (uint32_t)((float)local * s.rw[j]);
+    yy -= yy * wj > local ? 1u : 0u;
+    yy += (yy + 1u) * wj <= local ? 1u : 0u;
+    const uint32_t xx = local - yy * wj;
+    return (s.y0[j] + yy) * gx + (s.x0[j] + xx);
+}
+
+__global__ void __launch_bounds__(RS_THREADS) fused_pass1_count_kernel(const ViewBatch<FusedPassArgs> B, uint32_t gx,
+                                                                      int T, int nbits)
+{
+    const FusedPassArgs& J = B.v[blockIdx.y];
+    const int c = (int)blockIdx.x;
+    if (c >= J.nchunks) return;  // past this view's chunks (uniform)
+    __shared__ uint32_t h[4][RS_MAXBINS];
+    const int tid = threadIdx.x, w = tid >> 6;
+    // ranges must be zero for tile_ranges (empty tiles keep (0, 0)): cleared here, not by a memset
+    for (int t = c * RS_THREADS + tid; t < T; t += J.nchunks * RS_THREADS) J.ranges[t] = make_uint2(0u, 0u);
+    for (int q = 0; q < 4; q++) h[q][tid] = 0;
+    __syncthreads();
+    // a histogram needs no instance order: each thread walks its own rank's rect (no owner search)
+    const uint32_t nb = 1u << nbits, mask = nb - 1u;
+    const int k = c * FE_RANKS + tid;
+    if (k < J.P) {
+        const uint32_t start = k == 0 ? 0u : J.offsets[k - 1], end = J.offsets[k];
+        if (end > start) {
+            const uint2 rc = J.sorted_rects[k];
+            const uint32_t x0 = rc.x & 0xFFFFu, y0 = rc.x >> 16, x1 = rc.y & 0xFFFFu, y1 = rc.y >> 16;
+            for (uint32_t y = y0; y < y1; y++)
+                for (uint32_t x = x0; x < x1; x++) atomicAdd(&h[w][(y * gx + x) & mask], 1u);
+            // the backward flags the records it writes: clear the bit words starting in [start, end)
+            for (uint32_t sl = (start + 31u) & ~31u; sl < end; sl += 32u) J.valid[sl >> 5] = 0u;
+        }
+    }
+    __syncthreads();
+    if ((uint32_t)tid < nb) J.counts[(size_t)tid * J.nchunks + c] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+}
+
+template <int ITEMS>
+__global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const ViewBatch<FusedPassArgs> B, uint32_t gx,
+                                                                        int nbits)
+{
+    constexpr int TILE = RS_THREADS * ITEMS;
+    const FusedPassArgs& J = B.v[blockIdx.y];
+    const int c = (int)blockIdx.x;
+    if (c >= J.nchunks) return;  // past this view's chunks (uniform)
+    __shared__ FeRanks s;
+    __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
+    __shared__ uint32_t s_blk[RS_MAXBINS];     // round-local start of each digit
+    __shared__ uint32_t s_base[RS_MAXBINS];    // global position of each digit's next element
+    __shared__ uint32_t s_keys[TILE];
+    __shared__ uint2 s_vals[TILE];
+    __shared__ uint32_t s_w0[4], s_w1[4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t nb = 1u << nbits, mask = nb - 1u;
+    for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
+    const uint32_t tot = (uint32_t)tid < nb ? J.totals[tid] : 0u;
+    const uint32_t rowp = (uint32_t)tid < nb ? J.counts[(size_t)tid * J.nchunks + c] : 0u;
+    const uint32_t gbase = block_excl_scan256(tot, s_w0) + rowp;
+    s_base[tid] = gbase;
+    uint32_t wbeg, wend;
+    fe_stage<true>(J, c, s, wbeg, wend);  // its barrier also publishes s_cnt = 0 and s_base
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const bool last = J.keys_out == nullptr;
+    for (uint32_t r0 = wbeg; r0 < wend; r0 += TILE) {
+        const int nvalid = (int)min((uint32_t)TILE, wend - r0);
+        uint32_t key[ITEMS], rank[ITEMS];
+        uint2 val[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const int li = w * (ITEMS * 64) + i * 64 + lane;
+            const uint32_t sl = r0 + (uint32_t)min(li, nvalid - 1);
+            const int j = fe_owner(s, sl);
+            uint32_t local;
+            key[i] = fe_tile(s, j, sl, gx, local);
+            val[i] = make_uint2(s.rec[j] + local, s.g[j]);
+        }
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const int li = w * (ITEMS * 64) + i * 64 + lane;
+            const bool valid = li < nvalid;
+            const uint32_t d = key[i] & mask;
+            uint64_t peers = __ballot(valid);
+            for (int b = 0; b < nbits; b++) {
+                const uint64_t bal = __ballot((d >> b) & 1u);
+                peers &= ((d >> b) & 1u) ? bal : ~bal;
+            }
+            const uint32_t before = s_cnt[w][d];
+            rank[i] = before + (uint32_t)__popcll(peers & lt);
+            const bool leader = valid && (peers & lt) == 0ull;
+            if (leader) s_cnt[w][d] = before + (uint32_t)__popcll(peers);
+            if (!valid) rank[i] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        const uint32_t c0 = s_cnt[0][tid], c1 = s_cnt[1][tid], c2 = s_cnt[2][tid], c3 = s_cnt[3][tid];
+        const uint32_t total = c0 + c1 + c2 + c3;
+        s_cnt[0][tid] = 0;
+        s_cnt[1][tid] = c0;
+        s_cnt[2][tid] = c0 + c1;
+        s_cnt[3][tid] = c0 + c1 + c2;
+        s_blk[tid] = block_excl_scan256(total, s_w1);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            if (rank[i] != 0xFFFFFFFFu) {
+                const uint32_t d = key[i] & mask;
+                const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
+                s_keys[lpos] = key[i];
+                s_vals[lpos] = val[i];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {  // contiguous write-out: runs of one digit
+            const int lpos = i * RS_THREADS + tid;
+            if (lpos < nvalid) {
+                const uint32_t k = s_keys[lpos];
+                const uint32_t d = k & mask;
+                const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
+                const uint2 v = s_vals[lpos];
+                if (!last) {
+                    J.keys_out[dst] = k;
+                    J.vals_out[dst] = v;
+                } else {
+                    J.out_slot[dst] = v.x;
+                    J.out_ids[dst] = v.y;
+                    J.out_tiles[dst] = k;
+                }
+            }
+        }
+        __syncthreads();
+        s_base[tid] += total;  // the next round's elements follow this round's in every digit
+        s_cnt[0][tid] = s_cnt[1][tid] = s_cnt[2][tid] = s_cnt[3][tid] = 0;
+        __syncthreads();
+    }
+}
+
 // identifyTileRanges (rasterizer_impl.cu:116-138): four consecutive instances per thread (one
 // 16-byte load); each element's predecessor comes from the same load or, for the first, from the
 // neighbouring lane (the wave's first lane loads it).
@@ -487,7 +709,7 @@ static inline uint32_t* sort_totals(const SortJob& j)
     return reinterpret_cast<uint32_t*>(j.scratch + align_up(rs_chunks(j.n) * RS_MAXBINS * 4 + 256, 256));
 }
 
-hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s)
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
 {
     if (nbits < 1) nbits = 1;
     const int npass = (nbits + 7) / 8;
@@ -505,7 +727,7 @@ hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s
             kin[v] = jobs[v0 + v].keys_in;
             vin[v] = reinterpret_cast<const uint32_t*>(jobs[v0 + v].pairs);
         }
-        int shift = 0;
+        int shift = shift0;
         for (int p = 0; p < npass; p++) {
             const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
             const bool last = p == npass - 1;
@@ -549,6 +771,64 @@ hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s
             shift += w;
         }
         return hipGetLastError();
+    });
+}
+
+size_t fused_pass1_scratch_bytes(int P)
+{
+    const size_t chunks = ((size_t)(P > 0 ? P : 0) + FE_RANKS - 1) / FE_RANKS;
+    return align_up(chunks * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
+}
+
+hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s)
+{
+    const int nbits = max((int)higher_msb((uint32_t)T), 1);
+    const int npass = (nbits + 7) / 8;
+    const int w1 = nbits / npass + (nbits % npass ? 1 : 0);  // radix_sort_batch's balanced first width
+    return for_groups(V, [&](int v0, int nv) -> hipError_t {
+        ViewBatch<FusedPassArgs> fb;
+        ViewBatch<RowJob> rb;
+        SortJob rest[VIEW_BATCH];
+        fb.n = rb.n = nv;
+        int maxc = 0;
+        for (int v = 0; v < nv; v++) {
+            const TileSortJob& j = jobs[v0 + v];
+            FusedPassArgs& a = fb.v[v];
+            a.P = j.P;
+            a.L = j.L;
+            a.nchunks = (j.P + FE_RANKS - 1) / FE_RANKS;
+            a.sorted_ids = j.sorted_ids;
+            a.offsets = j.offsets;
+            a.sorted_rects = j.sorted_rects;
+            a.rec_start = j.rec_start;
+            a.counts = reinterpret_cast<uint32_t*>(j.pass1_scratch);
+            a.totals = reinterpret_cast<uint32_t*>(j.pass1_scratch +
+                                                   align_up((size_t)a.nchunks * RS_MAXBINS * 4 + 256, 256));
+            // the fused pass writes (k1, v1), so that the later passes ping-pong k0 <- k1 <- k0 ...
+            a.keys_out = npass > 1 ? j.k1 : nullptr;
+            a.vals_out = npass > 1 ? reinterpret_cast<uint2*>(j.v1) : nullptr;
+            a.out_slot = j.out_slot;
+            a.out_ids = j.out_ids;
+            a.out_tiles = j.out_tiles;
+            a.valid = j.valid;
+            a.ranges = j.ranges;
+            rb.v[v] = {a.counts, a.nchunks, a.totals};
+            maxc = max(maxc, a.nchunks);
+            rest[v] = {j.L, j.k1, reinterpret_cast<const uint2*>(j.v1), j.k0, j.v0, j.k1, j.v1, j.out_slot, j.out_ids,
+                       j.out_tiles, j.scratch, nullptr, nullptr, nullptr};
+        }
+        if (maxc == 0) return hipSuccess;
+        const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
+        hipLaunchKernelGGL(fused_pass1_count_kernel, g, b, 0, s, fb, gx, T, w1);
+        if (maxc <= RS_ROW_LDS)
+            hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+        else
+            hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+        hipLaunchKernelGGL(fused_pass1_scatter_kernel<RS_ITEMS>, g, b, 0, s, fb, gx, w1);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess || npass == 1) return e;
+        // the later passes: key bits [w1, nbits), ping-pong k1/v1 -> k0/v0 -> ...
+        return radix_sort_batch(rest, nv, nbits - w1, s, w1);
     });
 }
 
