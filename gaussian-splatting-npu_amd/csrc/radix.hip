@@ -64,8 +64,19 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch
             const uint4 q = k4[j * RS_THREADS + tid];
             k[4 * j] = q.x; k[4 * j + 1] = q.y; k[4 * j + 2] = q.z; k[4 * j + 3] = q.w;
         }
+        // a wave whose 64 keys share one digit (the depth keys' top byte, mostly) adds once: 64
+        // same-address LDS atomics would serialise
+        const int lane = tid & 63;
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+        for (int i = 0; i < ITEMS; i++) {
+            const uint32_t d = digit_of(k[i], shift, mask);
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            if (__all(d == d0)) {
+                if (lane == 0) atomicAdd(&h[w][d0], 64u);
+            } else {
+                atomicAdd(&h[w][d], 1u);
+            }
+        }
     } else {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
@@ -539,7 +550,9 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     __shared__ uint32_t s_base[RS_MAXBINS];    // global position of each digit's next element
     __shared__ uint32_t s_keys[TILE];
     __shared__ uint2 s_vals[TILE];
-    __shared__ uint32_t s_w0[4], s_w1[4];
+    __shared__ __attribute__((aligned(8))) uint8_t s_own[TILE];  // owner (staged rank) of each round position
+    __shared__ uint32_t s_w0[4], s_w1[4], s_w2[4];
+    static_assert(TILE == 8 * RS_THREADS && FE_RANKS <= 256, "owner scan: 8 positions per thread, u8 ranks");
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nb = 1u << nbits, mask = nb - 1u;
     for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
@@ -551,15 +564,56 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     fe_stage<true>(J, c, s, wbeg, wend);  // its barrier also publishes s_cnt = 0 and s_base
     const uint64_t lt = (1ull << lane) - 1ull;
     const bool last = J.keys_out == nullptr;
+    // this thread's staged rank: start and end of its instances
+    const uint32_t my_start = s.start[tid];
+    const uint32_t my_end = min(tid + 1 < FE_RANKS ? s.start[tid + 1] : wend, wend);
     for (uint32_t r0 = wbeg; r0 < wend; r0 += TILE) {
         const int nvalid = (int)min((uint32_t)TILE, wend - r0);
+        // owners of the round's positions without a search per instance: every rank starting inside
+        // the round marks its first position, and an inclusive max-scan (ranks increase with the
+        // position) seeded with the owner of r0 fills the rest
+        reinterpret_cast<uint64_t*>(s_own)[tid] = 0ull;
+        __syncthreads();
+        if (my_end > my_start && my_start >= r0 && my_start < r0 + (uint32_t)nvalid)
+            s_own[my_start - r0] = (uint8_t)tid;
+        __syncthreads();
+        {
+            const uint32_t j0 = (uint32_t)fe_owner(s, r0);
+            const uint64_t q = reinterpret_cast<const uint64_t*>(s_own)[tid];
+            uint32_t b[8], mt = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                b[e] = (uint32_t)(q >> (8 * e)) & 0xFFu;
+                mt = max(mt, b[e]);
+            }
+            uint32_t inc = mt;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc = max(inc, y);
+            }
+            if (lane == 63) s_w2[w] = inc;
+            __syncthreads();
+            uint32_t run = j0;
+            for (int qq = 0; qq < w; qq++) run = max(run, s_w2[qq]);
+            const uint32_t ex = (uint32_t)__shfl_up((int)inc, 1, 64);
+            if (lane > 0) run = max(run, ex);
+            uint64_t o = 0;
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                run = max(run, b[e]);
+                o |= (uint64_t)run << (8 * e);
+            }
+            reinterpret_cast<uint64_t*>(s_own)[tid] = o;
+        }
+        __syncthreads();
         uint32_t key[ITEMS], rank[ITEMS];
         uint2 val[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const int li = w * (ITEMS * 64) + i * 64 + lane;
             const uint32_t sl = r0 + (uint32_t)min(li, nvalid - 1);
-            const int j = fe_owner(s, sl);
+            const int j = s_own[min(li, nvalid - 1)];
             uint32_t local;
             key[i] = fe_tile(s, j, sl, gx, local);
             val[i] = make_uint2(s.rec[j] + local, s.g[j]);
