@@ -860,17 +860,18 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     DEBUG_SYNC(ps);
     rc = prefix_end(caller, ps);
     if (rc) return rc;
+    RenderFwdArgs ra[MAX_VIEWS];
     for (int k = 0; k < nf; k++) {
         const int v = fit[k];
-        const RenderFwdArgs r = render_fwd_args(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L[v],
-                                                background, width, height, out_colors[v], out_invdepths[v]);
-        {
-            ProfScope ps_(PK_RENDER_FWD, caller);
-            HIP_TRY(launch_render_fwd(r, T, caller));
-        }
-        DEBUG_SYNC(caller);
+        ra[k] = render_fwd_args(geometry_buffers[v], binning_buffers[v], image_buffers[v], P, L[v], background, width,
+                                height, out_colors[v], out_invdepths[v]);
         rendered[v] = 1;
     }
+    if (nf) {  // every view's render in one launch (one launch tail per batch)
+        ProfScope ps_(PK_RENDER_FWD, caller);
+        HIP_TRY(launch_render_fwd_batch(ra, nf, T, caller));
+    }
+    DEBUG_SYNC(caller);
     return GSR_OK;
 }
 
@@ -988,31 +989,21 @@ int gsr_backward_dc(int P, int D, int M, int R, const float* background, int wid
                                dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug, 0u, stream);
 }
 
-int gsr_backward_render(int P, int R, const float* background, int width, int height, char* geom_buffer,
-                        char* binning_buffer, char* image_buffer, const float* dL_dpix, const float* dL_invdepths,
-                        bool debug, gsr_stream_t stream)
+// render_bwd's arguments for one view (P, R > 0)
+static RenderBwdArgs render_bwd_args(int P, int R, const float* background, int width, int height, char* gb,
+                                     char* bb, char* ib, const float* dL_dpix, const float* dL_invdepths)
 {
-    hipStream_t s = (hipStream_t)stream;
-    if (P < 0 || R < 0) return fail(GSR_ERR_INVALID, "P and R must be >= 0");
-    if (P == 0 || R == 0) return GSR_OK;
-    if (!geom_buffer || !image_buffer || !binning_buffer) return fail(GSR_ERR_ALLOC, "null state buffer");
-    if (!dL_dpix) return fail(GSR_ERR_INVALID, "null dL_dpix");
     const GeomLayout g = geom_layout(P);
     const ImageLayout im = image_layout(width, height);
     const BinLayout b = bin_layout(R);
-    char* gb = geom_buffer;
-    char* ib = image_buffer;
-    char* bb = binning_buffer;
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
-    const int T = (int)(gx * gy);
-    // BACKWARD::render (rasterizer_impl.cu:399-418): per-(tile, Gaussian) gradient records
     RenderBwdArgs r;
     r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
     r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
     r.W = width; r.H = height; r.grid_x = gx;
-    r.T = T;
+    r.T = (int)(gx * gy);
     r.bg = background;
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
@@ -1024,14 +1015,29 @@ int gsr_backward_render(int P, int R, const float* background, int width, int he
     r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
     r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
     r.hit = at<uint8_t>(bb, b.off[BIN_HIT]);
+    return r;
+}
+
+int gsr_backward_render(int P, int R, const float* background, int width, int height, char* geom_buffer,
+                        char* binning_buffer, char* image_buffer, const float* dL_dpix, const float* dL_invdepths,
+                        bool debug, gsr_stream_t stream)
+{
+    hipStream_t s = (hipStream_t)stream;
+    if (P < 0 || R < 0) return fail(GSR_ERR_INVALID, "P and R must be >= 0");
+    if (P == 0 || R == 0) return GSR_OK;
+    if (!geom_buffer || !image_buffer || !binning_buffer) return fail(GSR_ERR_ALLOC, "null state buffer");
+    if (!dL_dpix) return fail(GSR_ERR_INVALID, "null dL_dpix");
+    const ImageLayout im = image_layout(width, height);
+    const RenderBwdArgs r = render_bwd_args(P, R, background, width, height, geom_buffer, binning_buffer, image_buffer,
+                                            dL_dpix, dL_invdepths);
     {
         ProfScope ps_(PK_TILE_ORDER, s);
-        HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(ib, im.off[IMG_TILE_WORK]), T,
-                                  at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
+        HIP_TRY(launch_tile_order(nullptr, at<uint32_t>(image_buffer, im.off[IMG_TILE_WORK]), r.T,
+                                  at<uint32_t>(image_buffer, im.off[IMG_TILE_ORDER]), s));
     }
     {
-        ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emit_instances
-        HIP_TRY(launch_render_bwd(r, T, s));
+        ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emission
+        HIP_TRY(launch_render_bwd(r, r.T, s));
     }
     DEBUG_SYNC(s);
     return GSR_OK;
@@ -1134,13 +1140,37 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
         return fail(GSR_ERR_INVALID, "null per-view array");
     const bool has_inv = dL_invdepths != nullptr;
     if (P <= 0) return GSR_OK;
-    for (int v = 0; v < V; v++) {  // BACKWARD::render of every view: its per-(tile, Gaussian) records
-        if (!dL_dpix[v] || (has_inv && !dL_invdepths[v])) return fail(GSR_ERR_INVALID, "null per-view gradient");
-        const int rc = gsr_backward_render(P, R[v], background, width, height, geom_buffers[v], binning_buffers[v],
-                                           image_buffers[v], dL_dpix[v], has_inv ? dL_invdepths[v] : nullptr, debug,
-                                           stream);
-        if (rc) return rc;
+    // every view's backward tile order (longest n_contrib first) in one launch
+    OrderJob oj[MAX_VIEWS];
+    int no = 0;
+    const ImageLayout im = image_layout(width, height);
+    const int T = (int)(((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X) * ((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y));
+    for (int v = 0; v < V; v++) {
+        if (!image_buffers[v]) return fail(GSR_ERR_ALLOC, "null state buffer");
+        if (R[v] > 0)
+            oj[no++] = {nullptr, at<uint32_t>(image_buffers[v], im.off[IMG_TILE_WORK]),
+                        at<uint32_t>(image_buffers[v], im.off[IMG_TILE_ORDER])};
     }
+    if (no) {
+        ProfScope ps_(PK_TILE_ORDER, (hipStream_t)stream);
+        HIP_TRY(launch_tile_order_batch(oj, no, T, (hipStream_t)stream));
+    }
+    // BACKWARD::render of every view (its per-(tile, Gaussian) records), one launch per batch
+    RenderBwdArgs ra[MAX_VIEWS];
+    int nr = 0;
+    for (int v = 0; v < V; v++) {
+        if (!dL_dpix[v] || (has_inv && !dL_invdepths[v])) return fail(GSR_ERR_INVALID, "null per-view gradient");
+        if (R[v] < 0) return fail(GSR_ERR_INVALID, "R must be >= 0");
+        if (R[v] == 0) continue;
+        if (!geom_buffers[v] || !binning_buffers[v]) return fail(GSR_ERR_ALLOC, "null state buffer");
+        ra[nr++] = render_bwd_args(P, R[v], background, width, height, geom_buffers[v], binning_buffers[v],
+                                   image_buffers[v], dL_dpix[v], has_inv ? dL_invdepths[v] : nullptr);
+    }
+    if (nr) {
+        ProfScope ps_(PK_RENDER_BWD, (hipStream_t)stream);  // valid[] was cleared by the forward
+        HIP_TRY(launch_render_bwd_batch(ra, nr, T, (hipStream_t)stream));
+    }
+    DEBUG_SYNC((hipStream_t)stream);
     return gsr_backward_preprocess_views(V, P, D, M, R, width, height, means3D, dc, shs, colors_precomp, opacities,
                                          scales, scale_modifier, rotations, cov3D_precomp, viewmatrices,
                                          projmatrices, campos, tan_fovx, tan_fovy, radii, geom_buffers,

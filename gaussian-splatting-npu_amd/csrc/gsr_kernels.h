@@ -300,6 +300,10 @@ hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t
 hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, uint32_t* order, hipStream_t s);
 hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s);
 hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
+// V views of one image size in one launch per VIEW_BATCH views (grid.y = view); render_bwd: every
+// view with dL_invdepths, or none
+hipError_t launch_render_fwd_batch(const RenderFwdArgs* a, int V, int T, hipStream_t s);
+hipError_t launch_render_bwd_batch(const RenderBwdArgs* a, int V, int T, hipStream_t s);
 hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, hipStream_t s);
 

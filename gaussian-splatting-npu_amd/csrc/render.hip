@@ -238,9 +238,14 @@ __device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64
     return h;
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) render_fwd_kernel(RenderFwdArgs a)
+// One launch renders a batch of views (grid.y = view): the views' tiles are dispatched one view
+// after the other, so a view's long tiles start while the previous view's short tail still runs --
+// one launch tail per batch instead of one per view.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
 {
 #pragma clang fp contract(fast)
+    const RenderFwdArgs& a = B.v[blockIdx.y];
     const uint32_t tile = a.tile_order[blockIdx.x];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int tid = threadIdx.x;
@@ -507,9 +512,10 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 constexpr int BWD_TPW = 4;
 
 template <bool HAS_INV>
-__global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(RenderBwdArgs a)
+__global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
 {
 #pragma clang fp contract(fast)
+    const RenderBwdArgs& a = B.v[blockIdx.y];  // a batch of views: one launch tail per batch
     constexpr int G = 3;  // Gaussians per transposed reduction (3 x 10 gradient terms <= 32 values)
     const int wv = BWD_TPW == 1 ? 0 : (int)(threadIdx.x >> 6);
     const int ti = (int)blockIdx.x * BWD_TPW + wv;
@@ -702,23 +708,45 @@ hipError_t launch_tile_order(const uint2* ranges, const uint32_t* work, int T, u
     return launch_tile_order_batch(&j, 1, T, s);
 }
 
-hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s)
+hipError_t launch_render_fwd_batch(const RenderFwdArgs* a, int V, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(T), dim3(256), 0, s, a);
-    return hipGetLastError();
+    for (int v0 = 0; v0 < V; v0 += VIEW_BATCH) {
+        ViewBatch<RenderFwdArgs> B;
+        B.n = min(VIEW_BATCH, V - v0);
+        for (int v = 0; v < B.n; v++) B.v[v] = a[v0 + v];
+        hipLaunchKernelGGL(render_fwd_kernel, dim3((unsigned)T, (unsigned)B.n), dim3(256), 0, s, B);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
-hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s)
+hipError_t launch_render_fwd(const RenderFwdArgs& a, int T, hipStream_t s) { return launch_render_fwd_batch(&a, 1, T, s); }
+
+hipError_t launch_render_bwd_batch(const RenderBwdArgs* a, int V, int T, hipStream_t s)
 {
     if (T <= 0) return hipSuccess;
-    if (a.T != T) return hipErrorInvalidValue;
-    const dim3 grid((unsigned)((T + BWD_TPW - 1) / BWD_TPW)), block(64 * BWD_TPW);
-    if (a.dL_invdepths)
-        hipLaunchKernelGGL(render_bwd_kernel<true>, grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL(render_bwd_kernel<false>, grid, block, 0, s, a);
-    return hipGetLastError();
+    for (int v0 = 0; v0 < V; v0 += VIEW_BATCH) {
+        ViewBatch<RenderBwdArgs> B;
+        B.n = min(VIEW_BATCH, V - v0);
+        bool inv = false;
+        for (int v = 0; v < B.n; v++) {
+            B.v[v] = a[v0 + v];
+            if (B.v[v].T != T) return hipErrorInvalidValue;
+            inv = inv || B.v[v].dL_invdepths != nullptr;
+        }
+        for (int v = 0; v < B.n; v++)  // one kernel variant per launch: all views with or without invdepth
+            if ((B.v[v].dL_invdepths != nullptr) != inv) return hipErrorInvalidValue;
+        const dim3 grid((unsigned)((T + BWD_TPW - 1) / BWD_TPW), (unsigned)B.n), block(64 * BWD_TPW);
+        if (inv) hipLaunchKernelGGL(render_bwd_kernel<true>, grid, block, 0, s, B);
+        else hipLaunchKernelGGL(render_bwd_kernel<false>, grid, block, 0, s, B);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
+
+hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s) { return launch_render_bwd_batch(&a, 1, T, s); }
 
 }  // namespace gsr
