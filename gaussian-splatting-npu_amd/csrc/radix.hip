@@ -548,8 +548,7 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
     __shared__ uint32_t s_blk[RS_MAXBINS];     // round-local start of each digit
     __shared__ uint32_t s_base[RS_MAXBINS];    // global position of each digit's next element
-    __shared__ uint32_t s_keys[TILE];
-    __shared__ uint2 s_vals[TILE];
+    __shared__ uint16_t s_idx[TILE];  // round position of the element at each sorted slot
     __shared__ __attribute__((aligned(8))) uint8_t s_own[TILE];  // owner (staged rank) of each round position
     __shared__ uint32_t s_w0[4], s_w1[4], s_w2[4];
     static_assert(TILE == 8 * RS_THREADS && FE_RANKS <= 256, "owner scan: 8 positions per thread, u8 ranks");
@@ -607,22 +606,23 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
             reinterpret_cast<uint64_t*>(s_own)[tid] = o;
         }
         __syncthreads();
+        // only the digit is kept per element (the sorted slots stage round positions, and the
+        // write-out derives tile, slot and id again): 2 B of LDS per element instead of 12, and
+        // no payload registers
         uint32_t key[ITEMS], rank[ITEMS];
-        uint2 val[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const int li = w * (ITEMS * 64) + i * 64 + lane;
             const uint32_t sl = r0 + (uint32_t)min(li, nvalid - 1);
             const int j = s_own[min(li, nvalid - 1)];
             uint32_t local;
-            key[i] = fe_tile(s, j, sl, gx, local);
-            val[i] = make_uint2(s.rec[j] + local, s.g[j]);
+            key[i] = fe_tile(s, j, sl, gx, local) & mask;
         }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const int li = w * (ITEMS * 64) + i * 64 + lane;
             const bool valid = li < nvalid;
-            const uint32_t d = key[i] & mask;
+            const uint32_t d = key[i];
             uint64_t peers = __ballot(valid);
             for (int b = 0; b < nbits; b++) {
                 const uint64_t bal = __ballot((d >> b) & 1u);
@@ -646,10 +646,9 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             if (rank[i] != 0xFFFFFFFFu) {
-                const uint32_t d = key[i] & mask;
+                const uint32_t d = key[i];
                 const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
-                s_keys[lpos] = key[i];
-                s_vals[lpos] = val[i];
+                s_idx[lpos] = (uint16_t)(w * (ITEMS * 64) + i * 64 + lane);
             }
         }
         __syncthreads();
@@ -657,10 +656,13 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
         for (int i = 0; i < ITEMS; i++) {  // contiguous write-out: runs of one digit
             const int lpos = i * RS_THREADS + tid;
             if (lpos < nvalid) {
-                const uint32_t k = s_keys[lpos];
+                const uint32_t li = s_idx[lpos];
+                const int j = s_own[li];
+                uint32_t local;
+                const uint32_t k = fe_tile(s, j, r0 + li, gx, local);
                 const uint32_t d = k & mask;
                 const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
-                const uint2 v = s_vals[lpos];
+                const uint2 v = make_uint2(s.rec[j] + local, s.g[j]);
                 if (!last) {
                     J.keys_out[dst] = k;
                     J.vals_out[dst] = v;

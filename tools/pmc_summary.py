@@ -20,6 +20,7 @@ SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_lookback_kernel": "sca
          "radix_count_kernel": "radix_sorts", "radix_rowscan_kernel": "radix_sorts",
          "radix_rowscan_lds_kernel": "radix_sorts",
          "radix_scatter_kernel": "radix_sorts",
+         "fused_pass1_count_kernel": "radix_sorts", "fused_pass1_scatter_kernel": "radix_sorts",
          # SURVEY §8f side paths (bench.py aux leg)
          "knn_": "distCUDA2", "ssim_fwd_kernel": "ssim_fwd", "ssim_bwd_kernel": "ssim_bwd",
          "adam_update_multi_kernel": "sparse_adam"}
