@@ -373,9 +373,13 @@ def main():
         batched_bwd = args.batch_views or args.deferred
         ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if batched_bwd else 1)
         if args.batch_views:  # a batch's views share every launch (grid.y = view, up to 8 views per launch)
-            for k in ("preprocess_fwd", "depth_sort", "scan", "emit_instances", "tile_sort", "tile_ranges",
-                      "tile_order", "render_fwd", "render_bwd"):
-                ab[k] *= min(len(cams), 8)
+            vb = min(len(cams), 8)
+            for k in ("depth_sort", "scan", "emit_instances", "tile_sort", "tile_ranges", "tile_order", "render_fwd",
+                      "render_bwd"):
+                ab[k] *= vb
+            # the batched preprocess reads the parameters once for its views
+            params_b = P * 4 * (11 + 3 * M)
+            ab["preprocess_fwd"] = params_b + vb * (ab["preprocess_fwd"] - params_b)
         # the dominant kernel: the largest share of the step (mean launch time x launches per step)
         dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
