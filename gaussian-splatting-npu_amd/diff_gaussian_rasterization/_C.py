@@ -210,8 +210,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                               cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy, image_height,
                               image_width, sh, degree, campos, prefiltered, antialiasing, debug, dc=None, out=None):
-    """rasterize_gaussians over a batch of V views of the same Gaussians (gsr_forward_views: the
-    views' binning prefixes run side by side on internal streams).  Per-view lists of camera
+    """rasterize_gaussians over a batch of V views of the same Gaussians (gsr_forward_views: every
+    stage of the views' binning prefix and their render as one launch per stage, grid.y = view).  Per-view lists of camera
     arguments; `out` = (colors (V,3,H,W), radii (V,P), invdepths (V,1,H,W)) -- written in full.
     Returns per-view lists (num_rendered, geomBuffer, binningBuffer, imageBuffer); each view's
     results are bit-identical to rasterize_gaussians on that view."""
@@ -263,24 +263,26 @@ def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rota
     stream = _stream(dev)
     nr = (_i * V)()
     rendered = (_i * V)()
-    _check(lib.gsr_forward_views(
-        V, P, int(degree), M, bg_p, W, H, means_p, dc_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p,
-        cov_p, _ptr_array(views), _ptr_array(projs), _ptr_array(cams), (_f * V)(*[float(t) for t in tan_fovx]),
-        (_f * V)(*[float(t) for t in tan_fovy]), bool(prefiltered), bool(antialiasing), _ptr_array(geoms),
-        _ptr_array(imgs), _ptr_array(bins), (_sz * V)(*([cap] * V)), _ptr_array([colors_out[v] for v in range(V)]),
-        _ptr_array([inv_out[v] for v in range(V)]), _ptr_array([radii_out[v] for v in range(V)]), bool(debug),
-        stream, nr, rendered))
+
+    def run(caps):
+        _check(lib.gsr_forward_views(
+            V, P, int(degree), M, bg_p, W, H, means_p, dc_p, sh_p, colors_p, op_p, sc_p, float(scale_modifier), rot_p,
+            cov_p, _ptr_array(views), _ptr_array(projs), _ptr_array(cams), (_f * V)(*[float(t) for t in tan_fovx]),
+            (_f * V)(*[float(t) for t in tan_fovy]), bool(prefiltered), bool(antialiasing), _ptr_array(geoms),
+            _ptr_array(imgs), _ptr_array(bins), (_sz * V)(*caps), _ptr_array([colors_out[v] for v in range(V)]),
+            _ptr_array([inv_out[v] for v in range(V)]), _ptr_array([radii_out[v] for v in range(V)]), bool(debug),
+            stream, nr, rendered))
+
+    run([cap] * V)
     Ls = [int(nr[v]) for v in range(V)]
     _binning_hint[dev] = max(Ls)
-    for v in range(V):
-        need = lib.gsr_binning_buffer_size(Ls[v])
-        if rendered[v]:
-            bins[v] = bins[v][:need]  # a view: the backward re-derives the layout from num_rendered
-        else:  # first call on this device, or the scene grew past the headroom
-            bins[v] = torch.empty((need,), dtype=torch.uint8, device=dev)
-            _check(lib.gsr_forward_render(geoms[v].data_ptr(), bins[v].data_ptr(), imgs[v].data_ptr(), P, Ls[v],
-                                          bg_p, W, H, colors_p, colors_out[v].data_ptr(), inv_out[v].data_ptr(),
-                                          radii_out[v].data_ptr(), bool(debug), stream))
+    if all(rendered[v] for v in range(V)):
+        bins = [bins[v][:lib.gsr_binning_buffer_size(Ls[v])] for v in range(V)]  # views: the backward re-derives
+    else:  # first call on this device, or the scene grew past the headroom: the batch again, exact buffers
+        bins = [torch.empty((lib.gsr_binning_buffer_size(L),), dtype=torch.uint8, device=dev) for L in Ls]
+        run([b.numel() for b in bins])
+        if not all(rendered[v] for v in range(V)) or [int(nr[v]) for v in range(V)] != Ls:
+            raise RuntimeError("diff_gaussian_rasterization (HIP): the repeated batch did not reproduce num_rendered")
     return Ls, geoms, bins, imgs
 
 
