@@ -771,6 +771,11 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                                              tan_fovy[v], prefiltered, antialiasing, radii ? radii[v] : nullptr, v,
                                              &pa[v], &h[v], &hdev[v]);
         if (rc) return rc;
+        // GeometryState's means2D, depths and rgb are read by nothing after the forward: the
+        // batched forward does not write them (24 B per visible Gaussian and view)
+        pa[v].means2D = nullptr;
+        pa[v].depths = nullptr;
+        pa[v].rgb = nullptr;
     }
     // The binning prefix of all V views, batched: every stage is one launch over all views
     // (grid.y = view), on one high-priority prefix stream; the renders follow on the caller's.
@@ -799,11 +804,18 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
     }
-    HIP_TRY(launch_scan_batch(rec, V, true, ps));
+    // the record-slot scans (read only by the fused tile sort) on the auxiliary stream, beside the
+    // depth sorts
+    hipStream_t aux = ps;
+    rc = aux_fork(ps, &aux);
+    if (rc) return rc;
+    HIP_TRY(launch_scan_batch(rec, V, true, aux));
     {
         ProfScope ps_(PK_DEPTH_SORT, ps);
         HIP_TRY(radix_sort_batch(dsort, V, DEPTH_BITS, ps));
     }
+    rc = aux_join(ps, aux);
+    if (rc) return rc;
     {
         ProfScope ps_(PK_SCAN, ps);
         HIP_TRY(launch_scan_batch(off, V, false, ps));

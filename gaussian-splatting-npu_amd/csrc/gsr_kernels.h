@@ -22,7 +22,8 @@ struct PreprocessArgs {
     float tan_fovx, tan_fovy, focal_x, focal_y;
     uint32_t grid_x, grid_y;
     int prefiltered, antialiasing;
-    // outputs
+    // outputs (means2D, depths, rgb: GeometryState fields nothing downstream reads -- kept for the
+    // single-view forward's parity with the reference, null in the batched forward)
     int* radii;
     float* means2D;
     float* depths;

@@ -180,18 +180,20 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     if (!a.colors_precomp) {
         uint8_t cl;
         rgb = computeColorFromSH(p_orig, a.D, sh0, sh, a.campos, cl);
-        a.rgb[3 * (size_t)idx + 0] = rgb.x;
-        a.rgb[3 * (size_t)idx + 1] = rgb.y;
-        a.rgb[3 * (size_t)idx + 2] = rgb.z;
+        if (a.rgb) {
+            a.rgb[3 * (size_t)idx + 0] = rgb.x;
+            a.rgb[3 * (size_t)idx + 1] = rgb.y;
+            a.rgb[3 * (size_t)idx + 2] = rgb.z;
+        }
         a.clamped[idx] = cl;
     } else {
         const float* c = a.colors_precomp + 3 * (size_t)idx;
         rgb = {c[0], c[1], c[2]};
     }
-    a.depths[idx] = p_view.z;
+    if (a.depths) a.depths[idx] = p_view.z;
     a.dkey[idx] = __float_as_uint(p_view.z);  // z > 0.2: float bits are monotone in z
     a.radii[idx] = (int)my_radius;
-    reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
+    if (a.means2D) reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
     const float opacity = opacity_in * h_convolution_scaling;
     reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);

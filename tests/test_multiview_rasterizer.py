@@ -221,3 +221,61 @@ def test_deferred_backward_activations_streams_accumulation():
     for k in a:
         ok, rel = common.allclose_rel(b[k], a[k], rtol=1e-5, atol=1e-9)
         assert ok, f"d{k}: deferred vs per-view rel {rel:.3e}"
+
+
+def _settings_hw(cam, H_, W_, bg, scale_modifier=1.0, empty=False):
+    import diff_gaussian_rasterization as dgr
+    wv = cam.world_view_transform.clone()
+    if empty:  # every Gaussian far behind the camera: L = 0 for this view
+        wv[3, 2] -= 1000.0
+    proj = wv.unsqueeze(0).bmm(cam.projection_matrix.unsqueeze(0)).squeeze(0)
+    return dgr.GaussianRasterizationSettings(H_, W_, cam.tanfovx, cam.tanfovy, bg, scale_modifier, wv.to(DEV),
+                                             proj.to(DEV), 3, wv.inverse()[3, :3].to(DEV), False, False, False)
+
+
+@pytest.mark.parametrize("H_,W_", [(144, 176), (304, 400)])
+def test_multiview_large_batch_big_splats_empty_view(H_, W_):
+    """10 views (two launch groups of the batched kernels), one of them empty (L = 0), splats scaled
+    6x so that a 256-rank chunk of the fused emission + tile-sort pass holds several 2,048-instance
+    rounds; 99 tiles (the fused pass is the only pass) and 475 tiles (two passes).  Images, radii,
+    inverse depths and screen-space gradients bit-identical to single-view GaussianRasterizer calls
+    (unfused emission, per-view launches); parameter gradients equal up to summation order."""
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+    Vb = 10
+    case = common.make_case(P=P, H=H_, W=W_, bg=(0.1, 0.2, 0.3))
+    bg = case["bg"].to(DEV)
+    cams = [synthetic.Camera(W_, H_, view=v, n_views=Vb) for v in range(Vb)]
+    settings = [_settings_hw(c, H_, W_, bg, scale_modifier=6.0, empty=(v == 3)) for v, c in enumerate(cams)]
+    grads = [synthetic.make_grads(H_, W_, seed=60 + v) for v in range(Vb)]
+    gc = torch.stack([g[0] for g in grads]).to(DEV)
+    gi = torch.stack([g[1] for g in grads]).to(DEV)
+
+    single = _leaves(case, "sh_scales")
+    imgs, radii, invs, m2, Ls = [], [], [], [], []
+    for v, s in enumerate(settings):
+        means2D = torch.zeros_like(single["means3D"], requires_grad=True)
+        c, r, i = dgr.GaussianRasterizer(s)(means2D=means2D, **single)
+        Ls.append(_C._binning_hint[DEV])
+        torch.autograd.backward([c, i], [gc[v], gi[v]])
+        imgs.append(c.detach())
+        radii.append(r)
+        invs.append(i.detach())
+        m2.append(means2D.grad)
+    assert Ls[3] == 0 and min(L for v, L in enumerate(Ls) if v != 3) > 0
+    assert max(Ls) > 4 * 2048, f"splats too small for multi-round chunks (L = {max(Ls)})"
+
+    multi = _leaves(case, "sh_scales")
+    means2D = torch.zeros((Vb, P, 3), device=DEV, requires_grad=True)
+    c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **multi)
+    torch.autograd.backward([c, i], [gc, gi])
+    torch.cuda.synchronize()
+    for v in range(Vb):
+        assert torch.equal(c[v].detach(), imgs[v]), f"view {v} image"
+        assert torch.equal(i[v].detach(), invs[v]), f"view {v} invdepth"
+        assert torch.equal(r[v], radii[v]), f"view {v} radii"
+        assert torch.equal(means2D.grad[v], m2[v]), f"view {v} screen-space gradient"
+    for k in single:
+        ok, rel = common.allclose_rel(multi[k].grad.cpu().numpy(), single[k].grad.cpu().numpy(), rtol=1e-5,
+                                      atol=1e-9)
+        assert ok, f"d{k} multi vs sum of single views rel {rel:.3e}"
