@@ -297,12 +297,13 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
 
 /* Forward of a batch of V <= 16 camera views of the same Gaussians (the forward half of
  * gsr_backward_views; each view the result of gsr_forward_prealloc_dc with its own state buffers).
- * One preprocess launch per 8 views reads the Gaussians' parameters once for all of them; then
- * every view's depth sort, scans and emission are enqueued, view v on internal high-priority
- * stream v mod 4, so the short latency-bound launch chains of several views run side by side;
- * then, in view order, its num_rendered is read back (the one host
- * hand-off per view, rasterizer_impl.cu:283-284), its tile sort runs on the same internal stream
- * and its render on the caller's stream.  Per-view arrays hold one pointer per view
+ * Every stage is ONE launch over up to 8 views (grid.y = view), on an internal high-priority
+ * stream: preprocess (the Gaussians' parameters read once for the batch; GeometryState's means2D,
+ * depths and rgb, read by nothing downstream, are not written), the record-slot scans (beside the
+ * depth sorts, on an auxiliary stream), the depth sorts, the tile-count scans; then every view's
+ * num_rendered is read back (the one host hand-off, rasterizer_impl.cu:283-284); then the tile
+ * sorts with the instance emission fused into their first pass, tile ranges, tile orders, and on
+ * the caller's stream one render launch for the views (one launch tail per batch).  Per-view arrays hold one pointer per view
  * (viewmatrices, projmatrices, campos, the three state buffers, out_colors (3,H,W), out_invdepths
  * (1,H,W), radii (P) -- radii may be NULL); tan_fovx, tan_fovy, binning_capacity, num_rendered and
  * rendered are host arrays.  rendered[v] = 0: view v's binning buffer was NULL or smaller than
