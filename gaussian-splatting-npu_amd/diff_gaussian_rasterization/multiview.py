@@ -141,7 +141,8 @@ class DataParallelTrainer:
     batch of views; every rank holds a full replica of the Gaussians and renders its share of the
     batch (view v on rank v mod G, `views_of_batch`), and:
 
-    1. renders each of its views through GaussianRasterizer with train.py's inputs
+    1. renders its views -- as ONE MultiViewRasterizer batch (the default; `batched=False`: one
+       GaussianRasterizer call per view) -- with train.py's inputs
        (activations of gaussian_model.py:40-48,102-135; the separate-DC surface train.py selects
        with SparseGaussianAdam, gaussian_renderer/__init__.py:82-100; image clamped to [0, 1],
        :119), loss = (1 - lambda_dssim) L1 + lambda_dssim (1 - fused SSIM) (train.py:119-124),
@@ -164,13 +165,14 @@ class DataParallelTrainer:
     nothing is counted twice.  Backend-agnostic: RCCL ("nccl") on MI355X nodes, gloo in the tests.
     """
 
-    def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None):
+    def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None, batched=True):
         import diff_gaussian_rasterization as dgr
         self._dgr = dgr
         dev = raw["xyz"].device
         self.device = dev
         self.P = P = raw["xyz"].shape[0]
         self.group = group
+        self.batched = batched  # a rank's views as one MultiViewRasterizer batch (one launch per stage)
         self.lambda_dssim = lambda_dssim
         self.bg = bg if bg is not None else torch.zeros(3, device=dev)
         lr = dict(TRAIN_LR, **(lr or {}))
@@ -211,10 +213,39 @@ class DataParallelTrainer:
             opacities=act["opacities"], scales=act["scales"], rotations=act["rotations"], cov3D_precomp=None)
         return img.clamp(0, 1), means2D, radii
 
+    def render_views(self, settings_list, act=None):
+        """render() for a batch of views in one MultiViewRasterizer call: (clamped images (V,3,H,W),
+        screen-space points (V,P,3), radii (V,P))."""
+        act = act or self.activations()
+        means2D = torch.zeros((len(settings_list),) + tuple(act["means3D"].shape), dtype=act["means3D"].dtype,
+                              device=act["means3D"].device, requires_grad=True)
+        means2D.retain_grad()
+        imgs, radii, _ = self._dgr.MultiViewRasterizer(settings_list)(
+            means3D=act["means3D"], means2D=means2D, dc=act["dc"], shs=act["shs"], colors_precomp=None,
+            opacities=act["opacities"], scales=act["scales"], rotations=act["rotations"], cov3D_precomp=None)
+        return imgs.clamp(0, 1), means2D, radii
+
     def render_and_backward(self, views):
         """Step 1-2 for this rank's views: [(GaussianRasterizationSettings, gt image (3,H,W))].
-        Gradients accumulate into the flat buffer; returns the per-view losses."""
+        Gradients accumulate into the flat buffer; returns the per-view losses.  With `batched`
+        (the default) the views are one MultiViewRasterizer batch: each view's image is the one
+        GaussianRasterizer renders, bit for bit, and the parameter gradients are the sum over the
+        views up to fp32 summation order."""
         from fused_ssim import fused_ssim
+        if self.batched and len(views) > 1:
+            with self._dgr.accumulate_grads_in_place():
+                imgs, means2D, radii = self.render_views([s for s, _ in views])
+            losses = []
+            for v, (_, gt) in enumerate(views):
+                l1 = (imgs[v] - gt).abs().mean()
+                losses.append((1.0 - self.lambda_dssim) * l1 +
+                              self.lambda_dssim * (1.0 - fused_ssim(imgs[v][None], gt[None])))
+            torch.stack(losses).sum().backward()
+            with torch.no_grad():
+                for v in range(len(views)):
+                    add_view_stats(self.stats, means2D.grad[v], radii[v])
+                    self.visible_count += (radii[v] > 0).to(self.visible_count.dtype)
+            return [l.detach() for l in losses]
         losses = []
         for settings, gt in views:
             # xyz, f_dc, f_rest enter the rasterizer as leaves whose .grad are views of the flat

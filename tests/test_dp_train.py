@@ -127,3 +127,28 @@ def test_two_ranks_match_single_process():
         np.testing.assert_array_equal(s_r["max_radii2D"], stats["max_radii2D"])
         np.testing.assert_allclose(s_r["xyz_gradient_accum"], stats["xyz_gradient_accum"], rtol=1e-5, atol=1e-9)
     assert stats["denom"].max() > 0
+
+
+def test_batched_views_match_per_view_renders():
+    """A rank's views as one MultiViewRasterizer batch (the trainer's default) against one
+    GaussianRasterizer call per view: the per-view losses are bit-identical (same images), the
+    summed gradient buffer equal up to fp32 summation order, the densification counts equal."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "gaussian-splatting-npu_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dev = torch.device("cuda", 0)
+    out = {}
+    for batched in (False, True):
+        trainer, settings, targets = _setup(dev)
+        trainer.batched = batched
+        trainer.zero_grad()
+        losses = trainer.render_and_backward([(settings[v], targets[v]) for v in range(BATCH)])
+        torch.cuda.synchronize()
+        out[batched] = ([float(l) for l in losses], trainer.flat.clone().cpu().numpy(),
+                        trainer.stats["denom"].clone().cpu().numpy())
+    assert out[True][0] == out[False][0], (out[True][0], out[False][0])
+    a, b = out[True][1], out[False][1]
+    assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max() + 1e-9, np.abs(a - b).max()
+    np.testing.assert_array_equal(out[True][2], out[False][2])
