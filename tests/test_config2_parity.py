@@ -118,3 +118,46 @@ def test_config2_full_size(case, antialiasing):
     _grad_check(f"config2 aa={antialiasing} dc dL_ddc", out[5].cpu().numpy(), sh_ref[:, :1])
     _grad_check(f"config2 aa={antialiasing} dc dL_drest", out[6].cpu().numpy(), sh_ref[:, 1:])
     _grad_check(f"config2 aa={antialiasing} dc dL_dmeans3D", out[3].cpu().numpy(), og["dL_dmeans3D"])
+
+
+def test_config2_batched_views_match_single_views(case):
+    """The bench's batched step at full size: a MultiViewRasterizer batch of ring views 0 and 1
+    (batched prefix, emission fused into the tile sort, one render launch per pass) against one
+    GaussianRasterizer call per view (the path the oracle comparisons above check): images, radii,
+    inverse depths and each view's dL/dmean2D bit-identical, parameter gradients equal up to fp32
+    summation order (1e-5 of their max)."""
+    import diff_gaussian_rasterization as dgr
+    import synthetic
+    cams = [synthetic.Camera(W, H, view=v) for v in (0, 1)]
+    settings = [dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, bg=case["bg"].to(DEV), scale_modifier=1.0,
+        viewmatrix=c.world_view_transform.to(DEV), projmatrix=c.full_proj_transform.to(DEV), sh_degree=3,
+        campos=c.camera_center.to(DEV), prefiltered=False, debug=False, antialiasing=False) for c in cams]
+    grads = [tuple(g.to(DEV) for g in synthetic.make_grads(H, W, seed=1 + v)) for v in (0, 1)]
+
+    def leaves():
+        return {k: case["scene"][k].to(DEV).clone().requires_grad_(True)
+                for k in ("means3D", "shs", "opacities", "scales", "rotations")}
+
+    single = leaves()
+    outs, m2 = [], []
+    for s, (gc, gi) in zip(settings, grads):
+        means2D = torch.zeros_like(single["means3D"], requires_grad=True)
+        c, r, i = dgr.GaussianRasterizer(s)(means2D=means2D, **single)
+        torch.autograd.backward([c, i], [gc, gi])
+        outs.append((c.detach(), r, i.detach()))
+        m2.append(means2D.grad)
+    multi = leaves()
+    means2D = torch.zeros((2, P, 3), device=DEV, requires_grad=True)
+    c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **multi)
+    torch.autograd.backward([c, i], [torch.stack([g[0] for g in grads]), torch.stack([g[1] for g in grads])])
+    torch.cuda.synchronize()
+    for v in (0, 1):
+        assert torch.equal(c[v].detach(), outs[v][0]), f"view {v} image"
+        assert torch.equal(r[v], outs[v][1]), f"view {v} radii"
+        assert torch.equal(i[v].detach(), outs[v][2]), f"view {v} invdepth"
+        assert torch.equal(means2D.grad[v], m2[v]), f"view {v} dL/dmean2D"
+    for k in single:
+        ok, rel = common.allclose_rel(multi[k].grad.cpu().numpy(), single[k].grad.cpu().numpy(), rtol=1e-5,
+                                      atol=1e-12)
+        assert ok, f"d{k}: batch vs single views rel {rel:.3e}"
