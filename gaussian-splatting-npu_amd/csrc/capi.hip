@@ -503,7 +503,39 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
 
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, bool emitted, hipStream_t prefix);
+                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix);
+
+// The tile sort of one view (L > 0 instances) with the instance emission fused into its first
+// pass: the instances are generated from the depth-ordered rects; the sort's ping-pong buffers live
+// in the (not yet used) gradient-record region of the binning buffer, the first pass's count
+// matrix in the depth sort's ping-pong buffer (free by then).
+static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int L, int width, int height)
+{
+    const GeomLayout g = geom_layout(P);
+    const ImageLayout im = image_layout(width, height);
+    const BinLayout b = bin_layout(L);
+    const size_t q = align_up(4 * (size_t)L, 256);
+    char* w = bb + b.off[BIN_GRAD_INST];
+    TileSortJob j;
+    j.P = P;
+    j.L = L;
+    j.sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
+    j.offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    j.sorted_rects = at<uint2>(gb, g.off[GEOM_SORTED_RECT]);
+    j.rec_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+    j.pass1_scratch = gb + g.off[GEOM_DSORT_TMP];
+    j.k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
+    j.k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
+    j.v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
+    j.v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
+    j.scratch = bb + b.off[BIN_RADIX_SCRATCH];
+    j.out_slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
+    j.out_ids = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
+    j.out_tiles = at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
+    j.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
+    j.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    return j;
+}
 
 int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P, int num_rendered,
                        const float* background, int width, int height, const float* colors_precomp,
@@ -515,7 +547,7 @@ int gsr_forward_render(char* geometry_buffer, char* binning_buffer, char* image_
     const int rc = prefix_begin((hipStream_t)stream, &ps);
     if (rc) return rc;
     return forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, num_rendered, background, width,
-                               height, out_color, depth, debug, stream, false, ps);
+                               height, out_color, depth, debug, stream, ps);
 }
 
 // render_fwd's arguments for a view whose binning is complete
@@ -543,19 +575,17 @@ static RenderFwdArgs render_fwd_args(char* gb, char* bb, char* ib, int P, int L,
     return r;
 }
 
-// Forward, second half.  `emitted`: the early emission (gsr_forward_prealloc_dc) already wrote the
-// instances into this binning buffer.
+// Forward, second half: the tile sort (emission fused in), tile ranges and tile order on the
+// prefix stream, render_fwd on the caller's.
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, bool emitted, hipStream_t prefix)
+                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix)
 {
-    // binning on the prefix stream, render_fwd on the caller's (colors_precomp was folded into the
-    // render record by preprocess)
+    // (colors_precomp was folded into the render record by preprocess)
     hipStream_t s = prefix;
     hipStream_t caller = (hipStream_t)stream;
     if (P <= 0) return prefix_end(caller, prefix);
     const int L = num_rendered;
-    const GeomLayout g = geom_layout(P);
     const ImageLayout im = image_layout(width, height);
     const BinLayout b = bin_layout(L);
     char* gb = geometry_buffer;
@@ -565,39 +595,15 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
     const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     const int T = (int)(gx * gy);
-    uint32_t* point_list = L > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     uint32_t* sorted_tiles = L > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr;
-    uint32_t* slot = L > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
-    uint32_t* emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     if (L > 0) {
-        // emission arrays and sort ping-pong live in the (not yet used) gradient-record region
-        const size_t n = (size_t)L;
-        char* w = bb + b.off[BIN_GRAD_INST];
-        const size_t q = align_up(4 * n, 256);
-        uint32_t* tile_keys = reinterpret_cast<uint32_t*>(w);
-        uint2* pairs = reinterpret_cast<uint2*>(w + 8 * q);  // (record slot, Gaussian id) per instance
-        uint32_t* k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
-        uint32_t* k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
-        uint32_t* v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
-        uint32_t* v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
-        if (!emitted) {
-            ProfScope ps_(PK_EMIT, s);
-            HIP_TRY(launch_emit_instances(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
-                                          at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
-                                          at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx, tile_keys, pairs, emit_start,
-                                          at<uint32_t>(bb, b.off[BIN_VALID]),
-                                          at<uint2>(ib, im.off[IMG_RANGES]), T, s));
-        }
-        DEBUG_SYNC(s);
-        // stable sort by tile id over bits [0, bit) (rasterizer_impl.cu:303-311 sorts [0, 32+bit))
-        const int bit = (int)higher_msb(gx * gy);
-        {
-            ProfScope ps_(PK_TILE_SORT, s);
-            HIP_TRY(radix_sort(L, bit, tile_keys, pairs, k0, v0, k1, v1, slot, point_list, sorted_tiles,
-                               bb + b.off[BIN_RADIX_SCRATCH], s));
-        }
-        DEBUG_SYNC(s);
+        // stable sort by tile id over bits [0, msb(T)) of the depth-ordered instances
+        // (rasterizer_impl.cu:303-311 sorts [0, 32 + msb(T)) of the tile|depth keys)
+        const TileSortJob j = fused_tile_sort_job(gb, bb, ib, P, L, width, height);
+        ProfScope ps_(PK_TILE_SORT, s);
+        HIP_TRY(tile_sort_fused_batch(&j, 1, gx, T, s));
     }
+    DEBUG_SYNC(s);
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     {
         ProfScope ps_(PK_RANGES, s);
@@ -673,25 +679,6 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
                                  viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
                                  radii, debug, ps, &h);
     if (rc) return rc;
-    // Emission does not need num_rendered on the host: enqueue it now, so the GPU works through
-    // the read-back below instead of idling until the host launches it (it resolves its output
-    // arrays from the device-side total and writes nothing if the buffer is too small).
-    const bool early = binning_buffer != nullptr && binning_capacity > 0;
-    if (early) {
-        hipStream_t s = ps;
-        const GeomLayout g = geom_layout(P);
-        const ImageLayout im = image_layout(width, height);
-        const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
-        const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
-        char* gb = geometry_buffer;
-        ProfScope ps_(PK_EMIT, s);
-        HIP_TRY(launch_emit_instances_early(P, at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]),
-                                            at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
-                                            at<uint2>(gb, g.off[GEOM_SORTED_RECT]), gx,
-                                            at<uint32_t>(gb, g.off[GEOM_EMIT_START]), binning_buffer,
-                                            binning_capacity, at<uint2>(image_buffer, im.off[IMG_RANGES]),
-                                            (int)(gx * gy), s));
-    }
     int L = 0;
     rc = forward_geometry_wait(h, ps, &L);
     *num_rendered = L;
@@ -702,35 +689,10 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity)  // caller allocates
         return prefix_end((hipStream_t)stream, ps);
     rc = forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
-                             out_color, depth, debug, stream, early && L > 0, ps);
+                             out_color, depth, debug, stream, ps);
     if (rc) return rc;
     *rendered = 1;
     return GSR_OK;
-}
-
-// Tile-sort job of one view whose instances were emitted into binning buffer bb (layout of L):
-// the emission arrays and ping-pong buffers live in the not yet used gradient-record region.
-static SortJob tile_sort_job(char* bb, int L)
-{
-    const BinLayout b = bin_layout(L);
-    const size_t q = align_up(4 * (size_t)L, 256);
-    char* w = bb + b.off[BIN_GRAD_INST];
-    SortJob j;
-    j.n = L;
-    j.keys_in = reinterpret_cast<const uint32_t*>(w);                  // tile keys (emission)
-    j.pairs = reinterpret_cast<const uint2*>(w + 8 * q);               // (record slot, Gaussian id)
-    j.k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
-    j.k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
-    j.v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
-    j.v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
-    j.out_x = at<uint32_t>(bb, b.off[BIN_SLOT]);
-    j.out_y = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
-    j.sorted_keys = at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
-    j.scratch = bb + b.off[BIN_RADIX_SCRATCH];
-    j.rects = nullptr;
-    j.sorted_rects = nullptr;
-    j.sorted_counts = nullptr;
-    return j;
 }
 
 int gsr_forward_views(int V, int P, int D, int M, const float* background, int width, int height,
@@ -846,13 +808,7 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         char* ib = image_buffers[v];
         char* gb = geometry_buffers[v];
         const BinLayout b = bin_layout(L[v]);
-        if (L[v] > 0) {
-            const SortJob t = tile_sort_job(bb, L[v]);
-            tsort[ns++] = {P, L[v], at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
-                           at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_EMIT_START]),
-                           gb + g.off[GEOM_DSORT_TMP], t.k0, t.v0, t.k1, t.v1, t.scratch, t.out_x, t.out_y,
-                           t.sorted_keys, at<uint32_t>(bb, b.off[BIN_VALID]), at<uint2>(ib, im.off[IMG_RANGES])};
-        }
+        if (L[v] > 0) tsort[ns++] = fused_tile_sort_job(gb, bb, ib, P, L[v], width, height);
         rj[nf] = {L[v], L[v] > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr, at<uint2>(ib, im.off[IMG_RANGES])};
         oj[nf] = {at<uint2>(ib, im.off[IMG_RANGES]), nullptr, at<uint32_t>(ib, im.off[IMG_TILE_ORDER])};
         fit[nf++] = v;

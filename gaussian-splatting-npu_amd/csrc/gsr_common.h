@@ -242,25 +242,6 @@ inline ImageLayout image_layout(int W, int H)
     return l;
 }
 
-// bin_layout on the device (the early emission resolves its output arrays from the device-side
-// num_rendered): the tile sort's scratch size restated for 2,048-key chunks; a static_assert in
-// radix.hip keeps it equal to radix_status_bytes.
-__host__ __device__ inline size_t tile_sort_status_bytes(size_t n)
-{
-    const size_t chunks = (n + 2047) / 2048;
-    return align_up(chunks * 256 * 4 + 256, 256) + align_up(256 * 4, 256);
-}
-
-__host__ __device__ inline BinLayout bin_layout_dev(size_t n)
-{
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, tile_sort_status_bytes(n), 4 * ((n + 31) / 32), n};
-    BinLayout l;
-    size_t o = 0;
-    for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }
-    l.off[BIN_COUNT] = o;
-    return l;
-}
-
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);

@@ -247,21 +247,6 @@ struct TileSortJob {
 size_t fused_pass1_scratch_bytes(int P);
 hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s);
 
-struct EmitJob {  // emission of one view (bb != null: the early form, arrays resolved on the device)
-    int P;
-    const uint32_t* sorted_ids;
-    const uint32_t* offsets_d;
-    const uint2* sorted_rects;
-    const uint32_t* rec_start;
-    uint32_t* tile_keys;
-    uint2* pairs;
-    uint32_t* valid;
-    uint2* ranges;
-    char* bb;
-    size_t capacity;
-};
-hipError_t launch_emit_batch(const EmitJob* jobs, int V, uint32_t gx, int T, hipStream_t s);
-
 struct RangesJob {
     int L;
     const uint32_t* sorted_tiles;
@@ -282,16 +267,7 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pa
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
                       uint32_t* sorted_counts = nullptr);
-// Emission: tile_keys[i] and pairs[i] = (gradient-record slot, Gaussian id) of every instance, in
-// depth order (rec_start: index-order exclusive scan of the tile counts).  Also clears the valid
-// bit mask (the backward's record flags) and ranges[0..T) for tile_ranges.
-hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
-                                       const uint2* sorted_rects, uint32_t gx, const uint32_t* rec_start, char* bb,
-                                       size_t capacity, uint2* ranges, int T, hipStream_t s);
-hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
-                                 uint32_t gx, uint32_t* tile_keys, uint2* pairs, const uint32_t* rec_start,
-                                 uint32_t* valid, uint2* ranges, int T, hipStream_t s);
-// ranges must be zero on entry unless L == 0 (emit_instances clears them)
+// ranges must be zero on entry unless L == 0 (the fused tile sort's first pass clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
                              uint64_t* keys, hipStream_t s);

@@ -5,10 +5,11 @@
 // Binning scheme (same result as the reference's 64-bit tile|depth key sort):
 //   1. sort the P Gaussians by depth bits (4 x 8-bit passes; ties keep index order;
 //      culled Gaussians carry key 0xFFFFFFFF and land last);
-//   2. emit (tile, Gaussian) instances in that depth order (y-major, then x, inside each
-//      Gaussian's rect, exactly like duplicateWithKeys, rasterizer_impl.cu:98-109);
-//   3. stable-sort the instances by tile id alone: ceil(bit/8) passes over bit = msb(T) bits
-//      (2 at 1080p) instead of the reference's ceil((32+bit)/8) passes over 12-byte pairs.
+//   2. the (tile, Gaussian) instances in that depth order (y-major, then x, inside each
+//      Gaussian's rect, exactly like duplicateWithKeys, rasterizer_impl.cu:98-109) are
+//      stably sorted by tile id alone: ceil(bit/8) passes over bit = msb(T) bits (2 at 1080p)
+//      instead of the reference's ceil((32+bit)/8) passes over 12-byte pairs; the first pass
+//      generates the instances itself from the depth-ordered rects (no emission array).
 // Because both sorts are stable, every tile's list comes out ordered by (depth bits,
 // Gaussian index) -- the reference's order -- and the sorted key array
 // (tile << 32 | depth bits) is bit-identical to the reference's.
@@ -330,89 +331,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
         }
     }
 }
-
-// Emission in depth order: instances [off(k-1), off(k)) of depth rank k belong to Gaussian
-// g = sorted_ids[k]; tiles y-major then x inside its rect (rasterizer_impl.cu:98-109).  Each
-// instance carries (slot, g): its gradient-record slot rec_start[g] + j (j-th tile of g), with
-// rec_start the index-order exclusive scan of the tile counts -- a Gaussian's records are
-// contiguous and Gaussians' record ranges follow their index, so the per-Gaussian gather of the
-// backward (preprocess_bwd, thread i <-> Gaussian i) reads consecutive lines across a wave.
-// One wave per 64 consecutive ranks: the lanes first publish their rects (read in depth order:
-// the depth sort laid them out, no gathers by Gaussian id) in LDS, then the wave fills its whole
-// instance range 64 consecutive instances at a time (coalesced stores), each lane finding the
-// owner of its instance by a binary search over the 64 rect starts.
-// Early form (bb != null): launched before the host has read num_rendered back, so the output
-// arrays are resolved here from the device-side total (offsets_d[P-1]) with the binning layout
-// the host will use; if that layout does not fit in `capacity` bytes, nothing is written (the
-// host then allocates the exact size and emits again).
-__global__ void __launch_bounds__(256) emit_instances_kernel(const ViewBatch<EmitJob> B, uint32_t gx, int T)
-{
-    const EmitJob& J = B.v[blockIdx.y];
-    const int P = J.P;
-    const uint32_t* sorted_ids = J.sorted_ids;
-    const uint32_t* offsets_d = J.offsets_d;
-    const uint2* sorted_rects = J.sorted_rects;
-    const uint32_t* rec_start = J.rec_start;
-    uint32_t* tile_keys = J.tile_keys;
-    uint2* pairs = J.pairs;
-    uint32_t* valid = J.valid;
-    uint2* ranges = J.ranges;
-    char* bb = J.bb;
-    const size_t capacity = J.capacity;
-    __shared__ uint32_t s_start[4][64], s_x0[4][64], s_y0[4][64], s_w[4][64], s_g[4][64], s_rec[4][64];
-    if (bb) {
-        const size_t n = offsets_d[P - 1];
-        const BinLayout b = bin_layout_dev(n);
-        if (n == 0 || b.off[BIN_COUNT] + 256 > capacity) return;  // gsr_binning_buffer_size = total + 256
-        const size_t q = align_up(4 * n, 256);
-        tile_keys = reinterpret_cast<uint32_t*>(bb + b.off[BIN_GRAD_INST]);
-        pairs = reinterpret_cast<uint2*>(bb + b.off[BIN_GRAD_INST] + 8 * q);
-        valid = reinterpret_cast<uint32_t*>(bb + b.off[BIN_VALID]);
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int k0 = (blockIdx.x * 4 + w) * 64;
-    // ranges must be zero for tile_ranges (empty tiles keep (0, 0)): cleared here, not by a memset
-    for (int t = blockIdx.x * 256 + (int)threadIdx.x; t < T; t += gridDim.x * 256) ranges[t] = make_uint2(0u, 0u);
-    if (k0 >= P) return;  // whole wave out of range (waves are independent: no block barriers)
-    const int k = k0 + lane;
-    const int kc = min(k, P - 1);
-    const uint32_t g = sorted_ids[kc];
-    const uint32_t prev = offsets_d[max(kc - 1, 0)];
-    const uint2 rc = sorted_rects[kc];
-    const uint32_t wend = offsets_d[min(k0 + 63, P - 1)];
-    const uint32_t r0 = rec_start[g];
-    uint32_t start = 0xFFFFFFFFu, x0 = 0, y0 = 0, wd = 1;
-    if (k < P) {
-        start = k == 0 ? 0u : prev;
-        x0 = rc.x & 0xFFFFu;
-        y0 = rc.x >> 16;
-        wd = max((rc.y & 0xFFFFu) - x0, 1u);
-    }
-    s_start[w][lane] = start;
-    s_x0[w][lane] = x0;
-    s_y0[w][lane] = y0;
-    s_w[w][lane] = wd;
-    s_g[w][lane] = g;
-    s_rec[w][lane] = r0;
-    const uint32_t wbeg = (uint32_t)__shfl((int)start, 0, 64);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (uint32_t sl = wbeg + lane; sl < wend; sl += 64) {
-        // largest j with start_j <= sl (ranks without instances share their successor's start)
-        int j = 0;
-#pragma unroll
-        for (int step = 32; step >= 1; step >>= 1)
-            if (s_start[w][j + step] <= sl) j += step;
-        const uint32_t local = sl - s_start[w][j];
-        const uint32_t wj = s_w[w][j];
-        const uint32_t yy = local / wj, xx = local - yy * wj;
-        tile_keys[sl] = (s_y0[w][j] + yy) * gx + (s_x0[w][j] + xx);
-        pairs[sl] = make_uint2(s_rec[w][j] + local, s_g[w][j]);
-        if ((sl & 31u) == 0u) valid[sl >> 5] = 0u;  // the backward flags the records it writes
-    }
-}
-
 
 // ---------------------------------------------------------------------------
 // Emission fused into the first tile-sort pass.  Chunk c of a view = the instances of its depth
@@ -740,7 +658,7 @@ size_t radix_status_bytes(int n, int npass)
     return align_up(rs_chunks(n) * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
 }
 static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 2048 && RS_MAXBINS == 256,
-              "tile_sort_status_bytes (gsr_common.h) restates radix_status_bytes for 2,048-key chunks");
+              "2,048-key chunks");
 
 // Full LSD sort of n u32 keys over bits [0, nbits), stable.  Payload: the input index i, or with
 // `pairs` the u32x2 pairs[i].  Ping-pongs between (k0,v0) and (k1,v1) (v: u32, or u32x2 with
@@ -896,42 +814,6 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pa
     const SortJob j = {n, keys_in, pairs, k0, v0, k1, v1, out_x, out_y, sorted_keys, scratch, rects, sorted_rects,
                        sorted_counts};
     return radix_sort_batch(&j, 1, nbits, s);
-}
-
-hipError_t launch_emit_batch(const EmitJob* jobs, int V, uint32_t gx, int T, hipStream_t s)
-{
-    return for_groups(V, [&](int v0, int nv) -> hipError_t {
-        ViewBatch<EmitJob> B;
-        B.n = nv;
-        int maxp = 0;
-        for (int v = 0; v < nv; v++) {
-            B.v[v] = jobs[v0 + v];
-            maxp = max(maxp, B.v[v].P);
-        }
-        if (maxp <= 0) return hipSuccess;
-        hipLaunchKernelGGL(emit_instances_kernel, dim3((unsigned)((maxp + 255) / 256), (unsigned)nv), dim3(256), 0, s,
-                           B, gx, T);
-        return hipGetLastError();
-    });
-}
-
-hipError_t launch_emit_instances(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d, const uint2* sorted_rects,
-                                 uint32_t gx, uint32_t* tile_keys, uint2* pairs, const uint32_t* rec_start,
-                                 uint32_t* valid, uint2* ranges, int T, hipStream_t s)
-{
-    if (P <= 0) return hipSuccess;
-    const EmitJob j = {P, sorted_ids, offsets_d, sorted_rects, rec_start, tile_keys, pairs, valid, ranges, nullptr, 0};
-    return launch_emit_batch(&j, 1, gx, T, s);
-}
-
-hipError_t launch_emit_instances_early(int P, const uint32_t* sorted_ids, const uint32_t* offsets_d,
-                                       const uint2* sorted_rects, uint32_t gx, const uint32_t* rec_start, char* bb,
-                                       size_t capacity, uint2* ranges, int T, hipStream_t s)
-{
-    if (P <= 0 || !bb) return hipSuccess;
-    const EmitJob j = {P, sorted_ids, offsets_d, sorted_rects, rec_start, nullptr, nullptr, nullptr, ranges, bb,
-                       capacity};
-    return launch_emit_batch(&j, 1, gx, T, s);
 }
 
 hipError_t launch_tile_ranges_batch(const RangesJob* jobs, int V, int T, hipStream_t s)
