@@ -225,6 +225,32 @@ def test_uhd_view_multi_pass_tile_order():
         assert ok_, f"grad {hk} rel err {rel:.3e}"
 
 
+def test_8k_view_three_pass_tile_sort():
+    """7680x4320 (129,600 tiles: 17-bit tile ids): the tile sort takes three passes -- the fused
+    emission pass and two plain ones; keys, Gaussian ids, tile ranges and radii bit-exact against
+    the oracle, the image through check_render."""
+    dgr = _dgr()
+    case = common.make_case(P=3000, H=4320, W=7680)
+    o, _ = common.run_oracle(case, nthreads=8, backward=False)
+    s = _settings(case)
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    L, color, radii, geom, binning, img, inv = dgr._C.rasterize_gaussians(
+        s.bg, sc["means3D"], torch.Tensor([]), sc["opacities"], sc["scales"], sc["rotations"], 1.0,
+        torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width,
+        sc["shs"], s.sh_degree, s.campos, False, False, False)
+    torch.cuda.synchronize()
+    P = sc["means3D"].shape[0]
+    assert L == o.num_rendered and L > 0
+    np.testing.assert_array_equal(radii.cpu().numpy(), o.radii)
+    keys, vals, ranges = dgr._C.sorted_keys(geom, binning, img, P, L, s.image_width, s.image_height)
+    np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
+    np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+    kw = {"means3D": sc["means3D"], "shs": sc["shs"], "opacities": sc["opacities"], "scales": sc["scales"],
+          "rotations": sc["rotations"]}
+    common.check_render("8k 3k", _hip_render(s, kw, color.cpu().numpy(), inv.cpu().numpy()), _ora_render(o))
+
+
 def test_mark_visible():
     import oracle
     dgr = _dgr()
