@@ -74,7 +74,7 @@ int pinned(int slot, uint32_t** out)
 }
 
 // ---------------------------------------------------------------------------
-// The forward's binning prefix (preprocess, depth sort, scan, emission, tile sort, tile ranges,
+// The forward's binning prefix (preprocess, depth sort, scans, tile sort, tile ranges,
 // tile order: small, latency-bound launches) runs on an internal stream of the highest priority,
 // forked from the caller's stream and joined back into it before render_fwd.  When the caller
 // overlaps views on several streams (the forward of view v+1 beside the backward of view v,
@@ -383,7 +383,7 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
     const GeomLayout g = geom_layout(P);
     // 1b. each Gaussian's first gradient-record slot: index-order exclusive scan of the tile counts
     //     (records in Gaussian order: preprocess_bwd's per-Gaussian gathers are contiguous), on the
-    //     auxiliary stream beside the depth sort; emission (which reads it) waits for it
+    //     auxiliary stream beside the depth sort; the tile sort's first pass (which reads it) waits for it
     hipStream_t aux = s;
     {
         // (one auxiliary stream per device: views whose prefixes run side by side on several
@@ -901,7 +901,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
                                       at<uint32_t>(ib, im.off[IMG_TILE_ORDER]), s));
         }
         {
-            ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emit_instances
+            ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's tile sort
             HIP_TRY(launch_render_bwd(r, T, s));
         }
         DEBUG_SYNC(s);
@@ -1004,7 +1004,7 @@ int gsr_backward_render(int P, int R, const float* background, int width, int he
                                   at<uint32_t>(image_buffer, im.off[IMG_TILE_ORDER]), s));
     }
     {
-        ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's emission
+        ProfScope ps_(PK_RENDER_BWD, s);  // valid[] was cleared by the forward's tile sort
         HIP_TRY(launch_render_bwd(r, r.T, s));
     }
     DEBUG_SYNC(s);

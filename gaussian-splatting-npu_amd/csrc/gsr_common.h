@@ -195,11 +195,11 @@ enum ImageArray {
 enum BinArray {
     BIN_POINT_LIST = 0,   // u32[L] Gaussian id of sorted position
     BIN_SORTED_TILES,     // u32[L] tile id of sorted position
-    BIN_SLOT,             // u32[L] emission slot of sorted position
+    BIN_SLOT,             // u32[L] gradient-record slot of sorted position
     BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
-                          // it hosts the emission arrays and sort ping-pong buffers (40 B/instance)
+                          // it hosts the tile sort's ping-pong buffers (24 B/instance)
     BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
-    BIN_VALID,            // u32[ceil(L/32)] bit per emission slot: its gradient record was written (backward)
+    BIN_VALID,            // u32[ceil(L/32)] bit per record slot: its gradient record was written (backward)
     BIN_HIT,              // u8[L] per sorted position: quadrants (bit w = 8x8 quadrant w) with a pixel the
                           // entry contributed to in the forward (render_fwd), read by render_bwd
     BIN_COUNT

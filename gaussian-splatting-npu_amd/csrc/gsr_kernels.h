@@ -70,9 +70,9 @@ struct RenderBwdArgs {
     const float4* accum;  // IMG_ACCUM written by the forward
     const float* dL_dpixels;
     const float* dL_invdepths;  // (1,H,W) or null
-    const uint32_t* slot;       // emission slot of each sorted position
+    const uint32_t* slot;       // gradient-record slot of each sorted position
     uint32_t* valid;            // bit (slot & 31) of valid[slot >> 5] set for every record written (cleared by emit)
-    float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its emission slot
+    float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its record slot
     const uint8_t* hit;         // BIN_HIT (render_fwd): the quadrants each entry contributed to
 };
 
@@ -111,12 +111,12 @@ struct PreprocessBwdArgs {
     const float* campos;
     int antialiasing;
     // per-instance gradient records and the gather map
-    const float* grad_inst;         // f32x12[L], emission order
+    const float* grad_inst;         // f32x12[L], at the record slots (Gaussian order)
     const uint32_t* valid;          // one bit per slot: records not flagged were never written (no contribution)
     // (Gaussian i's records are slots [emit_start[i], +tiles_touched[i]), emit_start the index-order
     // exclusive scan of tiles_touched)
     const uint32_t* emit_start;     // first record slot of Gaussian i
-    const uint32_t* tiles_touched;  // number of emission slots of Gaussian i
+    const uint32_t* tiles_touched;  // number of record slots of Gaussian i
     int has_invdepth;
     const float4* conic_opacity;    // GEOM_CONIC_OPACITY (the rendered, AA-scaled opacity in .w)
     int W, H;

@@ -38,7 +38,7 @@ struct BwdIn {
 constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +3 us, 2: +10 us)
 
 // Sum of one Gaussian's per-tile gradient records of one view.  Its records are contiguous
-// (emission order); entries that contributed to no pixel were never written (their bit in the valid
+// (slots [emit_start, + tiles_touched)); entries that contributed to no pixel were never written (their bit in the valid
 // mask is 0) and are not read (most slots: records are sparse).  The mask has one bit per slot
 // (L/8 bytes: it stays in L2), so a Gaussian's flags are one or two words; its flagged records are
 // then read B at a time in slot order (bitwise reproducible sums).

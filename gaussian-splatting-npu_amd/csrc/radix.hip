@@ -819,7 +819,7 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pa
 hipError_t launch_tile_ranges_batch(const RangesJob* jobs, int V, int T, hipStream_t s)
 {
     for (int v = 0; v < V; v++) {
-        if (jobs[v].L <= 0) {  // no emission ran to clear them
+        if (jobs[v].L <= 0) {  // no tile sort ran to clear them
             const hipError_t e = hipMemsetAsync(jobs[v].ranges, 0, sizeof(uint2) * (size_t)T, s);
             if (e != hipSuccess) return e;
         } else if ((uintptr_t)jobs[v].sorted_tiles & 15) {

@@ -500,12 +500,12 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 // (exact ellipse test + per-quadrant max n_contrib); the surviving entries are taken from the
 // ballot in list order, three at a time: every lane accumulates its pixels' ten gradient terms,
 // the transposed reduction sums the 64 lanes, and the even lanes 0..58 store the 3 records (10
-// contiguous floats each) at their emission slots and flag them valid; entries that survive
+// contiguous floats each) at their record slots and flag them valid; entries that survive
 // no quadrant get no record.  No atomics:
 // per-(tile, Gaussian) sums are bitwise reproducible.
 // Tiles (independent waves) per workgroup.  A retiring 4-wave workgroup frees one wave slot on
 // each SIMD of its CU -- the footprint of a 256-thread binning-prefix workgroup of the next view
-// (depth sort, scans, emission, tile sort), which then runs beside this launch instead of
+// (depth sort, scans, tile sort), which then runs beside this launch instead of
 // waiting for its last wave; single-wave workgroups left no such hole (a freed slot was refilled
 // by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
 // 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
@@ -678,7 +678,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
             const int k = lane >> 1;  // value held by this lane (lanes 2k, 2k + 1)
             const int jj = k / GF_NUM;
             const int jl = s_list[min(g0 + jj, 63)];
-            const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // emission slot of entry jl
+            const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // record slot of entry jl
             if ((lane & 1) == 0 && k < G * GF_NUM && g0 + jj < cnt) {
                 a.grad_inst[(size_t)dst * GRAD_REC + (k - jj * GF_NUM)] = r;
                 if (k == jj * GF_NUM) atomicOr(&a.valid[dst >> 5], 1u << (dst & 31u));
