@@ -20,12 +20,12 @@
 // stops fetching once all four are (the reference's __syncthreads_count,
 // forward.cu:329-331).
 //
-// Backward: one wave64 per tile, 4 pixels per lane (one per quadrant); traversal is
-// back-to-front from each pixel's n_contrib; entries behind a quadrant's largest
-// n_contrib are culled for that quadrant, batches behind the tile's largest are not
-// loaded.  The ten per-(pixel, Gaussian) gradient terms are reduced over the tile's 256
-// pixels on chip (in-lane over the 4 pixels, then a transposed cross-lane reduction) and
-// stored once per (tile, Gaussian) entry -- no global atomics, bitwise-reproducible sums
+// Backward: one wave64 per tile, split into four 16-lane groups, one per quadrant, each lane
+// owning 4 pixels of its group's quadrant; each group walks only the entries that contributed
+// in its quadrant in the forward, front to back.  The ten per-(pixel, Gaussian) gradient terms
+// are reduced on chip (in-lane over the 4 pixels, a transposed cross-lane reduction over the
+// group, the <= 4 quadrant partials added in LDS in a fixed order) and stored once per
+// (tile, Gaussian) entry -- no global atomics, bitwise-reproducible sums
 // (the reference issues up to ten float atomics per contributing pixel,
 // backward.cu:593-635).
 #include "gsr_common.h"
@@ -90,8 +90,8 @@ __device__ __forceinline__ uint32_t quad_mask(const float4 r0, const float4 k, u
 
 // ---- packed-f32 pixel pairs -----------------------------------------------------------------
 // gfx950 issues v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 at the cost of one scalar f32 op, so
-// the backward evaluates its pixels two at a time: each lane owns two horizontally paired
-// pixels (x, x + 8) of the upper and of the lower half of the tile.
+// the backward evaluates its pixels two at a time: each lane owns two pairs of pixels (x, x + 4)
+// in one row of one 8x8 quadrant.
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ v2f fma2(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
@@ -389,21 +389,23 @@ __device__ __forceinline__ float dpp(float x)
 {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
-constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141, DPP_QUAD_2301 = 0x4E, DPP_QUAD_1032 = 0xB1;
+constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141;
 
-// Sums 32 per-lane values over the 64 lanes of the wave and returns, in lanes 2k and 2k + 1, the
-// wave total of v[k].  Recursive halving: each exchange step hands half of the live values to
-// the partner lane (v_permlane32_swap, v_permlane16_swap, then DPP row_mirror / row_half_mirror /
-// quad_perm fused into v_add_f32_dpp), and a last quad_perm butterfly adds the two lanes that
-// still hold halves of one total: 32 exchanges for 32 totals instead of the 32 x 6 shuffle+add
-// pairs of per-value butterflies, in half the registers of a 64-value transpose.
-__device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lane)
+// Sums 32 per-lane values over each of four 16-lane groups and returns in r0 / r1 of lane l the
+// group totals of v[2 (l >> 2)] / v[2 (l >> 2) + 1].  Recursive halving: each exchange step hands
+// half of the live values to the partner lane -- l ^ 32 (v_permlane32_swap), l ^ 16
+// (v_permlane16_swap), then DPP row_mirror (l ^ 15) and row_half_mirror (l ^ 7) fused into
+// v_add_f32_dpp.  A group, quad_group(l), is the set of lanes those four partners connect: the
+// coset of l & 15 under {0, 7, 8, 15}, across the four rows.  66 instructions for 4 x 32 totals,
+// against 32 x 4 shuffle+add pairs of per-value butterflies.
+__device__ __forceinline__ int quad_group(int lane) { return (lane & 4) ? 3 - (lane & 3) : (lane & 3); }
+__device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lane, float& r0, float& r1)
 {
 #pragma unroll
     for (int i = 0; i < 16; i++) { xswap32(v[i], v[i + 16]); v[i] = v[i] + v[i + 16]; }
 #pragma unroll
     for (int i = 0; i < 8; i++) { xswap16(v[i], v[i + 8]); v[i] = v[i] + v[i + 8]; }
-    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
+    const bool b3 = lane & 8, b2 = lane & 4;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         const float keep = b3 ? v[i + 4] : v[i], send = b3 ? v[i] : v[i + 4];
@@ -414,9 +416,8 @@ __device__ __forceinline__ float wave_transpose_reduce32(float (&v)[32], int lan
         const float keep = b2 ? v[i + 2] : v[i], send = b2 ? v[i] : v[i + 2];
         v[i] = keep + dpp<DPP_ROW_HALF_MIRROR>(send);
     }
-    const float keep = b1 ? v[1] : v[0], send = b1 ? v[0] : v[1];
-    const float h = keep + dpp<DPP_QUAD_2301>(send);
-    return h + dpp<DPP_QUAD_1032>(h);
+    r0 = v[0];
+    r1 = v[1];
 }
 
 // State of two pixels of the backward pass (backward.cu:498-528, restated front to back).
@@ -493,16 +494,19 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
     }
 }
 
-// Backward: ONE wave per 16x16 tile, each lane owning 4 pixels as two packed pairs (upper half:
-// quadrants 0|1, lower half: 2|3), so there are no workgroup barriers in the main loop and no
-// cross-wave combine.  The list is walked front to back in batches of 64 entries up to the
-// tile's largest n_contrib; each lane stages one record in LDS and computes its quadrant mask
-// (exact ellipse test + per-quadrant max n_contrib); the surviving entries are taken from the
-// ballot in list order, three at a time: every lane accumulates its pixels' ten gradient terms,
-// the transposed reduction sums the 64 lanes, and the even lanes 0..58 store the 3 records (10
-// contiguous floats each) at their record slots and flag them valid; entries that survive
-// no quadrant get no record.  No atomics:
-// per-(tile, Gaussian) sums are bitwise reproducible.
+// Backward: ONE wave per 16x16 tile, so there are no workgroup barriers in the main loop and no
+// cross-wave combine.  Lane group quad_group(lane) owns quadrant (g & 1, g >> 1); lane
+// l >> 2 of it the pixels (x, x + 4) and (x + 2, x + 6) of one quadrant row as two packed pairs.
+// The list is walked front to back in batches of 64 entries up to the tile's largest n_contrib:
+// each lane stages the record of its entry if that entry contributed anywhere in the forward, and
+// each quadrant's contributing entries are listed in LDS (ballot + mbcnt, list order).  Iteration
+// i then evaluates the i-th entry of every quadrant at once (pixels of different quadrants share no
+// state; a group past its list evaluates a staged record at position "never", which adds zeros),
+// three iterations per transposed reduction; the groups add their partial totals into the
+// entries' LDS sums one group after the other, and at the end of the batch every contributing
+// entry's lane stores its record (10 floats) at its record slot and flags it valid.  Against one
+// 64-lane pass per entry over the half-tiles it reaches, this skips the pixel pairs of quadrants
+// an entry does not reach (25 % of them) and reduces over 16 lanes: render_bwd -11 %.
 // Tiles (independent waves) per workgroup.  A retiring 4-wave workgroup frees one wave slot on
 // each SIMD of its CU -- the footprint of a 256-thread binning-prefix workgroup of the next view
 // (depth sort, scans, tile sort), which then runs beside this launch instead of
@@ -512,22 +516,26 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_
 constexpr int BWD_TPW = 4;
 
 template <bool HAS_INV>
-__global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
+__global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_eu(4))) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
 {
 #pragma clang fp contract(fast)
     const RenderBwdArgs& a = B.v[blockIdx.y];  // a batch of views: one launch tail per batch
-    constexpr int G = 3;  // Gaussians per transposed reduction (3 x 10 gradient terms <= 32 values)
+    constexpr int G = 3;  // entries per group and transposed reduction (3 x 10 gradient terms <= 32 values)
     const int wv = BWD_TPW == 1 ? 0 : (int)(threadIdx.x >> 6);
     const int ti = (int)blockIdx.x * BWD_TPW + wv;
     if (ti >= a.T) return;  // waves are independent: no workgroup barrier below
     const uint32_t tile = a.tile_order[ti];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
     const int lane = (int)(threadIdx.x & 63);
+    // quadrant group (quadrant (grp & 1, grp >> 1)) and index in it (see group_transpose_reduce32)
+    const int grp = quad_group(lane), li = lane >> 2;
     const uint2 range = a.ranges[tile];
     const size_t HW = (size_t)a.H * a.W;
-    const float px0 = (float)(tx * GSR_BLOCK_X + (lane & 7));
-    const float py0 = (float)(ty * GSR_BLOCK_Y + (lane >> 3));
-    const v2f pfx = {px0, px0 + 8.f};
+    // pixels p = 0..3 of this lane: row qy, columns qx0 + 2 (p >> 1) + 4 (p & 1); pair h = p >> 1
+    const uint32_t qx0 = tx * GSR_BLOCK_X + 8 * (grp & 1) + (li & 1);
+    const uint32_t qy = ty * GSR_BLOCK_Y + 8 * (grp >> 1) + (li >> 1);
+    const float fx0 = (float)qx0, pfy = (float)qy;
+    const v2f pfx0 = {fx0, fx0 + 4.f}, pfx1 = {fx0 + 2.f, fx0 + 6.f};
 
     // Pixel state: every load issued before the first use (clamped addresses, masked after), so
     // the prologue costs one memory round trip instead of one per pixel.
@@ -536,34 +544,31 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
     uint32_t lc[4];
     bool inside[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {  // q = 2 h + e: pixel (x + 8 e, y + 8 h)
-        const uint32_t px = tx * GSR_BLOCK_X + (lane & 7) + 8 * (q & 1);
-        const uint32_t py = ty * GSR_BLOCK_Y + (lane >> 3) + 8 * (q >> 1);
-        inside[q] = px < (uint32_t)a.W && py < (uint32_t)a.H;
-        const uint32_t pix_id = inside[q] ? (uint32_t)a.W * py + px : 0u;
-        Tf[q] = a.final_Ts[pix_id];
-        acc[q] = a.accum[pix_id];
-        lc[q] = a.n_contrib[pix_id];
-        dp0[q] = a.dL_dpixels[0 * HW + pix_id];
-        dp1[q] = a.dL_dpixels[1 * HW + pix_id];
-        dp2[q] = a.dL_dpixels[2 * HW + pix_id];
-        dinv[q] = HAS_INV ? a.dL_invdepths[pix_id] : 0.f;
+    for (int p = 0; p < 4; p++) {
+        const uint32_t px = qx0 + 2 * (p >> 1) + 4 * (p & 1);
+        inside[p] = px < (uint32_t)a.W && qy < (uint32_t)a.H;
+        const uint32_t pix_id = inside[p] ? (uint32_t)a.W * qy + px : 0u;
+        Tf[p] = a.final_Ts[pix_id];
+        acc[p] = a.accum[pix_id];
+        lc[p] = a.n_contrib[pix_id];
+        dp0[p] = a.dL_dpixels[0 * HW + pix_id];
+        dp1[p] = a.dL_dpixels[1 * HW + pix_id];
+        dp2[p] = a.dL_dpixels[2 * HW + pix_id];
+        dinv[p] = HAS_INV ? a.dL_invdepths[pix_id] : 0.f;
     }
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
-    uint32_t qmax[4];
     float R[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        if (!inside[q]) {
-            Tf[q] = 0.f;
-            acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-            lc[q] = 0u;
-            dp0[q] = dp1[q] = dp2[q] = dinv[q] = 0.f;
+    for (int p = 0; p < 4; p++) {
+        if (!inside[p]) {
+            Tf[p] = 0.f;
+            acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
+            lc[p] = 0u;
+            dp0[p] = dp1[p] = dp2[p] = dinv[p] = 0.f;
         }
-        R[q] = (acc[q].x + Tf[q] * bg0) * dp0[q] + (acc[q].y + Tf[q] * bg1) * dp1[q] +
-               (acc[q].z + Tf[q] * bg2) * dp2[q] + acc[q].w * dinv[q];
-        qmax[q] = __builtin_amdgcn_readfirstlane(wave_max_u32(lc[q]));
+        R[p] = (acc[p].x + Tf[p] * bg0) * dp0[p] + (acc[p].y + Tf[p] * bg1) * dp1[p] +
+               (acc[p].z + Tf[p] * bg2) * dp2[p] + acc[p].w * dinv[p];
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
@@ -578,12 +583,15 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
         s.lc0 = lc[2 * h];
         s.lc1 = lc[2 * h + 1];
     }
-    const uint32_t tmax = max(max(qmax[0], qmax[1]), max(qmax[2], qmax[3]));
+    const uint32_t tmax =
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u32(max(max(lc[0], lc[1]), max(lc[2], lc[3]))));
 
     __shared__ float4 s_recw[BWD_TPW][3][64];
-    __shared__ uint8_t s_listw[BWD_TPW][64];
+    __shared__ uint8_t s_lqw[BWD_TPW][4][64];
+    __shared__ float s_accw[BWD_TPW][GF_NUM][64];
     float4 (&s_rec)[3][64] = s_recw[wv];
-    uint8_t (&s_list)[64] = s_listw[wv];
+    uint8_t (&s_lq)[4][64] = s_lqw[wv];  // per quadrant: the batch entries it evaluates, in list order
+    float (&s_acc)[GF_NUM][64] = s_accw[wv];  // per batch entry: sums of its quadrant partials
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
@@ -615,51 +623,53 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;
         }
-        const uint64_t b = __ballot(m != 0);
-        const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0));
-        if (m != 0) s_list[before] = (uint8_t)lane;
-        const int cnt = __popcll(b);
+        const uint64_t any = __ballot(m != 0);
+        if (any == 0) continue;  // nothing staged, nothing to store
+        int cq[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bool in = (m >> q) & 1u;
+            const uint64_t bq = __ballot(in);
+            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0));
+            if (in) s_lq[q][before] = (uint8_t)lane;
+            cq[q] = __popcll(bq);
+        }
+#pragma unroll
+        for (int f = 0; f < GF_NUM; f++) s_acc[f][lane] = 0.f;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // Surviving entries in list order straight from the ballot (scalar bit scan); each
-        // record is read from LDS one entry ahead of its use.
-        uint64_t rem = b;
-        for (int g0 = 0; g0 < cnt; g0 += G) {
-            int js[G];
+        // Each quadrant group walks its own entries in list order (pixels of different quadrants
+        // share no state), iteration i of all four groups at once; a group past its count
+        // evaluates a staged record at position "never" (alpha = 0: state unchanged, zero terms).
+        const int fv = (int)__builtin_ctzll(any);
+        const int mycnt = grp == 0 ? cq[0] : grp == 1 ? cq[1] : grp == 2 ? cq[2] : cq[3];
+        const int niter = max(max(cq[0], cq[1]), max(cq[2], cq[3]));
+        for (int i0 = 0; i0 < niter; i0 += G) {
+            int ej[G];
+            bool act[G];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                js[jj] = rem ? (int)__builtin_ctzll(rem) : -1;
-                rem &= rem - 1;
+                act[jj] = i0 + jj < mycnt;
+                ej[jj] = act[jj] ? (int)s_lq[grp][i0 + jj] : fv;
             }
             float v[32];
-            float4 xy = s_rec[0][js[0]], co = s_rec[1][js[0]], col = s_rec[2][js[0]];
+            float4 xy = s_rec[0][ej[0]], co = s_rec[1][ej[0]], col = s_rec[2][ej[0]];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                if (js[jj] >= 0) {
-                    const int j = js[jj];
+                if (i0 + jj < niter) {  // wave-uniform
                     float4 nxy, nco, ncol;
                     if (jj + 1 < G) {
-                        const int nj = js[jj + 1] >= 0 ? js[jj + 1] : j;
-                        nxy = s_rec[0][nj];
-                        nco = s_rec[1][nj];
-                        ncol = s_rec[2][nj];
+                        nxy = s_rec[0][ej[jj + 1]];
+                        nco = s_rec[1][ej[jj + 1]];
+                        ncol = s_rec[2][ej[jj + 1]];
                     }
-                    const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)m, j);
-                    const uint32_t pos = (uint32_t)(p0 + j);
+                    const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
                     const Falloff f = falloff(co);
                     v2f o[GF_NUM];
-                    // both halves in one straight-line block (two independent dependency chains
-                    // for the scheduler to interleave), or the one the entry reaches
-                    if ((mj & 3u) && (mj & 12u)) {
-                        bwd_pair<HAS_INV, true>(st[0], pfx, py0, pos, xy, f, co, col, o);
-                        bwd_pair<HAS_INV, false>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
-                    } else if (mj & 3u) {
-                        bwd_pair<HAS_INV, true>(st[0], pfx, py0, pos, xy, f, co, col, o);
-                    } else {
-                        bwd_pair<HAS_INV, true>(st[1], pfx, py0 + 8.f, pos, xy, f, co, col, o);
-                    }
+                    bwd_pair<HAS_INV, true>(st[0], pfx0, pfy, pos, xy, f, co, col, o);
+                    bwd_pair<HAS_INV, false>(st[1], pfx1, pfy, pos, xy, f, co, col, o);
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
                     if (jj + 1 < G) {
@@ -674,17 +684,40 @@ __global__ void __launch_bounds__(64 * BWD_TPW) render_bwd_kernel(const ViewBatc
             }
 #pragma unroll
             for (int q = G * GF_NUM; q < 32; q++) v[q] = 0.f;
-            const float r = wave_transpose_reduce32(v, lane);
-            const int k = lane >> 1;  // value held by this lane (lanes 2k, 2k + 1)
-            const int jj = k / GF_NUM;
-            const int jl = s_list[min(g0 + jj, 63)];
-            const uint32_t dst = (uint32_t)__shfl((int)myslot, jl, 64);  // record slot of entry jl
-            if ((lane & 1) == 0 && k < G * GF_NUM && g0 + jj < cnt) {
-                a.grad_inst[(size_t)dst * GRAD_REC + (k - jj * GF_NUM)] = r;
-                if (k == jj * GF_NUM) atomicOr(&a.valid[dst >> 5], 1u << (dst & 31u));
+            float r0, r1;
+            group_transpose_reduce32(v, lane, r0, r1);
+            // lane li of a group holds the group totals of values 2 li and 2 li + 1 (value
+            // jj * GF_NUM + f = term f of the group's entry jj); the four groups add their
+            // partials into the entries' sums one after the other (fixed order: reproducible)
+            const int k0 = 2 * li, k1 = k0 + 1;
+            const int j0 = k0 / GF_NUM, j1 = k1 / GF_NUM;
+            const bool ok0 = k0 < G * GF_NUM && (j0 == 0 ? act[0] : j0 == 1 ? act[1] : act[2]);
+            const bool ok1 = k1 < G * GF_NUM && (j1 == 0 ? act[0] : j1 == 1 ? act[1] : act[2]);
+            const int e0 = j0 == 0 ? ej[0] : j0 == 1 ? ej[1] : ej[2];
+            const int e1 = j1 == 0 ? ej[0] : j1 == 1 ? ej[1] : ej[2];
+            float* a0 = &s_acc[min(k0 - j0 * GF_NUM, GF_NUM - 1)][e0];
+            float* a1 = &s_acc[min(k1 - j1 * GF_NUM, GF_NUM - 1)][e1];
+#pragma unroll
+            for (int gg = 0; gg < 4; gg++) {
+                if (grp == gg) {
+                    if (ok0) __hip_atomic_fetch_add(a0, r0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    if (ok1) __hip_atomic_fetch_add(a1, r1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
-        __builtin_amdgcn_wave_barrier();  // s_rec / s_list reuse in the next batch
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // one 48-B record per contributing entry, stored by its own lane
+        if (m != 0) {
+            float* rec = a.grad_inst + (size_t)myslot * GRAD_REC;
+            reinterpret_cast<float4*>(rec)[0] = make_float4(s_acc[0][lane], s_acc[1][lane], s_acc[2][lane], s_acc[3][lane]);
+            reinterpret_cast<float4*>(rec)[1] = make_float4(s_acc[4][lane], s_acc[5][lane], s_acc[6][lane], s_acc[7][lane]);
+            reinterpret_cast<float2*>(rec)[4] = make_float2(s_acc[8][lane], s_acc[9][lane]);
+            atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
+        }
+        __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
     }
 }
 
