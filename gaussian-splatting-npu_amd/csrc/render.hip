@@ -288,8 +288,11 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
         s_rec[2 * BATCH + tid] = r2;
         const uint32_t m = k < todo ? quad_mask(r0, r1, tx, ty) : 0u;
         s_mask[tid] = (uint8_t)m;
-        if (tid < 4 * (BATCH / 64)) (&s_hitw[0][0])[tid] = 0ull;
         __syncthreads();
+        // each wave clears its own round words after the barrier: every wave has flushed the
+        // previous batch's bits (above, before the barrier), and the wave's own stores below
+        // follow in program order
+        if (lane < BATCH / 64) s_hitw[wid][lane] = 0ull;
         const int n = min(BATCH, todo - base);
         // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
         // per 64 entries, then a scalar bit scan; each record is read one entry ahead of use.
