@@ -740,10 +740,11 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         pa[v].rgb = nullptr;
     }
     // The binning prefix of all V views, batched: every stage is one launch over all views
-    // (grid.y = view), on one high-priority prefix stream; the renders follow on the caller's.
-    hipStream_t ps = nullptr;
-    int rc = prefix_begin(caller, &ps);
-    if (rc) return rc;
+    // (grid.y = view), on the caller's stream like the renders that follow (a separate prefix
+    // stream would overlap nothing here -- it would fork from the caller's previous work and the
+    // render would join it -- and each hop between the queues costs ~10 us of idle GPU).
+    hipStream_t ps = caller;
+    int rc = GSR_OK;
     {
         ProfScope ps_(PK_PREPROCESS, ps);
         HIP_TRY(launch_preprocess_views(pa, V, ps));  // the parameters and SH rows read once per 8 views
