@@ -198,6 +198,7 @@ struct Prof {
     bool on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool[PK_COUNT];
     size_t used[PK_COUNT] = {};
+    size_t parts[PK_COUNT] = {};  // scopes that continue the kernel's previous one (not a new launch)
 };
 Prof g_prof;
 
@@ -215,17 +216,20 @@ hipEvent_t prof_begin(int k, hipStream_t s)
     return e;
 }
 
-void prof_end(int k, hipStream_t s, hipEvent_t begun)
+void prof_end(int k, hipStream_t s, hipEvent_t begun, bool part)
 {
     if (!g_prof.on || !begun) return;
     (void)hipEventRecord(g_prof.pool[k][g_prof.used[k]].second, s);
     g_prof.used[k]++;
+    if (part) g_prof.parts[k]++;
 }
 
+// part: the scope times the rest of a kernel stage whose first part had a scope of its own (its time
+// adds to the stage's total, not to its launch count)
 struct ProfScope {
-    int k; hipStream_t s; hipEvent_t e;
-    ProfScope(int k_, hipStream_t s_) : k(k_), s(s_), e(prof_begin(k_, s_)) {}
-    ~ProfScope() { prof_end(k, s, e); }
+    int k; hipStream_t s; hipEvent_t e; bool part;
+    ProfScope(int k_, hipStream_t s_, bool part_ = false) : k(k_), s(s_), e(prof_begin(k_, s_)), part(part_) {}
+    ~ProfScope() { prof_end(k, s, e, part); }
 };
 
 template <typename T>
@@ -270,8 +274,9 @@ int gsr_profile_read(double* total_ms, int* counts, int n)
             acc += ms;
         }
         total_ms[k] = acc;
-        counts[k] = (int)g_prof.used[k];
+        counts[k] = (int)(g_prof.used[k] - g_prof.parts[k]);
         g_prof.used[k] = 0;
+        g_prof.parts[k] = 0;
     }
     return PK_COUNT;
 }
@@ -515,8 +520,7 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     const ImageLayout im = image_layout(width, height);
     const BinLayout b = bin_layout(L);
     const size_t q = align_up(4 * (size_t)L, 256);
-    char* w = bb + b.off[BIN_GRAD_INST];
-    TileSortJob j;
+    TileSortJob j = {};
     j.P = P;
     j.L = L;
     j.sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
@@ -524,6 +528,9 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     j.sorted_rects = at<uint2>(gb, g.off[GEOM_SORTED_RECT]);
     j.rec_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     j.pass1_scratch = gb + g.off[GEOM_DSORT_TMP];
+    j.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    if (!bb) return j;  // the histogram phase only (FUSED_COUNT): no binning buffer yet
+    char* w = bb + b.off[BIN_GRAD_INST];
     j.k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
     j.k1 = reinterpret_cast<uint32_t*>(w + 3 * q);
     j.v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
@@ -533,7 +540,6 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     j.out_ids = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
     j.out_tiles = at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
     j.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
-    j.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     return j;
 }
 
@@ -783,6 +789,14 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         ProfScope ps_(PK_SCAN, ps);
         HIP_TRY(launch_scan_batch(off, V, false, ps));
     }
+    {
+        // the first tile-sort pass's histograms need only the depth-ordered rects and offsets: the
+        // GPU computes them while the host waits for L below
+        TileSortJob cj[MAX_VIEWS];
+        for (int v = 0; v < V; v++) cj[v] = fused_tile_sort_job(geometry_buffers[v], nullptr, image_buffers[v], P, 0, width, height);
+        ProfScope ps_(PK_TILE_SORT, ps);
+        HIP_TRY(tile_sort_fused_batch(cj, V, gx, T, ps, FUSED_COUNT));
+    }
     DEBUG_SYNC(ps);
     // the one host hand-off: every view's num_rendered (rasterizer_impl.cu:283-284)
     int L[MAX_VIEWS];
@@ -815,8 +829,8 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         fit[nf++] = v;
     }
     if (ns) {
-        ProfScope ps_(PK_TILE_SORT, ps);
-        HIP_TRY(tile_sort_fused_batch(tsort, ns, gx, T, ps));
+        ProfScope ps_(PK_TILE_SORT, ps, true);
+        HIP_TRY(tile_sort_fused_batch(tsort, ns, gx, T, ps, FUSED_SCATTER));
     }
     if (nf) {
         {

@@ -245,7 +245,11 @@ struct TileSortJob {
     uint2* ranges;                // IMG_RANGES, cleared
 };
 size_t fused_pass1_scratch_bytes(int P);
-hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s);
+// phases: FUSED_COUNT = the first pass's histogram and row scan (needs neither L nor the binning
+// buffer: the batched forward runs it while the host reads L back), FUSED_SCATTER = the rest
+enum FusedPhase { FUSED_COUNT = 1, FUSED_SCATTER = 2, FUSED_ALL = 3 };
+hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s,
+                                 int phases = FUSED_ALL);
 
 struct RangesJob {
     int L;

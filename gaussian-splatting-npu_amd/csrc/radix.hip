@@ -446,8 +446,6 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_count_kernel(const Vie
             const uint32_t x0 = rc.x & 0xFFFFu, y0 = rc.x >> 16, x1 = rc.y & 0xFFFFu, y1 = rc.y >> 16;
             for (uint32_t y = y0; y < y1; y++)
                 for (uint32_t x = x0; x < x1; x++) atomicAdd(&h[w][(y * gx + x) & mask], 1u);
-            // the backward flags the records it writes: clear the bit words starting in [start, end)
-            for (uint32_t sl = (start + 31u) & ~31u; sl < end; sl += 32u) J.valid[sl >> 5] = 0u;
         }
     }
     __syncthreads();
@@ -484,6 +482,10 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     // this thread's staged rank: start and end of its instances
     const uint32_t my_start = s.start[tid];
     const uint32_t my_end = min(tid + 1 < FE_RANKS ? s.start[tid + 1] : wend, wend);
+    // the backward flags the records it writes: clear the bit words starting in this rank's
+    // instances (here, not in the count kernel, which runs before L and the binning buffer exist)
+    if (my_end > my_start)
+        for (uint32_t sl = (my_start + 31u) & ~31u; sl < my_end; sl += 32u) J.valid[sl >> 5] = 0u;
     for (uint32_t r0 = wbeg; r0 < wend; r0 += TILE) {
         const int nvalid = (int)min((uint32_t)TILE, wend - r0);
         // owners of the round's positions without a search per instance: every rank starting inside
@@ -754,7 +756,7 @@ size_t fused_pass1_scratch_bytes(int P)
     return align_up(chunks * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
 }
 
-hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s)
+hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, int T, hipStream_t s, int phases)
 {
     const int nbits = max((int)higher_msb((uint32_t)T), 1);
     const int npass = (nbits + 7) / 8;
@@ -793,11 +795,14 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
         }
         if (maxc == 0) return hipSuccess;
         const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
-        hipLaunchKernelGGL(fused_pass1_count_kernel, g, b, 0, s, fb, gx, T, w1);
-        if (maxc <= RS_ROW_LDS)
-            hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
-        else
-            hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+        if (phases & FUSED_COUNT) {
+            hipLaunchKernelGGL(fused_pass1_count_kernel, g, b, 0, s, fb, gx, T, w1);
+            if (maxc <= RS_ROW_LDS)
+                hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+            else
+                hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+        }
+        if (!(phases & FUSED_SCATTER)) return hipGetLastError();
         hipLaunchKernelGGL(fused_pass1_scatter_kernel<RS_ITEMS>, g, b, 0, s, fb, gx, w1);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || npass == 1) return e;
