@@ -658,16 +658,10 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                 ej[jj] = act[jj] ? (int)s_lq[grp][i0 + jj] : fv;
             }
             float v[32];
-            float4 xy = s_rec[0][ej[0]], co = s_rec[1][ej[0]], col = s_rec[2][ej[0]];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 if (i0 + jj < niter) {  // wave-uniform
-                    float4 nxy, nco, ncol;
-                    if (jj + 1 < G) {
-                        nxy = s_rec[0][ej[jj + 1]];
-                        nco = s_rec[1][ej[jj + 1]];
-                        ncol = s_rec[2][ej[jj + 1]];
-                    }
+                    const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
                     const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
                     const Falloff f = falloff(co);
                     v2f o[GF_NUM];
@@ -675,11 +669,6 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                     bwd_pair<HAS_INV, false>(st[1], pfx1, pfy, pos, xy, f, co, col, o);
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
-                    if (jj + 1 < G) {
-                        xy = nxy;
-                        co = nco;
-                        col = ncol;
-                    }
                 } else {
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = 0.f;
