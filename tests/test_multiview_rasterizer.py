@@ -279,3 +279,26 @@ def test_multiview_large_batch_big_splats_empty_view(H_, W_):
         ok, rel = common.allclose_rel(multi[k].grad.cpu().numpy(), single[k].grad.cpu().numpy(), rtol=1e-5,
                                       atol=1e-9)
         assert ok, f"d{k} multi vs sum of single views rel {rel:.3e}"
+
+
+def test_backward_bitwise_reproducible():
+    """render_bwd sums an entry's quadrant partials in LDS in a fixed group order (no global float
+    atomics): repeated backwards of the same batch give bitwise-identical gradients."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    settings = [_settings(c, True, bg) for c in case["cams"]]
+    gc = torch.stack([g[0] for g in case["grads"]]).to(DEV)
+    gi = torch.stack([g[1] for g in case["grads"]]).to(DEV)
+    runs = []
+    for _ in range(3):
+        t = _leaves(case, "sh_scales")
+        means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+        c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **t)
+        torch.autograd.backward([c, i], [gc, gi])
+        torch.cuda.synchronize()
+        runs.append({"means2D": means2D.grad.clone(), **{k: v.grad.clone() for k, v in t.items()}})
+    assert any(float(runs[0][k].abs().max()) > 0 for k in runs[0])
+    for r in runs[1:]:
+        for k in runs[0]:
+            assert torch.equal(r[k], runs[0][k]), f"d{k} differs between identical backwards"
