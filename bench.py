@@ -84,7 +84,11 @@ def parse():
                          "before this view's backward, or every forward before every backward")
     ap.add_argument("--no-fused-accumulation", action="store_true",
                     help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
+    ap.add_argument("--no-single-view", action="store_true",
+                    help="skip the config2_single_view leg (plain GaussianRasterizer fwd+bwd of view 0, own roofline)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
+    # the pmc child of rank 0 of an N-rank run (started before the process group): rank 0's views
+    ap.add_argument("--pmc-world", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -122,14 +126,25 @@ def lib_sha256():
     return h.hexdigest()
 
 
-def pmc_traffic(args, timeout=240):
-    """HBM traffic and VALU wave-instructions per launch of every rasterizer kernel, measured now
-    on this build: three rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE -- together they exceed
-    the 4 TCC counters of one pass -- and SQ_INSTS_VALU) over this script's own workload
-    (`--pmc-child`: the same views, 1 warm-up + 1 step), each a child process under a time limit;
-    bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per MI355X_MICROARCH.md §HBM, per launch
-    (tools/pmc_summary.py).  Returns (traffic, valu) dicts, or None if rocprofv3 is absent or a
-    pass fails."""
+PMC_CHILD_STEPS = 2  # the --pmc-child workload: 1 warm-up + 1 step
+
+
+def workload_stamp(args, world, views_rank):
+    """What a PMC figure was measured on: traffic per launch belongs to exactly this workload."""
+    return {"P": args.P, "width": args.width, "height": args.height, "views_per_rank": views_rank,
+            "world": world, "mode": "batch" if args.batch_views else ("per-view deferred" if args.deferred
+                                                                     else "per-view"),
+            "antialiasing": bool(args.antialiasing)}
+
+
+def pmc_traffic(args, world, timeout=240):
+    """HBM traffic and VALU wave-instructions of every rasterizer operation, measured now on this
+    build: three rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE -- together they exceed the 4 TCC
+    counters of one pass -- and SQ_INSTS_VALU) over this script's own workload (`--pmc-child`:
+    this rank's views, PMC_CHILD_STEPS steps, nothing else), each a child process under a time
+    limit; bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per MI355X_MICROARCH.md §HBM.  Returns the
+    pmc_summary totals over all dispatches of each operation (the caller divides by the number of
+    calls), or None if rocprofv3 is absent or a pass fails."""
     exe = shutil.which("rocprofv3")
     if not exe:
         return None
@@ -138,10 +153,16 @@ def pmc_traffic(args, timeout=240):
     tmp = tempfile.mkdtemp(prefix="gsr_pmc_")
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "1", "--warmup", "1",
              "--P", str(args.P), "--width", str(args.width), "--height", str(args.height),
-             "--views-total", str(args.views_total), "--views-per-rank", str(args.views_per_rank)]
-    if args.antialiasing:
-        child.append("--antialiasing")
-    env = dict(os.environ, TMPDIR=tmp)
+             "--views-total", str(args.views_total), "--views-per-rank", str(args.views_per_rank),
+             "--pmc-world", str(world)]
+    for flag, on in (("--antialiasing", args.antialiasing), ("--per-view", not args.batch_views),
+                     ("--no-deferred", not args.deferred), ("--no-overlap", not args.overlap)):
+        if on:
+            child.append(flag)
+    # a clean environment for the child: no rank variables (it is one process, not a rank)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK")}
+    env["TMPDIR"] = tmp
     try:
         for counter in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
             r = subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", os.path.join(tmp, counter),
@@ -155,12 +176,32 @@ def pmc_traffic(args, timeout=240):
                 pmc_summary.main(tmp)
             finally:
                 sys.stdout = old
-        return (json.load(open(os.path.join(tmp, "pmc_traffic.json")))["bytes_per_launch"],
-                json.load(open(os.path.join(tmp, "pmc_valu.json")))["winst_per_launch"])
+        t = json.load(open(os.path.join(tmp, "pmc_traffic.json")))
+        v = json.load(open(os.path.join(tmp, "pmc_valu.json")))
+        return {"bytes_total": t["bytes_total"], "winst_total": v["winst_total"]}
     except Exception:
         return None
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def single_view_leg(args, timeout=400):
+    """config2_single_view: the plain single-view step train.py runs -- one GaussianRasterizer
+    forward + full backward of view 0 per step (bench.py --views-total 1 --per-view --no-deferred),
+    its own per-kernel times, roofline and PMC traffic, in a child process."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--views-total", "1", "--per-view", "--no-deferred",
+           "--no-aux", "--no-cpu-baseline", "--no-single-view", "--steps", str(max(args.steps, 20)),
+           "--warmup", str(args.warmup), "--P", str(args.P), "--width", str(args.width),
+           "--height", str(args.height)] + (["--antialiasing"] if args.antialiasing else []) \
+        + (["--no-pmc"] if args.no_pmc else []) + (["--no-profile"] if args.no_profile else [])
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, timeout=timeout, capture_output=True, text=True)
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+        d = json.loads(line)
+        return {k: d[k] for k in ("value", "unit", "ms_per_step", "ms_per_step_median", "roofline")} | {
+            "workload": d["config"]["workload"], "execution": d["config"]["execution"]}
+    except Exception as e:
+        return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
 
 def main():
@@ -168,6 +209,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.pmc_child:  # one process replaying rank 0's share of a `--pmc-world`-rank step
+        world, rank, local_rank = 1, 0, 0
+    views_world = args.pmc_world if (args.pmc_child and args.pmc_world > 0) else world
+    # PMC passes of this rank's workload, on rank 0 only, before the process group exists and before
+    # this process touches the GPU (the child replays rank 0's views of the N-rank step)
+    pmc = None
+    if rank == 0 and not args.pmc_child and not args.no_pmc and not args.no_profile:
+        pmc = pmc_traffic(args, world)
     # GSR_DIST_BACKEND=gloo (rehearsal only): several ranks on one GPU exercise the N>1 path of
     # this script on a one-GPU box; the driver's multi-GPU runs use the default, RCCL ("nccl").
     backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
@@ -195,12 +244,12 @@ def main():
     M = params["shs"].shape[1]
     if args.views_per_rank > 0:  # weak scaling: K views per rank, distinct cameras over all ranks
         mode, scaling = "weak", "weak"
-        n_ring = max(N_RING, args.views_per_rank * world)
-        views = multiview.views_for_rank(rank, world, args.views_per_rank, n_views=n_ring)
+        n_ring = max(N_RING, args.views_per_rank * views_world)
+        views = multiview.views_for_rank(rank, views_world, args.views_per_rank, n_views=n_ring)
     else:  # strong scaling: a fixed batch of views per step, dealt round-robin
         mode, scaling = "strong", "strong"
         n_ring = max(N_RING, args.views_total)
-        views = multiview.views_of_batch(rank, world, args.views_total)
+        views = multiview.views_of_batch(rank, views_world, args.views_total)
     views_step = world * len(views) if mode == "weak" else args.views_total
     cams, grads = [], []
     for v in views:
@@ -305,14 +354,20 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    # step boundaries on the main stream (for the per-step median; recording costs nothing measurable)
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    marks[0].record()
+    for i in range(args.steps):
         step()
+        marks[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = multiview.max_over_ranks(t1 - t0, dev)
+    step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(args.steps)]
+    median_ms = multiview.max_over_ranks(statistics.median(step_ms) / 1e3, dev) * 1e3
 
     # per-kernel HIP-event timings: a second, instrumented run of the same steps (the events
     # recorded around every launch cost ~3% of the step, so they stay out of the timed region)
@@ -385,50 +440,52 @@ def main():
         dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
         sha = lib_sha256()
-        traffic, traffic_src, traffic_all = None, None, None
-        measured = None if (args.no_pmc or world > 1) else pmc_traffic(args)
-        valu_measured = measured[1] if measured else None
-        measured = measured[0] if measured else None
-        if measured and dom in measured:
-            traffic, traffic_src, traffic_all = measured[dom], "rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (this run)", \
-                measured
-        else:  # the committed figures, only if they were measured on this very library build
-            tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            try:
-                stamped = json.load(open(tf))
-                if stamped.get("lib_sha256") == sha:
-                    traffic, traffic_src = stamped["bytes_per_launch"].get(dom), "profiles/pmc_traffic.json (same build)"
-                    traffic_all = stamped["bytes_per_launch"]
-                else:
-                    traffic_src = "stale: profiles/pmc_traffic.json was measured on another build"
-            except Exception:
-                traffic_src = "unavailable"
+        stamp = workload_stamp(args, world, len(cams))
+        # calls of each operation during the PMC child's steps: launches per step (instrumented pass)
+        # x PMC_CHILD_STEPS; traffic per launch = the op's bytes over all its dispatches / its calls
+        calls = {k: v["launches"] / args.steps * PMC_CHILD_STEPS for k, v in kern.items()}
+        traffic_all, valu_all, traffic_src, vsrc = None, None, None, None
+        if pmc:
+            traffic_all = {k: round(v / calls[k]) for k, v in pmc["bytes_total"].items() if calls.get(k)}
+            valu_all = {k: round(v / calls[k]) for k, v in pmc["winst_total"].items() if calls.get(k)}
+            traffic_src = "rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE (this run, this workload)"
+            vsrc = "rocprofv3 --pmc SQ_INSTS_VALU (this run, this workload)"
+            # the stamped figures, for profiles/ (bench.py accepts them only for this build + workload)
+            os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+            tag = "single" if (not args.batch_views and not args.deferred and len(cams) == 1) else "step"
+            json.dump({"lib_sha256": sha, "workload": stamp, "bytes_per_launch": traffic_all,
+                       "winst_per_launch": valu_all, "source": "bench.py --pmc-child passes"},
+                      open(os.path.join(ROOT, "gpurun_out", f"pmc_{tag}.json"), "w"), indent=1)
+        else:  # committed figures, only if measured on this very library build AND this workload
+            for name in ("pmc_step.json", "pmc_single.json"):
+                try:
+                    st = json.load(open(os.path.join(ROOT, "profiles", name)))
+                except Exception:
+                    continue
+                if st.get("lib_sha256") == sha and st.get("workload") == stamp:
+                    traffic_all, valu_all = st["bytes_per_launch"], st["winst_per_launch"]
+                    traffic_src = vsrc = f"profiles/{name} (same build, same workload)"
+                    break
+            if traffic_all is None:
+                traffic_src = "not measured: no PMC pass in this run and no stamped file for this build + workload"
+        traffic = (traffic_all or {}).get(dom)
         valu = None  # secondary roofline: render kernels are VALU-issue bound, not HBM bound
-        vi, vsrc = valu_measured, "rocprofv3 --pmc SQ_INSTS_VALU (this run)"
-        if not vi:
-            try:
-                st = json.load(open(os.path.join(ROOT, "profiles", "pmc_valu.json")))
-                if st.get("lib_sha256") == sha:
-                    vi, vsrc = st["winst_per_launch"], "profiles/pmc_valu.json (SQ_INSTS_VALU, same build)"
-            except Exception:
-                vi = None
-        if vi:
-            valu = {k: {"winst_per_launch": vi[k],
-                        "achieved_Ginst_s": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
-                        "frac": round(vi[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
-                    for k in kern if k in vi}
+        if valu_all:
+            valu = {k: {"winst_per_launch": valu_all[k],
+                        "achieved_Ginst_s": round(valu_all[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9, 1),
+                        "frac": round(valu_all[k] / (kern[k]["avg_ms"] * 1e-3) / 1e9 / VALU_PEAK_GINST, 3)}
+                    for k in kern if k in valu_all}
             valu = {"peak_Ginst_s": VALU_PEAK_GINST, "source": vsrc, "kernels": valu}
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "traffic_source": traffic_src, "traffic_stale": traffic is None and traffic_src is not None
-                    and traffic_src.startswith("stale"), "lib_sha256": sha[:16],
+                    "traffic_source": traffic_src, "lib_sha256": sha[:16], "workload_stamp": stamp,
                     "algorithmic_bytes": ab[dom],
                     "kernels": {k: {"avg_ms": round(v["avg_ms"], 4), "launches": v["launches"],
                                     "GBps": round(ab[k] / (v["avg_ms"] * 1e-3) / 1e9, 1),
-                                    "algorithmic_bytes": ab[k], "traffic": (traffic_all or {}).get(k)}
+                                    "algorithmic_bytes": ab[k], "traffic": (traffic_all or {}).get(k),
+                                    "traffic_over_algorithmic": round((traffic_all or {})[k] / ab[k], 3)
+                                    if (traffic_all or {}).get(k) and ab.get(k) else None}
                                 for k, v in kern.items()},
-                    # the depth and tile sorts share their kernels: their traffic is reported together
-                    "radix_sorts_traffic": (traffic_all or {}).get("radix_sorts"),
                     "valu": valu}
 
     cpu = None
@@ -457,6 +514,8 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        # median of the steps' stream times (events at the step boundaries, max over ranks)
+        "ms_per_step_median": round(median_ms, 4),
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,
@@ -478,6 +537,8 @@ def main():
         "aux": aux,
         "allreduce": allreduce,
     }
+    if world == 1 and not args.pmc_child and not args.no_single_view and (args.batch_views or len(cams) > 1):
+        res["config2_single_view"] = single_view_leg(args)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

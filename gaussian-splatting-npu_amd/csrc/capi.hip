@@ -395,13 +395,15 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
         // prefix streams scan inline instead of coupling their streams through it)
         int rc = use_aux ? aux_fork(s, &aux) : GSR_OK;
         if (rc) return rc;
-        HIP_TRY(launch_inclusive_scan(a.tiles_touched, nullptr, at<uint32_t>(gb, g.off[GEOM_EMIT_START]), P,
-                                      a.scan_status + scan_status_words(P), nullptr, aux, true));
     }
+    // every exit after the fork joins the auxiliary stream back first (the caller's stream stays
+    // ordered after the scan queued there, which writes into the caller's geometry buffer)
+    hipError_t e = launch_inclusive_scan(a.tiles_touched, nullptr, at<uint32_t>(gb, g.off[GEOM_EMIT_START]), P,
+                                         a.scan_status + scan_status_words(P), nullptr, aux, true);
 
     // 2. stable depth sort of the Gaussians (first half of the reference's tile|depth key sort)
     uint32_t* sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
-    {
+    if (e == hipSuccess) {
         char* tmp = gb + g.off[GEOM_DSORT_TMP];
         const size_t q = align_up(4 * (size_t)P, 256);
         uint32_t* k0 = reinterpret_cast<uint32_t*>(tmp);
@@ -411,20 +413,21 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
         ProfScope ps_(PK_DEPTH_SORT, s);
         // the last pass also lays the tile rects and tile counts out in depth order (the counts
         // into point_offsets, which the scan then turns into offsets in place)
-        HIP_TRY(radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
-                           gb + g.off[GEOM_RADIX_SCRATCH], s, a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
-                           at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])));
+        e = radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
+                       gb + g.off[GEOM_RADIX_SCRATCH], s, a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
+                       at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]));
     }
-    DEBUG_SYNC(s);
+    if (debug && e == hipSuccess) e = hipStreamSynchronize(s);
 
     // 3. instance offsets in depth order (cub::DeviceScan::InclusiveSum, rasterizer_impl.cu:280)
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
-    {
+    if (e == hipSuccess) {
         ProfScope ps_(PK_SCAN, s);
-        HIP_TRY(launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s));
+        e = launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s);
     }
     {
         const int rc = aux_join(s, aux);
+        if (e != hipSuccess) return fail_hip(e, __LINE__);
         if (rc) return rc;
     }
     DEBUG_SYNC(s);
@@ -778,12 +781,17 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     hipStream_t aux = ps;
     rc = aux_fork(ps, &aux);
     if (rc) return rc;
-    HIP_TRY(launch_scan_batch(rec, V, true, aux));
     {
-        ProfScope ps_(PK_DEPTH_SORT, ps);
-        HIP_TRY(radix_sort_batch(dsort, V, DEPTH_BITS, ps));
+        // every exit after the fork joins the auxiliary stream back first: the caller's stream
+        // must stay ordered after what is already queued there (it writes the caller's buffers)
+        hipError_t e = launch_scan_batch(rec, V, true, aux);
+        if (e == hipSuccess) {
+            ProfScope ps_(PK_DEPTH_SORT, ps);
+            e = radix_sort_batch(dsort, V, DEPTH_BITS, ps);
+        }
+        rc = aux_join(ps, aux);
+        if (e != hipSuccess) return fail_hip(e, __LINE__);
     }
-    rc = aux_join(ps, aux);
     if (rc) return rc;
     {
         ProfScope ps_(PK_SCAN, ps);
@@ -1318,7 +1326,7 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
         const uint32_t* point_list = at<uint32_t>(binning_buffer, b.off[BIN_POINT_LIST]);
         if (keys_out)
             HIP_TRY(launch_debug_keys(num_rendered, at<uint32_t>(binning_buffer, b.off[BIN_SORTED_TILES]), point_list,
-                                      at<float>(geometry_buffer, g.off[GEOM_DEPTH]), keys_out, s));
+                                      at<uint32_t>(geometry_buffer, g.off[GEOM_DKEY]), keys_out, s));
         if (vals_out)
             HIP_TRY(hipMemcpyAsync(vals_out, point_list, 4 * (size_t)num_rendered, hipMemcpyDeviceToDevice, s));
     }

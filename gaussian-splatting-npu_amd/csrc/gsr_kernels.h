@@ -222,9 +222,12 @@ struct SortJob {  // radix_sort's arguments for one view
     uint2* sorted_rects;
     uint32_t* sorted_counts;
 };
+// which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
+enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };
 // V independent stable sorts over the same bit width (key bits [shift0, shift0 + nbits)), pass by
 // pass in shared launches.
-hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0 = 0);
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0 = 0,
+                            SortKind kind = SORT_DEPTH);
 
 // Emission fused into the tile sort (gsr_forward_views): the instances are generated from the
 // depth-ordered rects inside the first radix pass's count and scatter kernels instead of being
@@ -270,10 +273,10 @@ hipError_t launch_tile_order_batch(const OrderJob* jobs, int V, int T, hipStream
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
                       char* scratch, hipStream_t s, const uint2* rects = nullptr, uint2* sorted_rects = nullptr,
-                      uint32_t* sorted_counts = nullptr);
+                      uint32_t* sorted_counts = nullptr, SortKind kind = SORT_DEPTH);
 // ranges must be zero on entry unless L == 0 (the fused tile sort's first pass clears them)
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
-hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
+hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const uint32_t* dkeys,
                              uint64_t* keys, hipStream_t s);
 
 // Longest-first launch order of the T tiles: order[] = tiles by decreasing work, work = range length

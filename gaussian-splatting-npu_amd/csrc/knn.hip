@@ -281,7 +281,7 @@ hipError_t knn_dist2(int P, const float* pts, float* dist2, char* ws, uint32_t* 
     hipLaunchKernelGGL(knn_cell_kernel, grid, blk, 0, s, P, pts, g, at32(0));
     const int nbits = (int)higher_msb(ncells);  // as the reference sizes its tile sort
     if ((e = radix_sort(P, nbits, at32(0), nullptr, at32(1), at32(2), at32(3), at32(4), at32(5), nullptr, at32(6),
-                        ws + l.off[9], s)) != hipSuccess)
+                        ws + l.off[9], s, nullptr, nullptr, nullptr, SORT_CELLS)) != hipSuccess)
         return e;
     uint2* cell_range = reinterpret_cast<uint2*>(ws + l.off[8]);
     if ((e = hipMemsetAsync(cell_range, 0, 8 * (size_t)ncells, s)) != hipSuccess) return e;

@@ -35,6 +35,13 @@ constexpr int RS_ITEMS_SHORT = 8;               // short sorts (the depth sort; 
 constexpr int RS_SHORT_MAX = 1 << 21;           // n up to which a sort counts as short
 constexpr int RS_MAXBINS = 256;
 
+// Kernel-name tags: which sort a radix pass belongs to (the depth sort, the tile sort's later
+// passes, distCUDA2's cell sort) -- the kernels are identical, the names let a profile (rocprofv3
+// --pmc, tools/pmc_summary.py) attribute every dispatch to its sort.
+struct DepthSort;
+struct TileSort;
+struct CellSort;
+
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
 // (1) counts[d * nchunks + c] = number of elements of chunk c with digit d (view blockIdx.y).
@@ -43,7 +50,7 @@ struct CountJob {
     int n, nchunks;
     uint32_t* counts;
 };
-template <int ITEMS>
+template <int ITEMS, typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
     const CountJob& J = B.v[blockIdx.y];
@@ -97,6 +104,7 @@ struct RowJob {
     int nchunks;
     uint32_t* totals;
 };
+template <typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBatch<RowJob> B)
 {
     uint32_t* counts = B.v[blockIdx.y].counts;
@@ -134,6 +142,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBat
 // serially, and one block-wide scan of the segment sums joins them -- one global round trip and
 // two barriers instead of three barriers per 256 chunks.
 constexpr int RS_ROW_LDS = 12288;
+template <typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const ViewBatch<RowJob> RB)
 {
     uint32_t* counts = RB.v[blockIdx.y].counts;
@@ -220,7 +229,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
 }
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
-template <int ITEMS, bool PAIR>
+template <int ITEMS, bool PAIR, typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
@@ -638,12 +647,15 @@ __global__ void __launch_bounds__(256) tile_ranges_kernel(const ViewBatch<Ranges
     }
 }
 
+// the reference's 64-bit keys (tile << 32 | depth bits, rasterizer_impl.cu:98-106) of the sorted
+// instances, from the depth-sort keys (the depth bits of every listed Gaussian: preprocess writes
+// them in single-view and batched forwards alike)
 __global__ void __launch_bounds__(256) debug_keys_kernel(int L, const uint32_t* sorted_tiles, const uint32_t* point_list,
-                                                         const float* depths, uint64_t* keys)
+                                                         const uint32_t* dkeys, uint64_t* keys)
 {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= L) return;
-    keys[idx] = ((uint64_t)sorted_tiles[idx] << 32) | __float_as_uint(depths[point_list[idx]]);
+    keys[idx] = ((uint64_t)sorted_tiles[idx] << 32) | dkeys[point_list[idx]];
 }
 
 static inline int rs_items(int n) { return n <= RS_SHORT_MAX ? RS_ITEMS_SHORT : RS_ITEMS; }
@@ -685,7 +697,8 @@ static inline uint32_t* sort_totals(const SortJob& j)
     return reinterpret_cast<uint32_t*>(j.scratch + align_up(rs_chunks(j.n) * RS_MAXBINS * 4 + 256, 256));
 }
 
-hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
+template <typename KIND>
+static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
 {
     if (nbits < 1) nbits = 1;
     const int npass = (nbits + 7) / 8;
@@ -737,17 +750,26 @@ hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s
                 vin[v] = a.vals_out;
             }
             const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
-            hipLaunchKernelGGL(radix_count_kernel<RS_ITEMS>, g, b, 0, s, cb, shift, w);
+            hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND>), g, b, 0, s, cb, shift, w);
             if (maxc <= RS_ROW_LDS)
-                hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+                hipLaunchKernelGGL(radix_rowscan_lds_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
             else
-                hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
-            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true>), g, b, 0, s, sb);
-            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false>), g, b, 0, s, sb);
+                hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND>), g, b, 0, s, sb);
+            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND>), g, b, 0, s, sb);
             shift += w;
         }
         return hipGetLastError();
     });
+}
+
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0, SortKind kind)
+{
+    switch (kind) {
+    case SORT_TILE: return radix_sort_batch_k<TileSort>(jobs, V, nbits, s, shift0);
+    case SORT_CELLS: return radix_sort_batch_k<CellSort>(jobs, V, nbits, s, shift0);
+    default: return radix_sort_batch_k<DepthSort>(jobs, V, nbits, s, shift0);
+    }
 }
 
 size_t fused_pass1_scratch_bytes(int P)
@@ -798,27 +820,28 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
         if (phases & FUSED_COUNT) {
             hipLaunchKernelGGL(fused_pass1_count_kernel, g, b, 0, s, fb, gx, T, w1);
             if (maxc <= RS_ROW_LDS)
-                hipLaunchKernelGGL(radix_rowscan_lds_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+                hipLaunchKernelGGL(radix_rowscan_lds_kernel<TileSort>, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
             else
-                hipLaunchKernelGGL(radix_rowscan_kernel, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+                hipLaunchKernelGGL(radix_rowscan_kernel<TileSort>, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
         }
         if (!(phases & FUSED_SCATTER)) return hipGetLastError();
         hipLaunchKernelGGL(fused_pass1_scatter_kernel<RS_ITEMS>, g, b, 0, s, fb, gx, w1);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || npass == 1) return e;
         // the later passes: key bits [w1, nbits), ping-pong k1/v1 -> k0/v0 -> ...
-        return radix_sort_batch(rest, nv, nbits - w1, s, w1);
+        return radix_sort_batch(rest, nv, nbits - w1, s, w1, SORT_TILE);
     });
 }
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
-                      char* scratch, hipStream_t s, const uint2* rects, uint2* sorted_rects, uint32_t* sorted_counts)
+                      char* scratch, hipStream_t s, const uint2* rects, uint2* sorted_rects, uint32_t* sorted_counts,
+                      SortKind kind)
 {
     if (n <= 0) return hipSuccess;
     const SortJob j = {n, keys_in, pairs, k0, v0, k1, v1, out_x, out_y, sorted_keys, scratch, rects, sorted_rects,
                        sorted_counts};
-    return radix_sort_batch(&j, 1, nbits, s);
+    return radix_sort_batch(&j, 1, nbits, s, 0, kind);
 }
 
 hipError_t launch_tile_ranges_batch(const RangesJob* jobs, int V, int T, hipStream_t s)
@@ -852,11 +875,11 @@ hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges
     return launch_tile_ranges_batch(&j, 1, T, s);
 }
 
-hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const float* depths,
+hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const uint32_t* dkeys,
                              uint64_t* keys, hipStream_t s)
 {
     if (L <= 0) return hipSuccess;
-    hipLaunchKernelGGL(debug_keys_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, sorted_tiles, point_list, depths,
+    hipLaunchKernelGGL(debug_keys_kernel, dim3((L + 255) / 256), dim3(256), 0, s, L, sorted_tiles, point_list, dkeys,
                        keys);
     return hipGetLastError();
 }

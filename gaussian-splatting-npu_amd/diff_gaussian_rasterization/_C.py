@@ -84,6 +84,7 @@ _contig_cache = {}  # small non-contiguous inputs (the transposed view matrices)
 # render straight after the num_rendered read-back instead of returning to Python to allocate
 # (the reference's binningBuffer resize lambda, rasterize_points.cu:27-33, rasterizer_impl.cu:286).
 _binning_hint = {}
+_binning_hint_views = {}  # per device: the last view batch's num_rendered per view
 
 
 def _contiguous(t):
@@ -251,9 +252,15 @@ def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rota
     gsz, isz = lib.gsr_geometry_buffer_size(P), lib.gsr_image_buffer_size(W, H)
     geoms = [torch.empty((gsz,), dtype=torch.uint8, device=dev) for _ in range(V)]
     imgs = [torch.empty((isz,), dtype=torch.uint8, device=dev) for _ in range(V)]
-    hint = _binning_hint.get(dev)
-    cap = lib.gsr_binning_buffer_size(min(int(hint * 1.25) + 65536, 0x7FFFFFFF)) if hint is not None else 0
-    bins = [torch.empty((cap,), dtype=torch.uint8, device=dev) if cap else None for _ in range(V)]
+    # per-view capacity from that view's last num_rendered (a batch of the same V views: the previous
+    # step's batch), else from the largest of them: the views' buffers (kept alive by autograd
+    # until the backward) stay within 25 % + 64K instances of what each view needs
+    hints = _binning_hint_views.get(dev)
+    if hints is None or len(hints) != V:
+        h = _binning_hint.get(dev) if hints is None else max(hints)
+        hints = None if h is None else [h] * V
+    caps = [lib.gsr_binning_buffer_size(min(int(h * 1.25) + 65536, 0x7FFFFFFF)) for h in hints] if hints else [0] * V
+    bins = [torch.empty((c,), dtype=torch.uint8, device=dev) if c else None for c in caps]
     bg_p, means_p = p(background, "bg"), p(means3D, "means3D")
     colors_p, op_p = p(colors, "colors_precomp"), p(opacity, "opacities")
     sc_p, rot_p, cov_p = p(scales, "scales"), p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp")
@@ -273,9 +280,10 @@ def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rota
             _ptr_array([inv_out[v] for v in range(V)]), _ptr_array([radii_out[v] for v in range(V)]), bool(debug),
             stream, nr, rendered))
 
-    run([cap] * V)
+    run(caps)
     Ls = [int(nr[v]) for v in range(V)]
     _binning_hint[dev] = max(Ls)
+    _binning_hint_views[dev] = Ls
     if all(rendered[v] for v in range(V)):
         bins = [bins[v][:lib.gsr_binning_buffer_size(Ls[v])] for v in range(V)]  # views: the backward re-derives
     else:  # first call on this device, or the scene grew past the headroom: the batch again, exact buffers

@@ -70,15 +70,23 @@ class _DeferredBatch:
 
     def __init__(self):
         self.views = []
+        self.closed = False
         self.lock = threading.Lock()
 
     def add(self, view):
+        """Queue a view for the batched launch at the context's exit; a view whose backward runs
+        after that exit (its forward was inside the context, its loss.backward() outside) gets its
+        BACKWARD::preprocess right away, alone, so its gradients are never dropped."""
         with self.lock:
-            self.views.append(view)
+            if not self.closed:
+                self.views.append(view)
+                return
+        self._launch([view])
 
     def flush(self):
         with self.lock:
             views, self.views = self.views, []
+            self.closed = True
         # views share one set of Gaussian inputs and image/flag settings per batched launch
         groups = []
         for v in views:
@@ -100,6 +108,10 @@ class _DeferredBatch:
         stream = torch.cuda.current_stream(dev)
         for v in views:  # each view's render backward ran on its forward's stream
             stream.wait_event(v["event"])
+            # the batched kernel reads each view's state buffers on THIS stream: keep their memory
+            # out of the caching allocator's reuse on their own streams until it has run
+            for t in (v["geom"], v["binning"], v["radii"]):
+                t.record_stream(stream)
         inputs = {"means3D": c_m3, "dc": c_dc, "sh": c_sh, "opacities": c_op, "scales": c_sc, "rotations": c_rot,
                   "cov3D_precomp": c_cov, "colors_precomp": c_col}
         accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in inputs.items()) if g is not None}

@@ -134,8 +134,71 @@ TRAIN_LR = {"xyz": 0.00016, "f_dc": 0.0025, "f_rest": 0.0025 / 20.0, "opacity": 
             "rotation": 0.001}
 
 
+def expon_lr(lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_steps=1000000):
+    """utils/general_utils.py get_expon_lr_func (:29-63): log-linear decay from lr_init to
+    lr_final over max_steps, with an optional sine-eased delay."""
+    import math
+
+    def helper(step):
+        if step < 0 or (lr_init == 0.0 and lr_final == 0.0):
+            return 0.0
+        if lr_delay_steps > 0:
+            delay_rate = lr_delay_mult + (1 - lr_delay_mult) * math.sin(0.5 * math.pi * min(max(step / lr_delay_steps,
+                                                                                               0.0), 1.0))
+        else:
+            delay_rate = 1.0
+        t = min(max(step / max_steps, 0.0), 1.0)
+        return delay_rate * math.exp(math.log(lr_init) * (1 - t) + math.log(lr_final) * t)
+    return helper
+
+
+def build_rotation(r):
+    """utils/general_utils.py build_rotation (:78-99): normalised wxyz quaternions -> (N,3,3)."""
+    q = r / torch.sqrt(r[:, 0] * r[:, 0] + r[:, 1] * r[:, 1] + r[:, 2] * r[:, 2] + r[:, 3] * r[:, 3])[:, None]
+    w, x, y, z = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+    R = torch.zeros((q.size(0), 3, 3), device=r.device, dtype=r.dtype)
+    R[:, 0, 0] = 1 - 2 * (y * y + z * z)
+    R[:, 0, 1] = 2 * (x * y - w * z)
+    R[:, 0, 2] = 2 * (x * z + w * y)
+    R[:, 1, 0] = 2 * (x * y + w * z)
+    R[:, 1, 1] = 1 - 2 * (x * x + z * z)
+    R[:, 1, 2] = 2 * (y * z - w * x)
+    R[:, 2, 0] = 2 * (x * z - w * y)
+    R[:, 2, 1] = 2 * (y * z + w * x)
+    R[:, 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
+
+
+def inverse_sigmoid(x):
+    """utils/general_utils.py inverse_sigmoid (:18-19)."""
+    return torch.log(x / (1 - x))
+
+
+class OptimizationDefaults:
+    """The densification / schedule fields of arguments/__init__.py OptimizationParams (:74-100)
+    that train.py's iteration reads."""
+    iterations = 30_000
+    position_lr_init = 0.00016
+    position_lr_final = 0.0000016
+    position_lr_delay_mult = 0.01
+    position_lr_max_steps = 30_000
+    percent_dense = 0.01
+    lambda_dssim = 0.2
+    densification_interval = 100
+    opacity_reset_interval = 3000
+    densify_from_iter = 500
+    densify_until_iter = 15_000
+    densify_grad_threshold = 0.0002
+    depth_l1_weight_init = 1.0
+    depth_l1_weight_final = 0.01
+    exposure_lr_init = 0.01
+    exposure_lr_final = 0.001
+    exposure_lr_delay_steps = 0
+    exposure_lr_delay_mult = 0.0
+
+
 class DataParallelTrainer:
-    """train.py's iteration (train.py:97-183) over G ranks, one process per GPU.
+    """train.py's iteration (train.py:97-186) over G ranks, one process per GPU.
 
     The reference trains on one random view per iteration on one GPU.  Here one step takes a
     batch of views; every rank holds a full replica of the Gaussians and renders its share of the
@@ -144,53 +207,105 @@ class DataParallelTrainer:
     1. renders its views -- as ONE MultiViewRasterizer batch (the default; `batched=False`: one
        GaussianRasterizer call per view) -- with train.py's inputs
        (activations of gaussian_model.py:40-48,102-135; the separate-DC surface train.py selects
-       with SparseGaussianAdam, gaussian_renderer/__init__.py:82-100; image clamped to [0, 1],
-       :119), loss = (1 - lambda_dssim) L1 + lambda_dssim (1 - fused SSIM) (train.py:119-124),
-       backward; the per-view losses of the batch add up, so the step's gradient is the SUM of its
-       views' gradients;
+       with SparseGaussianAdam, gaussian_renderer/__init__.py:82-100; the per-camera exposure
+       when `exposures` is given, :112-115; image clamped to [0, 1], :119), loss = (1 - lambda_dssim)
+       L1 + lambda_dssim (1 - fused SSIM) (train.py:119-124) + the inverse-depth L1 term for views
+       with a depth target (train.py:128-141), backward; the per-view losses of the batch add up,
+       so the step's gradient is the SUM of its views' gradients;
     2. keeps train.py's densification statistics per view, locally (train.py:166,
        gaussian_model.py:471-473: max screen radius, norm of that view's screen-space gradient,
        visit count);
     3. all-reduces (SUM) ONE flat fp32 buffer: every parameter gradient (236 B per Gaussian at SH
        degree 3; the parameters' .grad are views into it, so autograd accumulates into it in place
-       and the collective runs in place) plus one visibility count per Gaussian, so the same
-       collective tells every rank which Gaussians some view of the step saw;
+       and the collective runs in place) plus one visibility count per Gaussian (and the exposure
+       gradients), so the same collective tells every rank which Gaussians some view of the step saw;
     4. steps the same optimizer on every rank: SparseGaussianAdam on the Gaussians visible in the
        step (train.py:180-183) or torch Adam (the default optimizer_type); identical reduced inputs
        keep the replicas bit-identical without a broadcast.
 
-    Densification itself stays with the caller (GaussianModel.densify_and_prune); before it runs,
-    `reduced_densification_stats()` gives every rank the statistics of ALL views since the last
-    reset (SUM of accum/denom, MAX of max_radii2D) -- reduced once at that point, not per step, so
-    nothing is counted twice.  Backend-agnostic: RCCL ("nccl") on MI355X nodes, gloo in the tests.
+    Densification (train.py:164-174) runs on every rank from the statistics of ALL views of ALL
+    ranks since the last densification (`reduced_densification_stats`: SUM of accum/denom, MAX of
+    max_radii2D, reduced once at that point): `densify_and_prune` / `reset_opacity` follow
+    gaussian_model.py:258-261,315-469, rebuild the flat buffer, the parameters and the optimizer
+    state (Adam / sparse-Adam moments: cat_tensors_to_optimizer, _prune_optimizer,
+    replace_tensor_to_optimizer) for the new P, identically on every rank (the split's random
+    samples come from a generator seeded identically everywhere).  `iteration()` is train.py's
+    loop body with that gating, the learning-rate schedule and the optimizer step.
+    Backend-agnostic: RCCL ("nccl") on MI355X nodes, gloo in the tests.
     """
 
-    def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None, batched=True):
+    def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None, batched=True,
+                 seed=0, exposures=None, spatial_lr_scale=None, opt=None):
         import diff_gaussian_rasterization as dgr
         self._dgr = dgr
         dev = raw["xyz"].device
         self.device = dev
-        self.P = P = raw["xyz"].shape[0]
         self.group = group
         self.batched = batched  # a rank's views as one MultiViewRasterizer batch (one launch per stage)
         self.lambda_dssim = lambda_dssim
+        self.opt = opt or OptimizationDefaults()
         self.bg = bg if bg is not None else torch.zeros(3, device=dev)
-        lr = dict(TRAIN_LR, **(lr or {}))
-        sizes = [raw[k].numel() for k in TRAIN_GROUPS]
-        # [gradients of every group | visibility count per Gaussian]
-        self.flat = torch.zeros(sum(sizes) + P, dtype=torch.float32, device=dev)
-        self.params = {}
-        off = 0
-        for k, n in zip(TRAIN_GROUPS, sizes):
-            p = torch.nn.Parameter(raw[k].detach().to(dev, torch.float32).contiguous().clone())
-            p.grad = self.flat[off:off + n].view_as(p)
-            self.params[k] = p
-            off += n
-        self.visible_count = self.flat[off:off + P]
-        groups = [{"params": [self.params[k]], "lr": lr[k], "name": k} for k in TRAIN_GROUPS]
+        self.lr = dict(TRAIN_LR, **(lr or {}))
+        # xyz schedule (gaussian_model.py:184,203-206): position_lr_* x spatial_lr_scale; only when
+        # the caller names the scene's spatial_lr_scale (else lr["xyz"] stays fixed)
+        self.xyz_schedule = None if spatial_lr_scale is None else expon_lr(
+            self.opt.position_lr_init * spatial_lr_scale, self.opt.position_lr_final * spatial_lr_scale,
+            lr_delay_mult=self.opt.position_lr_delay_mult, max_steps=self.opt.position_lr_max_steps)
+        self.depth_l1_weight = expon_lr(self.opt.depth_l1_weight_init, self.opt.depth_l1_weight_final,
+                                        max_steps=self.opt.iterations)
+        # the split's normal samples (gaussian_model.py:418): same seed on every rank -> same samples
+        self.gen = torch.Generator(device=dev)
+        self.gen.manual_seed(seed)
         self.sparse = optimizer == "sparse_adam"
+        self.optimizer = None
+        # per-camera 3x4 exposure (gaussian_model.py:175-176,201), optional (train_test_exp)
+        self.exposures = None
+        self.exposure_optimizer = None
+        if exposures is not None:
+            self.exposures = torch.nn.Parameter(exposures.detach().to(dev, torch.float32).contiguous().clone())
+            self.exposure_optimizer = torch.optim.Adam([self.exposures])
+            self.exposure_schedule = expon_lr(self.opt.exposure_lr_init, self.opt.exposure_lr_final,
+                                              lr_delay_steps=self.opt.exposure_lr_delay_steps,
+                                              lr_delay_mult=self.opt.exposure_lr_delay_mult,
+                                              max_steps=self.opt.iterations)
+        self._skip_step = set()
+        self._install({k: raw[k].detach().to(dev, torch.float32).contiguous().clone() for k in TRAIN_GROUPS})
+        groups = [{"params": [self.params[k]], "lr": self.lr[k], "name": k} for k in TRAIN_GROUPS]
         self.optimizer = (dgr.SparseGaussianAdam(groups, lr=0.0, eps=1e-15) if self.sparse
                           else torch.optim.Adam(groups, lr=0.0, eps=1e-15))
+
+    def _install(self, tensors, states=None):
+        """(Re)builds, for P = tensors["xyz"].shape[0]: the flat buffer [gradients of every group |
+        visibility count per Gaussian | exposure gradients], the parameters (their .grad views of
+        it), the densification statistics (zero), and -- after the first call -- the optimizer's
+        groups and state, moved onto the new parameters (`states`: group name -> state dict)."""
+        dev = self.device
+        P = tensors["xyz"].shape[0]
+        self.P = P
+        sizes = [tensors[k].numel() for k in TRAIN_GROUPS]
+        n_exp = self.exposures.numel() if self.exposures is not None else 0
+        self.flat = torch.zeros(sum(sizes) + P + n_exp, dtype=torch.float32, device=dev)
+        params = {}
+        off = 0
+        for k, n in zip(TRAIN_GROUPS, sizes):
+            p = torch.nn.Parameter(tensors[k].contiguous())
+            p.grad = self.flat[off:off + n].view_as(p)
+            params[k] = p
+            off += n
+        self.visible_count = self.flat[off:off + P]
+        off += P
+        if self.exposures is not None:
+            self.exposures.grad = self.flat[off:off + n_exp].view_as(self.exposures)
+        if self.optimizer is not None:
+            for group in self.optimizer.param_groups:
+                old = group["params"][0]
+                st = self.optimizer.state.pop(old, None)
+                new = params[group["name"]]
+                group["params"][0] = new
+                st = states.get(group["name"], st) if states is not None else st
+                if st:
+                    self.optimizer.state[new] = st
+        self.params = params
         self.stats = densification_stats(P, dev)
 
     def activations(self):
@@ -203,60 +318,85 @@ class DataParallelTrainer:
     def zero_grad(self):
         self.flat.zero_()
 
-    def render(self, settings, act=None):
-        """gaussian_renderer.render with separate_sh=True: (clamped image, screen-space points, radii)."""
+    def _expose(self, img, cam_index):
+        """gaussian_renderer/__init__.py:112-115: rendered = (img^T E[:3,:3])^T + E[:3,3]."""
+        if self.exposures is None or cam_index is None:
+            return img
+        e = self.exposures[cam_index]
+        return torch.matmul(img.permute(1, 2, 0), e[:3, :3]).permute(2, 0, 1) + e[:3, 3, None, None]
+
+    def render(self, settings, act=None, cam_index=None):
+        """gaussian_renderer.render with separate_sh=True: (clamped image, screen-space points, radii,
+        inverse depth)."""
         act = act or self.activations()
         means2D = torch.zeros_like(act["means3D"], requires_grad=True)
         means2D.retain_grad()
-        img, radii, _ = self._dgr.GaussianRasterizer(settings)(
+        img, radii, inv = self._dgr.GaussianRasterizer(settings)(
             means3D=act["means3D"], means2D=means2D, dc=act["dc"], shs=act["shs"], colors_precomp=None,
             opacities=act["opacities"], scales=act["scales"], rotations=act["rotations"], cov3D_precomp=None)
-        return img.clamp(0, 1), means2D, radii
+        return self._expose(img, cam_index).clamp(0, 1), means2D, radii, inv
 
     def render_views(self, settings_list, act=None):
-        """render() for a batch of views in one MultiViewRasterizer call: (clamped images (V,3,H,W),
-        screen-space points (V,P,3), radii (V,P))."""
+        """render() for a batch of views in one MultiViewRasterizer call: (images (V,3,H,W) before
+        exposure and clamp, screen-space points (V,P,3), radii (V,P), inverse depths (V,1,H,W))."""
         act = act or self.activations()
         means2D = torch.zeros((len(settings_list),) + tuple(act["means3D"].shape), dtype=act["means3D"].dtype,
                               device=act["means3D"].device, requires_grad=True)
         means2D.retain_grad()
-        imgs, radii, _ = self._dgr.MultiViewRasterizer(settings_list)(
+        imgs, radii, inv = self._dgr.MultiViewRasterizer(settings_list)(
             means3D=act["means3D"], means2D=means2D, dc=act["dc"], shs=act["shs"], colors_precomp=None,
             opacities=act["opacities"], scales=act["scales"], rotations=act["rotations"], cov3D_precomp=None)
-        return imgs.clamp(0, 1), means2D, radii
+        return imgs, means2D, radii, inv
 
-    def render_and_backward(self, views):
-        """Step 1-2 for this rank's views: [(GaussianRasterizationSettings, gt image (3,H,W))].
-        Gradients accumulate into the flat buffer; returns the per-view losses.  With `batched`
-        (the default) the views are one MultiViewRasterizer batch: each view's image is the one
-        GaussianRasterizer renders, bit for bit, and the parameter gradients are the sum over the
-        views up to fp32 summation order."""
+    def _view_loss(self, img, inv, view, depth_weight):
+        """train.py:115-141 for one view: alpha mask, L1 + D-SSIM, the inverse-depth L1 term."""
         from fused_ssim import fused_ssim
+        gt = view[1]
+        extra = view[2] if len(view) > 2 and view[2] is not None else {}
+        if extra.get("alpha_mask") is not None:
+            img = img * extra["alpha_mask"]
+        l1 = (img - gt).abs().mean()
+        loss = (1.0 - self.lambda_dssim) * l1 + self.lambda_dssim * (1.0 - fused_ssim(img[None], gt[None]))
+        if depth_weight > 0 and extra.get("invdepth") is not None:
+            mask = extra.get("depth_mask")
+            d = (inv - extra["invdepth"]) if mask is None else (inv - extra["invdepth"]) * mask
+            loss = loss + depth_weight * d.abs().mean()
+        return loss
+
+    def render_and_backward(self, views, depth_weight=0.0, track_stats=True):
+        """Step 1-2 for this rank's views: [(GaussianRasterizationSettings, gt image (3,H,W)[, extras])]
+        with extras an optional dict: "invdepth" / "depth_mask" (train.py:130-141, weighted by
+        `depth_weight`), "alpha_mask" (:115-117), "cam" (the view's exposure index).  Gradients
+        accumulate into the flat buffer; returns the per-view losses.  With `batched` (the default)
+        the views are one MultiViewRasterizer batch: each view's image is the one
+        GaussianRasterizer renders, bit for bit, and the parameter gradients are the sum over the
+        views up to fp32 summation order.  `track_stats`: train.py keeps densification statistics
+        only before densify_until_iter (train.py:164-167)."""
+        def cam_of(view):
+            return view[2].get("cam") if len(view) > 2 and view[2] is not None else None
         if self.batched and len(views) > 1:
             with self._dgr.accumulate_grads_in_place():
-                imgs, means2D, radii = self.render_views([s for s, _ in views])
-            losses = []
-            for v, (_, gt) in enumerate(views):
-                l1 = (imgs[v] - gt).abs().mean()
-                losses.append((1.0 - self.lambda_dssim) * l1 +
-                              self.lambda_dssim * (1.0 - fused_ssim(imgs[v][None], gt[None])))
+                imgs, means2D, radii, invs = self.render_views([v[0] for v in views])
+            losses = [self._view_loss(self._expose(imgs[j], cam_of(v)).clamp(0, 1), invs[j], v, depth_weight)
+                      for j, v in enumerate(views)]
             torch.stack(losses).sum().backward()
             with torch.no_grad():
-                for v in range(len(views)):
-                    add_view_stats(self.stats, means2D.grad[v], radii[v])
-                    self.visible_count += (radii[v] > 0).to(self.visible_count.dtype)
+                for j in range(len(views)):
+                    if track_stats:
+                        add_view_stats(self.stats, means2D.grad[j], radii[j])
+                    self.visible_count += (radii[j] > 0).to(self.visible_count.dtype)
             return [l.detach() for l in losses]
         losses = []
-        for settings, gt in views:
+        for v in views:
             # xyz, f_dc, f_rest enter the rasterizer as leaves whose .grad are views of the flat
             # buffer: the backward kernel adds into them directly (no separate accumulation pass)
             with self._dgr.accumulate_grads_in_place():
-                img, means2D, radii = self.render(settings)
-            l1 = (img - gt).abs().mean()
-            loss = (1.0 - self.lambda_dssim) * l1 + self.lambda_dssim * (1.0 - fused_ssim(img[None], gt[None]))
+                img, means2D, radii, inv = self.render(v[0], cam_index=cam_of(v))
+            loss = self._view_loss(img, inv, v, depth_weight)
             loss.backward()
             with torch.no_grad():
-                add_view_stats(self.stats, means2D.grad, radii)
+                if track_stats:
+                    add_view_stats(self.stats, means2D.grad, radii)
                 self.visible_count += (radii > 0).to(self.visible_count.dtype)
             losses.append(loss.detach())
         return losses
@@ -270,18 +410,64 @@ class DataParallelTrainer:
 
     @torch.no_grad()
     def optimizer_step(self):
-        """Step 4 (train.py:176-183)."""
-        if self.sparse:
-            self.optimizer.step(self.visible_count > 0, self.P)
-        else:
-            self.optimizer.step()
+        """Step 4 (train.py:176-183).  Parameters replaced by a densification or an opacity reset in
+        this iteration are new tensors without a gradient in the reference, so its optimizer skips
+        them (Adam skips parameters whose grad is None): the same here."""
+        if self.exposure_optimizer is not None:
+            self.exposure_optimizer.step()
+        skip = [self.params[k] for k in self._skip_step]
+        held = [p.grad for p in skip]
+        for p in skip:
+            p.grad = None
+        try:
+            if self.sparse:
+                self.optimizer.step(self.visible_count > 0, self.P)
+            else:
+                self.optimizer.step()
+        finally:
+            for p, g in zip(skip, held):
+                p.grad = g
+            self._skip_step = set()
 
-    def step(self, views):
+    def update_learning_rate(self, iteration):
+        """gaussian_model.py:213-223: the exposure and xyz schedules."""
+        if self.exposure_optimizer is not None:
+            for g in self.exposure_optimizer.param_groups:
+                g["lr"] = self.exposure_schedule(iteration)
+        if self.xyz_schedule is None:
+            return None
+        for g in self.optimizer.param_groups:
+            if g["name"] == "xyz":
+                g["lr"] = self.xyz_schedule(iteration)
+                return g["lr"]
+
+    def step(self, views, depth_weight=0.0):
         self.zero_grad()
-        losses = self.render_and_backward(views)
+        losses = self.render_and_backward(views, depth_weight)
         self.reduce()
         self.optimizer_step()
         return losses
+
+    def iteration(self, iteration, views, extent, white_background=False):
+        """train.py's loop body (train.py:93-186) for one data-parallel step: learning rates, render +
+        loss (with the depth term's schedule, :64,130), backward, the gradient all-reduce, the
+        densification gating (:164-174) and the optimizer step.  Returns the per-view losses and a
+        dict of what densification did (None when it did not run)."""
+        o = self.opt
+        self.update_learning_rate(iteration)
+        self.zero_grad()
+        track = iteration < o.densify_until_iter
+        losses = self.render_and_backward(views, self.depth_l1_weight(iteration), track_stats=track)
+        self.reduce()
+        did = None
+        if track:
+            if iteration > o.densify_from_iter and iteration % o.densification_interval == 0:
+                size_threshold = 20 if iteration > o.opacity_reset_interval else None
+                did = self.densify_and_prune(o.densify_grad_threshold, 0.005, extent, size_threshold)
+            if iteration % o.opacity_reset_interval == 0 or (white_background and iteration == o.densify_from_iter):
+                self.reset_opacity()
+        self.optimizer_step()
+        return losses, did
 
     def reduced_densification_stats(self):
         """Copies of the densification statistics of every view of every rank since the last
@@ -296,3 +482,91 @@ class DataParallelTrainer:
     def reset_densification_stats(self):
         self.stats["_sums"].zero_()
         self.stats["max_radii2D"].zero_()
+
+    # ---- densification (gaussian_model.py:315-469), identically on every rank ----------------
+    def _tensors_and_states(self):
+        T = {k: p.detach() for k, p in self.params.items()}
+        S = {k: dict(self.optimizer.state.get(p, {})) for k, p in self.params.items()}
+        return T, S
+
+    @staticmethod
+    def _cat(T, S, new):
+        """cat_tensors_to_optimizer (gaussian_model.py:364-384): append rows, zero moments for them."""
+        for k in TRAIN_GROUPS:
+            T[k] = torch.cat((T[k], new[k]), dim=0)
+            st = S[k]
+            if st:
+                st["exp_avg"] = torch.cat((st["exp_avg"], torch.zeros_like(new[k])), dim=0)
+                st["exp_avg_sq"] = torch.cat((st["exp_avg_sq"], torch.zeros_like(new[k])), dim=0)
+
+    @staticmethod
+    def _keep(T, S, mask):
+        """_prune_optimizer (gaussian_model.py:331-347): keep the rows of `mask`, moments too."""
+        for k in TRAIN_GROUPS:
+            T[k] = T[k][mask]
+            st = S[k]
+            if st:
+                st["exp_avg"] = st["exp_avg"][mask]
+                st["exp_avg_sq"] = st["exp_avg_sq"][mask]
+
+    @torch.no_grad()
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, stats=None, N=2):
+        """GaussianModel.densify_and_prune (gaussian_model.py:452-469) on the reduced statistics
+        (`stats`: the reduced statistics to use instead, e.g. a single process emulating ranks):
+        clone the small high-gradient Gaussians (:425-440), split the large ones into N samples
+        (:402-423), then prune the split originals, the transparent ones and -- with
+        max_screen_size -- the world-space large ones.  As in the reference, densification_postfix
+        zeroes max_radii2D before the prune reads it (:399), so the screen-space test never fires.
+        Rebuilds buffers, parameters and optimizer state for the new P; returns the counts."""
+        pd = self.opt.percent_dense
+        st = stats if stats is not None else self.reduced_densification_stats()
+        grads = st["xyz_gradient_accum"] / st["denom"]
+        grads[grads.isnan()] = 0.0
+        T, S = self._tensors_and_states()
+        P0 = T["xyz"].shape[0]
+        # clone (densify_and_clone)
+        sel = torch.norm(grads, dim=-1) >= max_grad
+        sel = torch.logical_and(sel, torch.exp(T["scaling"]).max(dim=1).values <= pd * extent)
+        n_clone = int(sel.sum())
+        self._cat(T, S, {k: T[k][sel] for k in TRAIN_GROUPS})
+        # split (densify_and_split)
+        n_init = T["xyz"].shape[0]
+        padded = torch.zeros((n_init,), device=self.device)
+        padded[:grads.shape[0]] = grads.squeeze()
+        scaling = torch.exp(T["scaling"])
+        sel = padded >= max_grad
+        sel = torch.logical_and(sel, scaling.max(dim=1).values > pd * extent)
+        n_split = int(sel.sum())
+        stds = scaling[sel].repeat(N, 1)
+        samples = torch.normal(mean=torch.zeros((stds.size(0), 3), device=self.device), std=stds, generator=self.gen)
+        rots = build_rotation(T["rotation"][sel]).repeat(N, 1, 1)
+        new = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + T["xyz"][sel].repeat(N, 1),
+               "scaling": torch.log(scaling[sel].repeat(N, 1) / (0.8 * N)),
+               "rotation": T["rotation"][sel].repeat(N, 1),
+               "f_dc": T["f_dc"][sel].repeat(N, 1, 1), "f_rest": T["f_rest"][sel].repeat(N, 1, 1),
+               "opacity": T["opacity"][sel].repeat(N, 1)}
+        self._cat(T, S, new)
+        prune_filter = torch.cat((sel, torch.zeros(N * n_split, device=self.device, dtype=torch.bool)))
+        self._keep(T, S, ~prune_filter)
+        # prune (max_radii2D is all zero here, see the docstring)
+        prune = (torch.sigmoid(T["opacity"]) < min_opacity).squeeze(-1)
+        if max_screen_size:
+            big_ws = torch.exp(T["scaling"]).max(dim=1).values > 0.1 * extent
+            prune = torch.logical_or(prune, big_ws)
+        n_prune = int(prune.sum())
+        self._keep(T, S, ~prune)
+        self._install(T, S)
+        self._skip_step = set(TRAIN_GROUPS)  # every parameter is a new tensor without a gradient
+        return {"P_before": P0, "cloned": n_clone, "split": n_split, "pruned": n_prune, "P_after": self.P}
+
+    @torch.no_grad()
+    def reset_opacity(self):
+        """GaussianModel.reset_opacity (gaussian_model.py:258-261) + replace_tensor_to_optimizer
+        (:315-329): opacities capped at 0.01, their moments zeroed, the step count kept."""
+        p = self.params["opacity"]
+        p.copy_(inverse_sigmoid(torch.min(torch.sigmoid(p), torch.ones_like(p) * 0.01)))
+        st = self.optimizer.state.get(p)
+        if st:
+            st["exp_avg"] = torch.zeros_like(p)
+            st["exp_avg_sq"] = torch.zeros_like(p)
+        self._skip_step.add("opacity")

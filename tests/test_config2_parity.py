@@ -61,6 +61,7 @@ def _grad_check(name, hip, ref):
                               "n_over_GRAD_RTOL": n_out, "elements": int(err.size)})
     assert ok, f"{name}: rel err {rel:.3e} (tolerance {GRAD_RTOL_FLIP} of max|ref|)"
     assert n_out <= GRAD_OUTLIERS, f"{name}: {n_out} elements beyond {common.GRAD_RTOL} of max|ref|"
+    common.check_rel(name, hip, ref)  # per element, not only relative to the max
 
 
 @pytest.mark.parametrize("antialiasing", [False, True])

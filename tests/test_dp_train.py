@@ -152,3 +152,146 @@ def test_batched_views_match_per_view_renders():
     a, b = out[True][1], out[False][1]
     assert np.abs(a - b).max() <= 1e-5 * np.abs(b).max() + 1e-9, np.abs(a - b).max()
     np.testing.assert_array_equal(out[True][2], out[False][2])
+
+
+# ---- densification across ranks -----------------------------------------
+D_ITERS = 4  # train.py iterations 1..4: densify at 2 and 4, opacity reset at 3
+
+
+def _densify_opt(threshold):
+    from diff_gaussian_rasterization import multiview
+    o = multiview.OptimizationDefaults()
+    o.densify_from_iter, o.densification_interval, o.opacity_reset_interval = 0, 2, 3
+    o.densify_until_iter, o.densify_grad_threshold = 100, threshold
+    return o
+
+
+EXTENT = 1.3  # percent_dense * extent = 0.013: about half the Gaussians clone, half split
+
+
+def _dsetup(dev, threshold):
+    import synthetic
+    trainer, settings, targets = _setup(dev)
+    raw = {k: p.detach().clone() for k, p in trainer.params.items()}
+    raw["opacity"][::10] = -6.0  # below train.py's min_opacity 0.005: pruned at the first densification
+    from diff_gaussian_rasterization import multiview
+    trainer = multiview.DataParallelTrainer(raw, lr={"xyz": 4.8e-4}, opt=_densify_opt(threshold), seed=11)
+    # inverse-depth targets (the ground-truth scene's own) so the depth L1 term is exercised
+    import diff_gaussian_rasterization as dgr
+    gt = {k: v.to(dev) for k, v in synthetic.make_scene(P, seed=0).items()}
+    views = []
+    with torch.no_grad():
+        for s, t in zip(settings, targets):
+            inv = dgr.GaussianRasterizer(s)(means3D=gt["means3D"], means2D=torch.zeros_like(gt["means3D"]),
+                                            shs=gt["shs"], opacities=gt["opacities"], scales=gt["scales"],
+                                            rotations=gt["rotations"])[2]
+            views.append((s, t, {"invdepth": inv * 1.1, "depth_mask": (inv > 0).float()}))
+    return trainer, views
+
+
+def _drank_views(it, rank, views):
+    from diff_gaussian_rasterization import multiview
+    batch = [(BATCH * it + j) % VIEWS for j in range(BATCH)]
+    return [views[batch[j]] for j in multiview.views_of_batch(rank, WORLD, BATCH)]
+
+
+def _dworker(rank, port, threshold, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "gaussian-splatting-npu_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        trainer, views = _dsetup(dev, threshold)
+        did = []
+        for it in range(1, D_ITERS + 1):
+            did.append(trainer.iteration(it, _drank_views(it, rank, views), EXTENT)[1])
+        torch.cuda.synchronize()
+        q.put((rank, {k: p.detach().cpu().numpy() for k, p in trainer.params.items()},
+               {k: trainer.optimizer.state[p]["exp_avg"].cpu().numpy() for k, p in trainer.params.items()}, did))
+    finally:
+        dist.destroy_process_group()
+
+
+def _emulate(dev, threshold):
+    """The same iterations in one process: both ranks' views rendered here, their gradient buffers
+    and densification statistics combined as the collectives combine them (x0 + x1, max)."""
+    from diff_gaussian_rasterization import multiview
+    trainer, views = _dsetup(dev, threshold)
+    o = trainer.opt
+    stats = [trainer.stats, multiview.densification_stats(trainer.P, dev)]
+    did = []
+    for it in range(1, D_ITERS + 1):
+        trainer.update_learning_rate(it)
+        w = trainer.depth_l1_weight(it)
+        trainer.zero_grad()
+        trainer.stats = stats[0]
+        trainer.render_and_backward(_drank_views(it, 0, views), w)
+        g0 = trainer.flat.clone()
+        trainer.zero_grad()
+        trainer.stats = stats[1]
+        trainer.render_and_backward(_drank_views(it, 1, views), w)
+        trainer.flat += g0
+        d = None
+        if it > o.densify_from_iter and it % o.densification_interval == 0:
+            red = multiview.densification_stats(trainer.P, dev)
+            red["_sums"].copy_(stats[0]["_sums"] + stats[1]["_sums"])
+            red["max_radii2D"].copy_(torch.max(stats[0]["max_radii2D"], stats[1]["max_radii2D"]))
+            d = trainer.densify_and_prune(o.densify_grad_threshold, 0.005, EXTENT,
+                                          20 if it > o.opacity_reset_interval else None, stats=red)
+            stats = [trainer.stats, multiview.densification_stats(trainer.P, dev)]
+        if it % o.opacity_reset_interval == 0:
+            trainer.reset_opacity()
+        trainer.optimizer_step()
+        did.append(d)
+    torch.cuda.synchronize()
+    return trainer, did
+
+
+def test_two_ranks_densify_and_reset_match_single_process():
+    """train.py's iteration with densification (train.py:164-174) over 2 gloo ranks: two
+    densify_and_prune calls (clone, split and prune each happen) and an opacity reset between
+    them, plus the inverse-depth L1 term; afterwards both ranks' parameters and Adam moments are
+    bit-identical to each other and to the single-process emulation."""
+    dev = torch.device("cuda", 0)
+    # a threshold that selects about half of the Gaussians: the median of the statistics the first
+    # densification will see (a dry run of iterations 1-2 in one process)
+    trainer, views = _dsetup(dev, 1.0)
+    from diff_gaussian_rasterization import multiview
+    for it in (1, 2):
+        trainer.zero_grad()
+        trainer.render_and_backward(_drank_views(it, 0, views), trainer.depth_l1_weight(it))
+        trainer.render_and_backward(_drank_views(it, 1, views), trainer.depth_l1_weight(it))
+    g = trainer.stats["xyz_gradient_accum"] / trainer.stats["denom"]
+    threshold = float(torch.nan_to_num(g, 0.0).median())
+    assert threshold > 0
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dworker, args=(r, port, threshold, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+
+    emu, did = _emulate(dev, threshold)
+    d2, d4 = did[1], did[3]
+    assert d2 is not None and d4 is not None and did[0] is None and did[2] is None
+    assert d2["cloned"] > 0 and d2["split"] > 0 and d2["pruned"] > 0, d2
+    assert d4["P_after"] != P, did
+    for rank, params, moments, rdid in res:
+        assert rdid == did, (rank, rdid, did)
+        for k in params:
+            np.testing.assert_array_equal(params[k], emu.params[k].detach().cpu().numpy(), err_msg=f"rank {rank} {k}")
+            np.testing.assert_array_equal(moments[k], emu.optimizer.state[emu.params[k]]["exp_avg"].cpu().numpy(),
+                                          err_msg=f"rank {rank} exp_avg {k}")

@@ -206,3 +206,113 @@ def test_views_of_batch_strong_scaling(world):
     assert all(len(vs) == 8 // world for vs in per)
     with pytest.raises(ValueError):
         multiview.views_of_batch(0, 16, 8)
+
+
+# ---- densification surgery (DataParallelTrainer.densify_and_prune / reset_opacity) on CPU ------
+def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_size, gen, pd=0.01, N=2):
+    """gaussian_model.py:315-469 step by step on dicts (the reference's own sequence: clone's
+    postfix, split's postfix, split prune, final prune; tensors and Adam moments)."""
+    names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
+    T = {k: raw[k].clone() for k in names}
+    S = {k: {"exp_avg": state[k][0].clone(), "exp_avg_sq": state[k][1].clone()} for k in names}
+
+    def cat(d):
+        for k in names:
+            T[k] = torch.cat((T[k], d[k]), 0)
+            S[k]["exp_avg"] = torch.cat((S[k]["exp_avg"], torch.zeros_like(d[k])), 0)
+            S[k]["exp_avg_sq"] = torch.cat((S[k]["exp_avg_sq"], torch.zeros_like(d[k])), 0)
+
+    def prune(mask):
+        keep = ~mask
+        for k in names:
+            T[k] = T[k][keep]
+            S[k]["exp_avg"] = S[k]["exp_avg"][keep]
+            S[k]["exp_avg_sq"] = S[k]["exp_avg_sq"][keep]
+    # densify_and_clone
+    sel = torch.where(torch.norm(grads, dim=-1) >= max_grad, True, False)
+    sel = torch.logical_and(sel, torch.max(torch.exp(T["scaling"]), dim=1).values <= pd * extent)
+    cat({k: T[k][sel] for k in names})
+    # densify_and_split
+    n_init = T["xyz"].shape[0]
+    padded = torch.zeros((n_init,))
+    padded[:grads.shape[0]] = grads.squeeze()
+    sel = torch.where(padded >= max_grad, True, False)
+    sel = torch.logical_and(sel, torch.max(torch.exp(T["scaling"]), dim=1).values > pd * extent)
+    stds = torch.exp(T["scaling"])[sel].repeat(N, 1)
+    samples = torch.normal(mean=torch.zeros((stds.size(0), 3)), std=stds, generator=gen)
+    rots = multiview.build_rotation(T["rotation"][sel]).repeat(N, 1, 1)
+    new = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + T["xyz"][sel].repeat(N, 1),
+           "scaling": torch.log(torch.exp(T["scaling"])[sel].repeat(N, 1) / (0.8 * N)),
+           "rotation": T["rotation"][sel].repeat(N, 1), "f_dc": T["f_dc"][sel].repeat(N, 1, 1),
+           "f_rest": T["f_rest"][sel].repeat(N, 1, 1), "opacity": T["opacity"][sel].repeat(N, 1)}
+    cat(new)
+    prune(torch.cat((sel, torch.zeros(N * int(sel.sum()), dtype=bool))))
+    max_radii2D = torch.zeros((T["xyz"].shape[0],))  # densification_postfix zeroed it
+    mask = (torch.sigmoid(T["opacity"]) < min_opacity).squeeze()
+    if max_screen_size:
+        mask = mask | (max_radii2D > max_screen_size) | (torch.exp(T["scaling"]).max(dim=1).values > 0.1 * extent)
+    prune(mask)
+    return T, S
+
+
+def test_densify_and_prune_matches_reference_sequence():
+    """DataParallelTrainer.densify_and_prune (one pass over the tensors and the optimizer state,
+    rebuilding the flat gradient buffer) against the reference's step-by-step sequence, and
+    reset_opacity against gaussian_model.py:258-261 -- on CPU tensors with torch Adam."""
+    P, M = 400, 15
+    g = torch.Generator().manual_seed(3)
+    raw = {"xyz": torch.randn(P, 3, generator=g), "f_dc": torch.randn(P, 1, 3, generator=g),
+           "f_rest": 0.1 * torch.randn(P, M, 3, generator=g),
+           "opacity": torch.randn(P, 1, generator=g) * 3.0,
+           "scaling": torch.log(0.003 + 0.02 * torch.rand(P, 3, generator=g)),
+           "rotation": torch.randn(P, 4, generator=g)}
+    tr = multiview.DataParallelTrainer(raw, optimizer="adam", seed=9)
+    for p in tr.params.values():  # one optimizer step so the moments are non-trivial
+        p.grad.copy_(torch.randn(p.shape, generator=g))
+    tr.optimizer_step()
+    state = {k: (tr.optimizer.state[p]["exp_avg"].clone(), tr.optimizer.state[p]["exp_avg_sq"].clone())
+             for k, p in tr.params.items()}
+    before = {k: p.detach().clone() for k, p in tr.params.items()}
+    stats = multiview.densification_stats(P)
+    stats["xyz_gradient_accum"].copy_(torch.rand(P, 1, generator=g) * 2e-3)
+    stats["denom"].copy_(torch.randint(0, 3, (P, 1), generator=g).float())  # some 0/0 -> NaN -> 0
+    stats["max_radii2D"].copy_(torch.rand(P, generator=g) * 40)
+    did = tr.densify_and_prune(5e-4, 0.05, 1.3, 20, stats=stats)
+    gen = torch.Generator().manual_seed(9)
+    grads = stats["xyz_gradient_accum"] / stats["denom"]
+    grads[grads.isnan()] = 0.0
+    T, S = _ref_densify(before, state, grads, 5e-4, 0.05, 1.3, 20, gen)
+    assert did["cloned"] > 0 and did["split"] > 0 and did["pruned"] > 0, did
+    assert tr.P == T["xyz"].shape[0] == did["P_after"]
+    for k, p in tr.params.items():
+        assert torch.equal(p.detach(), T[k]), k
+        assert torch.equal(tr.optimizer.state[p]["exp_avg"], S[k]["exp_avg"]), k
+        assert torch.equal(tr.optimizer.state[p]["exp_avg_sq"], S[k]["exp_avg_sq"]), k
+        # the gradients are views of the rebuilt flat buffer, zeroed
+        assert p.grad.shape == p.shape and p.grad.untyped_storage().data_ptr() == tr.flat.untyped_storage().data_ptr()
+    assert tr.stats["denom"].shape == (tr.P, 1) and float(tr.stats["_sums"].abs().sum()) == 0.0
+    # the iteration's optimizer step skips the replaced parameters (the reference's have no grad)
+    snap = {k: p.detach().clone() for k, p in tr.params.items()}
+    tr.optimizer_step()
+    assert all(torch.equal(snap[k], tr.params[k].detach()) for k in snap)
+    # reset_opacity: min(sigmoid, 0.01) in logit space, moments zeroed, opacity not stepped this time
+    op = tr.params["opacity"].detach().clone()
+    tr.reset_opacity()
+    want = multiview.inverse_sigmoid(torch.min(torch.sigmoid(op), torch.ones_like(op) * 0.01))
+    assert torch.equal(tr.params["opacity"].detach(), want)
+    assert float(tr.optimizer.state[tr.params["opacity"]]["exp_avg"].abs().sum()) == 0.0
+    for p in tr.params.values():
+        p.grad.copy_(torch.randn(p.shape, generator=g))
+    tr.optimizer_step()
+    assert torch.equal(tr.params["opacity"].detach(), want)
+    assert not torch.equal(tr.params["xyz"].detach(), T["xyz"])
+
+
+def test_expon_lr_matches_reference_formula():
+    """utils/general_utils.py get_expon_lr_func: endpoints, log-linear midpoint, delay easing."""
+    import math
+    f = multiview.expon_lr(1e-2, 1e-4, max_steps=100)
+    assert math.isclose(f(0), 1e-2) and math.isclose(f(100), 1e-4) and math.isclose(f(50), 1e-3)
+    assert f(-1) == 0.0 and math.isclose(f(1000), 1e-4)
+    d = multiview.expon_lr(1.0, 1.0, lr_delay_steps=10, lr_delay_mult=0.01)
+    assert math.isclose(d(0), 0.01) and math.isclose(d(10), 1.0) and 0.01 < d(5) < 1.0

@@ -186,6 +186,36 @@ def test_deferred_backward_matches_multiview(mode, antialiasing):
         assert torch.equal(deferred[k].grad, multi[k].grad), k
 
 
+def test_deferred_backward_after_context_exit():
+    """A forward inside deferred_backward whose backward runs after the context has exited: its
+    BACKWARD::preprocess runs at once, alone (ADVICE r02) -- the gradients equal the ordinary
+    backward's (dL/dmean2D bitwise, the parameters up to the batched kernel's summation order),
+    nothing is dropped."""
+    import diff_gaussian_rasterization as dgr
+    case = _case()
+    bg = case["bg"].to(DEV)
+    s = _settings(case["cams"][0], False, bg)
+    gc, gi = (g.to(DEV) for g in case["grads"][0])
+
+    plain = _leaves(case, "sh_scales")
+    m_plain = torch.zeros((P, 3), device=DEV, requires_grad=True)
+    c, _, i = dgr.GaussianRasterizer(s)(means2D=m_plain, **plain)
+    torch.autograd.backward([c, i], [gc, gi])
+
+    late = _leaves(case, "sh_scales")
+    m_late = torch.zeros((P, 3), device=DEV, requires_grad=True)
+    with dgr.deferred_backward():
+        c2, _, i2 = dgr.GaussianRasterizer(s)(means2D=m_late, **late)
+    torch.autograd.backward([c2, i2], [gc, gi])  # after the exit: its batch is already closed
+    torch.cuda.synchronize()
+    assert torch.equal(m_late.grad, m_plain.grad)
+    for k in plain:
+        assert late[k].grad is not None, f"d{k} dropped"
+        ok, rel = common.allclose_rel(late[k].grad.cpu().numpy(), plain[k].grad.cpu().numpy(), rtol=1e-5,
+                                      atol=1e-12)
+        assert ok, f"d{k}: late deferred vs plain rel {rel:.3e}"
+
+
 def test_deferred_backward_activations_streams_accumulation():
     """The train.py shape: activations between the parameters and the rasterizer (exp, sigmoid,
     normalize), views alternating between two streams, and a second batch adding into the .grad of

@@ -12,18 +12,19 @@ import json
 import os
 import sys
 
-SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "scan_lookback_kernel": "scan",
+SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "preprocess_views_kernel": "preprocess_fwd",
+         "scan_lookback_kernel": "scan",
          "emit_instances_kernel": "emit_instances", "tile_ranges_kernel": "tile_ranges",
          "tile_order_kernel": "tile_order", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
          "preprocess_bwd_kernel": "preprocess_bwd", "preprocess_bwd_views_kernel": "preprocess_bwd",
-         # the depth sort and the tile sort share these kernels: reported together, per step
-         "radix_count_kernel": "radix_sorts", "radix_rowscan_kernel": "radix_sorts",
-         "radix_rowscan_lds_kernel": "radix_sorts",
-         "radix_scatter_kernel": "radix_sorts",
-         "fused_pass1_count_kernel": "radix_sorts", "fused_pass1_scatter_kernel": "radix_sorts",
+         # the radix passes carry their sort's name tag (radix.hip): depth sort, tile sort (+ its fused
+         # first pass), distCUDA2's cell sort
+         "DepthSort": "depth_sort", "TileSort": "tile_sort", "fused_pass1_": "tile_sort", "CellSort": "distCUDA2",
          # SURVEY §8f side paths (bench.py aux leg)
          "knn_": "distCUDA2", "ssim_fwd_kernel": "ssim_fwd", "ssim_bwd_kernel": "ssim_bwd",
          "adam_update_multi_kernel": "sparse_adam"}
+# operations made of several kernels (several dispatches per call)
+MULTI = ("depth_sort", "tile_sort", "distCUDA2")
 
 
 def short_name(k):
@@ -33,7 +34,7 @@ def short_name(k):
     return None
 
 
-def main(d, lib_sha256=None):
+def main(d, lib_sha256=None, workload=None, calls=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
@@ -57,32 +58,46 @@ def main(d, lib_sha256=None):
             ent[c] = sum(per.values()) / max(1, len(per))
             ent["dispatches"] = len(per)
         out[k[:120]] = ent
-    # Per-launch figures per short name.  Template variants of one kernel (render_bwd<true/false>,
-    # tile_order<true/false>, ...) are alternatives of ONE launch: dispatch-weighted mean.  The radix
-    # kernels of a sort are consecutive launches: their per-dispatch means are summed.
-    def per_launch(counter_fn):
-        acc_v, acc_n = collections.defaultdict(float), collections.defaultdict(float)
+    # Per short name: the counter summed over ALL its dispatches (totals) and the dispatch count.
+    # A caller that knows how many times each operation ran (bench.py: launches per step x steps)
+    # divides the totals by that; the per-launch figures below assume single-kernel operations run
+    # once per dispatch, and for the multi-kernel sorts divide by `calls` when given.
+    def totals(counter_fn):
+        tot, n = collections.defaultdict(float), collections.defaultdict(int)
         for k, ent in out.items():
             s = short_name(k)
             v = counter_fn(ent)
             if not s or v is None:
                 continue
-            if s in ("radix_sorts", "distCUDA2"):  # several different kernels per call
-                acc_v[s] += v
-                acc_n[s] = 1.0
-            else:
-                acc_v[s] += v * ent["dispatches"]
-                acc_n[s] += ent["dispatches"]
-        return {s: acc_v[s] / acc_n[s] for s in acc_v if acc_n[s]}
+            tot[s] += v * ent["dispatches"]
+            n[s] += ent["dispatches"]
+        return tot, n
 
-    traffic = per_launch(lambda e: (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
-                         if "FETCH_SIZE" in e and "WRITE_SIZE" in e else None)
-    # stamped with the library they were measured on: bench.py uses committed figures only for that build
-    json.dump({"lib_sha256": lib_sha256, "bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
+    def per_launch(tot, n):
+        res = {}
+        for s in tot:
+            if s in MULTI:
+                if calls and calls.get(s):
+                    res[s] = tot[s] / calls[s]
+            elif n[s]:
+                res[s] = tot[s] / n[s]
+        return res
+
+    t_tot, t_n = totals(lambda e: (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
+                        if "FETCH_SIZE" in e and "WRITE_SIZE" in e else None)
+    traffic = per_launch(t_tot, t_n)
+    # stamped with the library AND the workload they were measured on: bench.py uses committed
+    # figures only for that build and that workload
+    json.dump({"lib_sha256": lib_sha256, "workload": workload,
+               "bytes_per_launch": {k: round(v) for k, v in traffic.items()},
+               "bytes_total": {k: round(v) for k, v in t_tot.items()}, "dispatches": dict(t_n)},
               open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
     # VALU wave-instructions per launch (bench.py's secondary, VALU-issue roofline)
-    valu = per_launch(lambda e: e.get("SQ_INSTS_VALU"))
-    json.dump({"lib_sha256": lib_sha256, "winst_per_launch": {k: round(v) for k, v in valu.items()}},
+    v_tot, v_n = totals(lambda e: e.get("SQ_INSTS_VALU"))
+    valu = per_launch(v_tot, v_n)
+    json.dump({"lib_sha256": lib_sha256, "workload": workload,
+               "winst_per_launch": {k: round(v) for k, v in valu.items()},
+               "winst_total": {k: round(v) for k, v in v_tot.items()}, "dispatches": dict(v_n)},
               open(os.path.join(d, "pmc_valu.json"), "w"), indent=1)
     print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
                      indent=1))

@@ -8,7 +8,7 @@ TAG=${1:-pmc}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-pmc ${BENCH_ARGS:-}"
+BENCH="python3 bench.py --pmc-child --steps 1 --warmup 1 ${BENCH_ARGS:-}"
 run() {
     local name=$1; shift
     echo "=== $name: $*"

@@ -1,0 +1,44 @@
+#!/bin/bash
+# GPU-box session in steps, each under its own time limit; the first failing step ends it.
+# Usage: tools/sess.sh <tag> <step>...   steps: test | testsel:<pytest selection> | bench | benchq |
+#        trace | hits | pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-sess}
+shift || true
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+run() {  # run <name> <timeout> <cmd...>
+    local name=$1 tmo=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -n 4 "$OUT/$name.log" | cut -c1-600
+    [ $rc -eq 0 ] || exit $rc
+}
+for st in "$@"; do
+  case "$st" in
+    test) run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
+          cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null ;;
+    testsel:*) run pytest_sel 600 python -u -m pytest ${st#testsel:} -m gpu -x -v --timeout 300 --timeout-method thread
+          cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null ;;
+    bench) run bench 600 python -u bench.py
+           cp -f gpurun_out/pmc_step.json gpurun_out/pmc_single.json "$OUT/" 2>/dev/null ;;
+    benchq) run benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-aux --no-pmc --no-single-view ;;
+    trace) run trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-aux --no-single-view
+           python3 - "$OUT" <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/prof/**/*kernel_stats.csv", recursive=True)[0]
+for r in csv.DictReader(open(f)):
+    if "at::" not in r["Name"]:
+        print(f'{r["Name"][:72]:72s} {r["Calls"]:>4} {float(r["AverageNs"])/1000:8.1f}us')
+PY
+           ;;
+    hits) run hits 200 python -u tools/dbg/hit_dump.py ;;
+    pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
+    *) echo "unknown step $st"; exit 2 ;;
+  esac
+done
+echo "session done"
