@@ -84,6 +84,10 @@ def parse():
                          "before this view's backward, or every forward before every backward")
     ap.add_argument("--no-fused-accumulation", action="store_true",
                     help="accumulate the views' gradients with autograd's separate add instead of in the kernel")
+    ap.add_argument("--no-overlap-allreduce", action="store_true",
+                    help="N > 1: all-reduce the gradients after the backward instead of overlapped with it")
+    ap.add_argument("--allreduce-chunks", type=int, default=4,
+                    help="N > 1: Gaussian ranges of the overlapped gradient all-reduce")
     ap.add_argument("--no-single-view", action="store_true",
                     help="skip the config2_single_view leg (plain GaussianRasterizer fwd+bwd of view 0, own roofline)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
@@ -282,23 +286,32 @@ def main():
     gc_batch = torch.stack([g[0] for g in grads]) if mv else None
     gi_batch = torch.stack([g[1] for g in grads]) if mv else None
 
-    def step(record_allreduce=False, overlap=True):
+    # N > 1: the gradient all-reduce overlapped with the batched backward (multiview.
+    # overlapped_allreduce: the preprocess backward in Gaussian ranges, each range reduced while the
+    # next computes) unless --no-overlap-allreduce; comm=False: no collective (compute-only pass)
+    overlap_ar = world > 1 and not args.no_overlap_allreduce and (args.batch_views or args.deferred)
+
+    def step(record_allreduce=False, overlap=True, comm=True):
         for p in params.values():
             p.grad = None
         for m in means2Ds:
             m.grad = None
-        if mv is not None:
-            means2D_batch.grad = None
-            color, radii, inv = mv(means3D=params["means3D"], means2D=means2D_batch, shs=params["shs"],
-                                   opacities=params["opacities"], scales=params["scales"],
-                                   rotations=params["rotations"])
-            torch.autograd.backward([color, inv], [gc_batch, gi_batch])
-        else:
-            n_st = len(streams) if overlap else 1
-            for st in streams[1:n_st]:
-                st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
-            with (dgr.deferred_backward() if args.deferred else contextlib.nullcontext()):
-                views_loop(n_st)
+        ovl = overlap_ar and comm and not record_allreduce
+        with (multiview.overlapped_allreduce(chunks=args.allreduce_chunks) if ovl else contextlib.nullcontext()):
+            if mv is not None:
+                means2D_batch.grad = None
+                color, radii, inv = mv(means3D=params["means3D"], means2D=means2D_batch, shs=params["shs"],
+                                       opacities=params["opacities"], scales=params["scales"],
+                                       rotations=params["rotations"])
+                torch.autograd.backward([color, inv], [gc_batch, gi_batch])
+            else:
+                n_st = len(streams) if overlap else 1
+                for st in streams[1:n_st]:
+                    st.wait_stream(main_stream)  # the step's start (parameters, previous step's collective)
+                with (dgr.deferred_backward() if args.deferred else contextlib.nullcontext()):
+                    views_loop(n_st)
+        if ovl or not comm:
+            return
         if record_allreduce:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -390,7 +403,9 @@ def main():
             if cnt[k]:
                 kern[lib.gsr_profile_kernel_name(k).decode()] = {"avg_ms": tot[k] / cnt[k], "launches": cnt[k]}
 
-    # all-reduce share of the step: events around the collective, separate pass
+    # all-reduce share of the step, separate passes: the collective alone (events around
+    # a non-overlapped allreduce_grads), and the step without any collective (compute only); the
+    # exposed communication is the timed step minus the compute-only step
     allreduce = None
     if world > 1:
         for _ in range(min(args.steps, 5)):
@@ -398,9 +413,22 @@ def main():
         torch.cuda.synchronize()
         ar_ms = sum(a.elapsed_time(b) for a, b, _ in ar_events) / len(ar_events)
         ar_ms = multiview.max_over_ranks(ar_ms / 1e3, dev) * 1e3
-        allreduce = {"ms": round(ar_ms, 4), "bytes_per_rank": ar_events[0][2],
-                     "fraction_of_step": round(ar_ms / (elapsed / args.steps * 1e3), 3),
-                     "algbw_GBps": round(ar_events[0][2] / (ar_ms * 1e-3) / 1e9, 1)}
+        n_c = min(args.steps, 10)
+        dist.barrier()
+        tc0 = time.perf_counter()
+        for _ in range(n_c):
+            step(comm=False)
+        torch.cuda.synchronize()
+        dist.barrier()
+        compute_ms = multiview.max_over_ranks((time.perf_counter() - tc0) / n_c, dev) * 1e3
+        step_ms = elapsed / args.steps * 1e3
+        allreduce = {"ms_standalone": round(ar_ms, 4), "bytes_per_rank": ar_events[0][2],
+                     "algbw_GBps": round(ar_events[0][2] / (ar_ms * 1e-3) / 1e9, 1),
+                     "overlapped": overlap_ar, "chunks": args.allreduce_chunks if overlap_ar else 1,
+                     "compute_only_ms_per_step": round(compute_ms, 4),
+                     "exposed_ms": round(max(step_ms - compute_ms, 0.0), 4),
+                     "fraction_of_step": round(max(step_ms - compute_ms, 0.0) / step_ms, 3),
+                     "standalone_fraction_of_step": round(ar_ms / step_ms, 3)}
 
     # geometry of the workload (one extra forward per view outside the timed region)
     with torch.no_grad():
@@ -502,7 +530,9 @@ def main():
     if mode == "strong":
         workload = (f"BASELINE config 4: {args.views_total} views per step of config 2 ({P} Gaussians, SH deg 3, "
                     f"{W}x{H}, fwd+bwd each), view v on rank v mod {world}"
-                    + (", one RCCL grad all-reduce per step" if world > 1 else ", grads accumulated on one GPU"))
+                    + ((", one RCCL grad all-reduce per step" + (f" overlapped with the backward ({args.allreduce_chunks} "
+                                                                  "Gaussian ranges)" if overlap_ar else ""))
+                       if world > 1 else ", grads accumulated on one GPU"))
     else:
         workload = (f"{args.views_per_rank} views per rank per step of config 2 ({P} Gaussians, SH deg 3, {W}x{H}, "
                     f"fwd+bwd each)" + (", one RCCL grad all-reduce per step" if world > 1 else ""))

@@ -1046,7 +1046,29 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
                                   float* dL_dscale, float* dL_drot, bool antialiasing, bool debug,
                                   unsigned accumulate, gsr_stream_t stream)
 {
+    return gsr_backward_preprocess_views_range(V, P, D, M, R, width, height, means3D, dc, shs, colors_precomp,
+                                               opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                               viewmatrices, projmatrices, campos, tan_fovx, tan_fovy, radii,
+                                               geom_buffers, binning_buffers, has_invdepth, dL_dmean2D, dL_dcolor,
+                                               dL_dopacity, dL_dmean3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot,
+                                               antialiasing, debug, accumulate, 0, P, stream);
+}
+
+int gsr_backward_preprocess_views_range(int V, int P, int D, int M, const int* R, int width, int height,
+                                        const float* means3D, const float* dc, const float* shs,
+                                        const float* colors_precomp, const float* opacities, const float* scales,
+                                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                        const float* const* viewmatrices, const float* const* projmatrices,
+                                        const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                        const int* const* radii, char* const* geom_buffers,
+                                        char* const* binning_buffers, bool has_invdepth, float* const* dL_dmean2D,
+                                        float* dL_dcolor, float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D,
+                                        float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                                        bool antialiasing, bool debug, unsigned accumulate, int g_begin, int g_end,
+                                        gsr_stream_t stream)
+{
     if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
+    if (g_begin < 0 || g_end > P || g_begin > g_end) return fail(GSR_ERR_INVALID, "range outside [0, P)");
     if (accumulate & ~(unsigned)GSR_ACC_ALL) return fail(GSR_ERR_INVALID, "unknown accumulate bits");
     if (dc && !dL_ddc) return fail(GSR_ERR_INVALID, "dc given without dL_ddc");
     if (dc && colors_precomp)
@@ -1081,6 +1103,8 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
     p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;
     p.acc = accumulate;
     A.V = V;
+    A.g_begin = g_begin;
+    A.g_end = g_end;
     for (int v = 0; v < V; v++) {
         char* gb = geom_buffers[v];
         char* bb = binning_buffers[v];
@@ -1114,17 +1138,10 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
     return GSR_OK;
 }
 
-int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
-                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
-                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
-                       const float* cov3D_precomp, const float* const* viewmatrices,
-                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
-                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
-                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
-                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
-                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
-                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
-                       gsr_stream_t stream)
+int gsr_backward_render_views(int V, int P, const int* R, const float* background, int width, int height,
+                              char* const* geom_buffers, char* const* binning_buffers, char* const* image_buffers,
+                              const float* const* dL_dpix, const float* const* dL_invdepths, bool debug,
+                              gsr_stream_t stream)
 {
     if (V < 1 || V > MAX_VIEWS) return fail(GSR_ERR_INVALID, "V must be in [1, 16]");
     if (!R || !geom_buffers || !binning_buffers || !image_buffers || !dL_dpix)
@@ -1142,10 +1159,6 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
             oj[no++] = {nullptr, at<uint32_t>(image_buffers[v], im.off[IMG_TILE_WORK]),
                         at<uint32_t>(image_buffers[v], im.off[IMG_TILE_ORDER])};
     }
-    if (no) {
-        ProfScope ps_(PK_TILE_ORDER, (hipStream_t)stream);
-        HIP_TRY(launch_tile_order_batch(oj, no, T, (hipStream_t)stream));
-    }
     // BACKWARD::render of every view (its per-(tile, Gaussian) records), one launch per batch
     RenderBwdArgs ra[MAX_VIEWS];
     int nr = 0;
@@ -1157,17 +1170,39 @@ int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* ba
         ra[nr++] = render_bwd_args(P, R[v], background, width, height, geom_buffers[v], binning_buffers[v],
                                    image_buffers[v], dL_dpix[v], has_inv ? dL_invdepths[v] : nullptr);
     }
+    if (no) {
+        ProfScope ps_(PK_TILE_ORDER, (hipStream_t)stream);
+        HIP_TRY(launch_tile_order_batch(oj, no, T, (hipStream_t)stream));
+    }
     if (nr) {
         ProfScope ps_(PK_RENDER_BWD, (hipStream_t)stream);  // valid[] was cleared by the forward
         HIP_TRY(launch_render_bwd_batch(ra, nr, T, (hipStream_t)stream));
     }
     DEBUG_SYNC((hipStream_t)stream);
+    return GSR_OK;
+}
+
+int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
+                       const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
+                       const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                       const float* cov3D_precomp, const float* const* viewmatrices,
+                       const float* const* projmatrices, const float* const* campos, const float* tan_fovx,
+                       const float* tan_fovy, const int* const* radii, char* const* geom_buffers,
+                       char* const* binning_buffers, char* const* image_buffers, const float* const* dL_dpix,
+                       const float* const* dL_invdepths, float* const* dL_dmean2D, float* dL_dcolor,
+                       float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
+                       float* dL_dscale, float* dL_drot, bool antialiasing, bool debug, unsigned accumulate,
+                       gsr_stream_t stream)
+{
+    const int rc = gsr_backward_render_views(V, P, R, background, width, height, geom_buffers, binning_buffers,
+                                             image_buffers, dL_dpix, dL_invdepths, debug, stream);
+    if (rc || P <= 0) return rc;
     return gsr_backward_preprocess_views(V, P, D, M, R, width, height, means3D, dc, shs, colors_precomp, opacities,
                                          scales, scale_modifier, rotations, cov3D_precomp, viewmatrices,
                                          projmatrices, campos, tan_fovx, tan_fovy, radii, geom_buffers,
-                                         binning_buffers, has_inv, dL_dmean2D, dL_dcolor, dL_dopacity, dL_dmean3D,
-                                         dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot, antialiasing, debug,
-                                         accumulate, stream);
+                                         binning_buffers, dL_invdepths != nullptr, dL_dmean2D, dL_dcolor,
+                                         dL_dopacity, dL_dmean3D, dL_dcov3D, dL_ddc, dL_dsh, dL_dscale, dL_drot,
+                                         antialiasing, debug, accumulate, stream);
 }
 
 // ---- the non-dc entry points: the reference's Rasterizer API (rasterizer.h:31-90) ----

@@ -156,6 +156,7 @@ struct BwdView {
 struct PreprocessBwdViewsArgs {
     PreprocessBwdArgs a;
     int V;  // 0: the single view of `a`
+    int g_begin, g_end;  // the Gaussians [g_begin, g_end) of this launch (a chunk of [0, P))
     BwdView v[MAX_VIEWS];
 };
 

@@ -876,9 +876,11 @@ __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const Preproc
     extern __shared__ __attribute__((aligned(16))) float s_sh[];
     const PreprocessBwdArgs& a = A.a;
     const int gl = (int)threadIdx.x / LPG, v = (int)threadIdx.x % LPG;
-    const int base = blockIdx.x * G;
-    const bool live = base + gl < a.P;
-    const int idx = live ? base + gl : a.P - 1;  // clamped: all lanes take part in the reductions
+    // the launch covers Gaussians [g_begin, g_end) (a chunk of the batch: gradient reduction
+    // overlapped with the later chunks)
+    const int base = A.g_begin + (int)blockIdx.x * G;
+    const bool live = base + gl < A.g_end;
+    const int idx = live ? base + gl : A.g_end - 1;  // clamped: all lanes take part in the reductions
     __shared__ float s_cam[MAX_VIEWS][CAM_FLOATS];
     BwdIn in;
     bwd_gather(a, idx, in, false);
@@ -897,7 +899,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const Preproc
             for (int k = (a.shs ? 48 : 0) + v; k < a.M * 3; k += LPG) a.dL_dsh[idx * w3 + k] = 0.f;
         return;
     }
-    staged_sh<G>(a, s_sh, base, min(G, a.P - base), gl, [&](float* c0, float* cr, int kw) {
+    staged_sh<G>(a, s_sh, base, min(G, A.g_end - base), gl, [&](float* c0, float* cr, int kw) {
         bwd_views_group<LPG>(A, idx, live, v, in, vi, cam, c0, cr, c0, cr, kw, false, false);
     });
 }
@@ -924,7 +926,7 @@ template <int LPG>
 static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
     constexpr int G = 256 / LPG;
-    const dim3 grid((A.a.P + G - 1) / G), block(256);
+    const dim3 grid((A.g_end - A.g_begin + G - 1) / G), block(256);
     if (staged_layout(A.a))
         hipLaunchKernelGGL((preprocess_bwd_views_kernel<LPG, true>), grid, block, staged_lds_bytes(G), s, A);
     else
@@ -935,7 +937,8 @@ static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
     if (A.V < 1 || A.V > MAX_VIEWS) return hipErrorInvalidValue;
-    if (A.a.P <= 0) return hipSuccess;
+    if (A.g_begin < 0 || A.g_end > A.a.P || A.g_begin > A.g_end) return hipErrorInvalidValue;
+    if (A.a.P <= 0 || A.g_end == A.g_begin) return hipSuccess;
     if (A.V <= 2) return launch_views<2>(A, s);
     if (A.V <= 4) return launch_views<4>(A, s);
     if (A.V <= 8) return launch_views<8>(A, s);

@@ -55,6 +55,8 @@ def _load():
     lib.gsr_backward_preprocess_views.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f,
                                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _vp, _vp,
                                                   _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _b, ctypes.c_uint, _vp]
+    lib.gsr_backward_preprocess_views_range.argtypes = lib.gsr_backward_preprocess_views.argtypes[:-1] + [_i, _i, _vp]
+    lib.gsr_backward_render_views.argtypes = [_i, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _b, _vp]
     lib.gsr_forward_views.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp, _vp,
                                       _vp, _vp, _vp, _vp, _b, _b, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _b, _vp, _vp,
                                       _vp]
@@ -434,15 +436,43 @@ def _views_result(dL_dmeans2D, r, acc, has_dc):
             r["scales"], r["rotations"])
 
 
+def _preprocess_views_chunks(on_chunk, V, P, degree, M, Rs, W, H, means_p, dc_p, sh_p, colors_p, op_p, sc_p,
+                             scale_modifier, rot_p, cov_p, views, projs, cams, tan_fovx, tan_fovy, radii, geomBuffers,
+                             binningBuffers, has_inv, dL_dmeans2D, r, has_dc, antialiasing, debug, mask, acc, dev):
+    """gsr_backward_preprocess_views_range over `chunks` Gaussian ranges (multiples of 256, the
+    batched kernel's workgroup width), fn(g0, g1, grads) after each."""
+    chunks, fn = on_chunk
+    step = max(256, -(-P // max(1, int(chunks)) // 256) * 256)
+    grads = {k: t for k, t in r.items() if t is not None}
+    for g0 in range(0, P, step):
+        g1 = min(P, g0 + step)
+        _check(lib.gsr_backward_preprocess_views_range(
+            V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), int(W), int(H), means_p, dc_p, sh_p, colors_p,
+            op_p, sc_p, float(scale_modifier), rot_p, cov_p, _ptr_array(views), _ptr_array(projs), _ptr_array(cams),
+            (_f * V)(*[float(x) for x in tan_fovx]), (_f * V)(*[float(x) for x in tan_fovy]), _ptr_array(radii),
+            _ptr_array(geomBuffers), _ptr_array([b if b.numel() else None for b in binningBuffers]), bool(has_inv),
+            _ptr_array([dL_dmeans2D[v] for v in range(V)]), r["colors_precomp"].data_ptr(),
+            r["opacities"].data_ptr(), r["means3D"].data_ptr(), r["cov3D_precomp"].data_ptr(),
+            r["dc"].data_ptr() if has_dc else None, r["sh"].data_ptr() if M else None, r["scales"].data_ptr(),
+            r["rotations"].data_ptr(), bool(antialiasing), bool(debug), mask, g0, g1, _stream(dev)))
+        fn(g0, g1, grads)
+
+
 def rasterize_gaussians_backward_views(background, means3D, radii, colors, opacities, scales, rotations,
                                        scale_modifier, cov3D_precomp, viewmatrices, projmatrices, tan_fovx, tan_fovy,
                                        dL_dout_colors, dL_dout_invdepths, sh, degree, campos, geomBuffers, Rs,
-                                       binningBuffers, imageBuffers, antialiasing, debug, dc=None, accumulate=None):
+                                       binningBuffers, imageBuffers, antialiasing, debug, dc=None, accumulate=None,
+                                       on_chunk=None):
     """Backward of a batch of V views (gsr_backward_views): per-view lists of the forward's state
     (radii (P,), camera, buffers, num_rendered) and dL_dout_colors (V,3,H,W), dL_dout_invdepths
     (V,1,H,W) or None.  Returns (dL_dmeans2D (V,P,3), dL_dcolors, dL_dopacity, dL_dmeans3D,
     dL_dcov3D, [dL_ddc,] dL_dsh, dL_dscales, dL_drotations): the screen-space gradient per view,
-    everything else summed over the views; `accumulate` as in rasterize_gaussians_backward."""
+    everything else summed over the views; `accumulate` as in rasterize_gaussians_backward.
+    on_chunk = (chunks, fn): the BACKWARD::preprocess runs as `chunks` launches over Gaussian ranges
+    (gsr_backward_render_views, then gsr_backward_preprocess_views_range per range) and fn(g0, g1,
+    grads) is called after each launch is enqueued, grads = {input name: its gradient tensor (P,...)}
+    (the caller's accumulate targets or the fresh buffers): rows [g0, g1) are final from then on in
+    stream order (multiview.overlapped_allreduce)."""
     _require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
@@ -474,6 +504,18 @@ def rasterize_gaussians_backward_views(background, means3D, radii, colors, opaci
     dpix = [dL_dout_colors[v].contiguous() for v in range(V)]
     dinv = [dL_dout_invdepths[v].contiguous() for v in range(V)] if has_inv else None
     keep.extend(dpix)
+    if on_chunk is not None:
+        _check(lib.gsr_backward_render_views(
+            V, P, (_i * V)(*[int(x) for x in Rs]), p(background, "bg"), W, H, _ptr_array(geomBuffers),
+            _ptr_array([b if b.numel() else None for b in binningBuffers]), _ptr_array(imageBuffers),
+            _ptr_array(dpix), _ptr_array(dinv) if has_inv else None, bool(debug), _stream(dev)))
+        _preprocess_views_chunks(on_chunk, V, P, degree, M, Rs, W, H, p(means3D, "means3D"),
+                                 p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"),
+                                 p(opacities, "opacities"), p(scales, "scales"), scale_modifier,
+                                 p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp"), views, projs, cams,
+                                 tan_fovx, tan_fovy, radii, geomBuffers, binningBuffers, has_inv, dL_dmeans2D, r,
+                                 has_dc, antialiasing, debug, mask, acc, dev)
+        return _views_result(dL_dmeans2D, r, acc, has_dc)
     _check(lib.gsr_backward_views(
         V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), p(background, "bg"), W, H, p(means3D, "means3D"),
         p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"), p(opacities, "opacities"),
@@ -508,9 +550,10 @@ def rasterize_gaussians_preprocess_backward_views(means3D, radii, colors, opacit
                                                   scale_modifier, cov3D_precomp, viewmatrices, projmatrices,
                                                   tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
                                                   geomBuffers, Rs, binningBuffers, has_invdepth, antialiasing, debug,
-                                                  dc=None, accumulate=None):
+                                                  dc=None, accumulate=None, on_chunk=None):
     """BACKWARD::preprocess of V views whose render backward already ran
-    (gsr_backward_preprocess_views); returns what rasterize_gaussians_backward_views returns."""
+    (gsr_backward_preprocess_views); returns what rasterize_gaussians_backward_views returns;
+    on_chunk as there."""
     _require_gpu(means3D)
     dev = means3D.device
     P = means3D.size(0)
@@ -533,6 +576,14 @@ def rasterize_gaussians_preprocess_backward_views(means3D, radii, colors, opacit
         return out
 
     views, projs, cams = cont(viewmatrices, "viewmatrix"), cont(projmatrices, "projmatrix"), cont(campos, "campos")
+    if on_chunk is not None:
+        _preprocess_views_chunks(on_chunk, V, P, degree, M, Rs, image_width, image_height, p(means3D, "means3D"),
+                                 p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"),
+                                 p(opacities, "opacities"), p(scales, "scales"), scale_modifier,
+                                 p(rotations, "rotations"), p(cov3D_precomp, "cov3D_precomp"), views, projs, cams,
+                                 tan_fovx, tan_fovy, radii, geomBuffers, binningBuffers, has_invdepth, dL_dmeans2D, r,
+                                 has_dc, antialiasing, debug, mask, acc, dev)
+        return _views_result(dL_dmeans2D, r, acc, has_dc)
     _check(lib.gsr_backward_preprocess_views(
         V, P, int(degree), M, (_i * V)(*[int(x) for x in Rs]), int(image_width), int(image_height),
         p(means3D, "means3D"), p(dc, "dc") if has_dc else None, p(sh, "sh"), p(colors, "colors_precomp"),

@@ -21,7 +21,8 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "SparseGaussianAdam",
-           "accumulate_grads_in_place", "deferred_backward", "MultiViewRasterizer", "rasterize_views"]
+           "accumulate_grads_in_place", "deferred_backward", "MultiViewRasterizer", "rasterize_views",
+           "grad_chunk_hook"]
 
 _state = threading.local()
 
@@ -44,6 +45,34 @@ def accumulate_grads_in_place(enabled=True):
         yield
     finally:
         _state.accumulate = prev
+
+
+@contextlib.contextmanager
+def grad_chunk_hook(chunks, fn, done):
+    """Batched backward passes (MultiViewRasterizer, deferred_backward's flush) run inside this
+    context split their BACKWARD::preprocess into `chunks` launches over Gaussian ranges and call
+    fn(g0, g1, grads) after each (grads: {input name: the gradient tensor that input receives},
+    rows [g0, g1) final in stream order), then done() before the backward returns -- the hook
+    multiview.overlapped_allreduce uses to reduce each range while the next one computes."""
+    prev = getattr(_state, "grad_chunks", None)
+    _state.grad_chunks = (int(chunks), fn, done)
+    try:
+        yield
+    finally:
+        _state.grad_chunks = prev
+
+
+def _chunk_hook(wanted):
+    """(on_chunk for _C, done) from the active grad_chunk_hook, restricted to the gradients of the
+    inputs in `wanted` (names); (None, None) outside the context."""
+    h = getattr(_state, "grad_chunks", None)
+    if h is None or not wanted:
+        return None, None
+    chunks, fn, done = h
+
+    def on(g0, g1, grads):
+        fn(g0, g1, {k: t for k, t in grads.items() if k in wanted and t.numel()})
+    return (chunks, on), done
 
 
 # Per device: an event recorded after the last backward run inside accumulate_grads_in_place.
@@ -122,13 +151,17 @@ class _DeferredBatch:
             stream.wait_event(fence)
         for g in accumulate.values():
             g.record_stream(stream)
+        on_chunk, done = _chunk_hook({k for k, t in inputs.items()
+                                      if t is not None and t.numel() and t.requires_grad})
         grads = _C.rasterize_gaussians_preprocess_backward_views(
             means3D, [v["radii"] for v in views], colors_precomp, opacities, scales, rotations, s0.scale_modifier,
             cov3Ds_precomp, [v["settings"].viewmatrix for v in views], [v["settings"].projmatrix for v in views],
             [v["settings"].tanfovx for v in views], [v["settings"].tanfovy for v in views], s0.image_height,
             s0.image_width, sh, s0.sh_degree, [v["settings"].campos for v in views], [v["geom"] for v in views],
             [v["num_rendered"] for v in views], [v["binning"] for v in views], any(v["has_inv"] for v in views),
-            s0.antialiasing, s0.debug, dc=dc, accumulate=accumulate)
+            s0.antialiasing, s0.debug, dc=dc, accumulate=accumulate, on_chunk=on_chunk)
+        if done is not None:
+            done()
         ev = torch.cuda.Event()
         ev.record(stream)
         _acc_fence[dev] = ev
@@ -426,12 +459,19 @@ class _RasterizeViews(torch.autograd.Function):
                 stream.wait_event(fence)
             for g in accumulate.values():
                 g.record_stream(stream)
+        # inputs of forward(): means3D 0, sh 2, colors_precomp 3, opacities 4, scales 5, rotations 6,
+        # cov3D_precomp 7, dc 9
+        names = {0: "means3D", 2: "sh", 3: "colors_precomp", 4: "opacities", 5: "scales", 6: "rotations",
+                 7: "cov3D_precomp", 9: "dc"}
+        on_chunk, done = _chunk_hook({n for i, n in names.items() if ctx.needs_input_grad[i]})
         grads = _C.rasterize_gaussians_backward_views(
             s0.bg, means3D, [radii[v] for v in range(V)], colors_precomp, opacities, scales, rotations,
             s0.scale_modifier, cov3Ds_precomp, [s.viewmatrix for s in ss], [s.projmatrix for s in ss],
             [s.tanfovx for s in ss], [s.tanfovy for s in ss], grad_colors, grad_invdepths, sh, s0.sh_degree,
             [s.campos for s in ss], bufs[0::3], ctx.num_rendered, bufs[1::3], bufs[2::3], s0.antialiasing, s0.debug,
-            dc=dc, accumulate=accumulate)
+            dc=dc, accumulate=accumulate, on_chunk=on_chunk)
+        if done is not None:
+            done()
         if ctx.acc_inputs is not None:
             ev = torch.cuda.Event()
             ev.record(stream)

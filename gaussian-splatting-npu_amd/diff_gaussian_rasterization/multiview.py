@@ -10,6 +10,8 @@ this is the multi-view form of that step, the only exchange the path has.
 
 Backend-agnostic: "nccl" (RCCL over xGMI) on the GPU box, "gloo" in the CPU tests.
 """
+import contextlib
+
 import torch
 import torch.distributed as dist
 
@@ -79,6 +81,43 @@ def allreduce_grads(params, order=PARAM_ORDER, group=None):
         g.copy_(flat[off:off + n].view_as(g))
         off += n
     return flat.numel() * flat.element_size()
+
+
+@contextlib.contextmanager
+def overlapped_allreduce(group=None, chunks=4):
+    """The gradient all-reduce overlapped with the backward ("overlap it with the last
+    view's backward"): batched backward passes run inside this context (MultiViewRasterizer, the
+    flush of deferred_backward) compute their parameter gradients in `chunks` Gaussian ranges, and
+    each range's rows of every parameter gradient go to an asynchronous all_reduce(SUM) as soon as
+    its launch is enqueued -- the collective of range k runs while range k+1 computes.  The backward
+    waits for its collectives before it returns, so the gradients it hands to autograd are already
+    the sums over the ranks; the caller then skips allreduce_grads.  Chunks over [0, P) write
+    exactly the rows one full launch writes, so the reduced gradients equal allreduce_grads after an
+    unchunked backward bit for bit (for leaf inputs; activations between the parameters and the
+    rasterizer are back-propagated from the reduced gradients afterwards).  Only for the one batched
+    backward of a step: each backward inside reduces what its inputs' gradients hold then.  Yields
+    a dict counting the collectives issued; a no-op (yields None) without a process group of more
+    than one rank."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        yield None
+        return
+    import diff_gaussian_rasterization as dgr
+    works, stats = [], {"collectives": 0, "chunks": 0, "bytes": 0}
+
+    def fn(g0, g1, grads):
+        stats["chunks"] += 1
+        for t in grads.values():
+            part = t[g0:g1]
+            works.append(dist.all_reduce(part, op=dist.ReduceOp.SUM, group=group, async_op=True))
+            stats["collectives"] += 1
+            stats["bytes"] += part.numel() * part.element_size()
+
+    def done():
+        for w in works:
+            w.wait()
+        works.clear()
+    with dgr.grad_chunk_hook(chunks, fn, done):
+        yield stats
 
 
 def densification_stats(P, device=None):

@@ -294,6 +294,28 @@ int gsr_backward_preprocess_views(int V, int P, int D, int M, const int* R, int 
                                   float* dL_dmean3D, float* dL_dcov3D, float* dL_ddc, float* dL_dsh,
                                   float* dL_dscale, float* dL_drot, bool antialiasing, bool debug,
                                   unsigned accumulate, gsr_stream_t stream);
+/* gsr_backward_render_views: the BACKWARD::render half of gsr_backward_views for all V views (one
+ * tile-order launch and one render launch per batch).  gsr_backward_preprocess_views_range: the
+ * BACKWARD::preprocess half restricted to the Gaussians [g_begin, g_end) -- only their rows of the
+ * parameter gradients (and of each view's dL_dmean2D) are written, so a caller can hand finished
+ * row ranges to a gradient all-reduce while the next range computes (the collective
+ * overlapped with the backward).  Chunks covering [0, P) equal one full call bit for bit. */
+int gsr_backward_render_views(int V, int P, const int* R, const float* background, int width, int height,
+                              char* const* geom_buffers, char* const* binning_buffers, char* const* image_buffers,
+                              const float* const* dL_dpix, const float* const* dL_invdepths, bool debug,
+                              gsr_stream_t stream);
+int gsr_backward_preprocess_views_range(int V, int P, int D, int M, const int* R, int width, int height,
+                                        const float* means3D, const float* dc, const float* shs,
+                                        const float* colors_precomp, const float* opacities, const float* scales,
+                                        float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                                        const float* const* viewmatrices, const float* const* projmatrices,
+                                        const float* const* campos, const float* tan_fovx, const float* tan_fovy,
+                                        const int* const* radii, char* const* geom_buffers,
+                                        char* const* binning_buffers, bool has_invdepth, float* const* dL_dmean2D,
+                                        float* dL_dcolor, float* dL_dopacity, float* dL_dmean3D, float* dL_dcov3D,
+                                        float* dL_ddc, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                                        bool antialiasing, bool debug, unsigned accumulate, int g_begin, int g_end,
+                                        gsr_stream_t stream);
 
 /* Forward of a batch of V <= 16 camera views of the same Gaussians (the forward half of
  * gsr_backward_views; each view the result of gsr_forward_prealloc_dc with its own state buffers).

@@ -47,8 +47,10 @@ def _settings(case, antialiasing):
 # beyond the common GRAD_RTOL.  The outliers are Gaussians blended into one of the few flipped
 # pixels (an alpha within an ulp of 1/255 or of the stop rule; common.check_render): their
 # gradient gains or loses that pixel's term.  Measured at this size: 8 elements of dL/dmean2D
-# (3M) beyond 1e-5 of max, the largest at 1.2e-4.
-GRAD_RTOL_FLIP = 5e-4
+# (3M) beyond 1e-5 of max, the largest at 1.2e-4 (view 0); over the 16 views of the bench step
+# (tests/test_bench_step_parity.py, AA off and on) the largest is 8.3e-4 (view 4, AA on, whose
+# flipped pixels are off by up to 1.1e-3).  The bulk is bounded per element by common.check_rel.
+GRAD_RTOL_FLIP = 2e-3
 GRAD_OUTLIERS = 64
 
 

@@ -9,6 +9,7 @@ the same views and sums the two ranks' gradient buffers itself (x0 + x1: a two-r
 each element once, and float addition commutes), and the reduced densification statistics must
 equal the single process's.
 """
+import contextlib
 import os
 import socket
 
@@ -295,3 +296,92 @@ def test_two_ranks_densify_and_reset_match_single_process():
             np.testing.assert_array_equal(params[k], emu.params[k].detach().cpu().numpy(), err_msg=f"rank {rank} {k}")
             np.testing.assert_array_equal(moments[k], emu.optimizer.state[emu.params[k]]["exp_avg"].cpu().numpy(),
                                           err_msg=f"rank {rank} exp_avg {k}")
+
+
+# ---- the gradient all-reduce overlapped with the batched backward ---------
+O_P, O_H, O_W, O_VIEWS = 4000, 144, 176, 4
+
+
+def _oworker(rank, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "gaussian-splatting-npu_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        import synthetic
+        import diff_gaussian_rasterization as dgr
+        from diff_gaussian_rasterization import multiview
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        scene = synthetic.make_scene(O_P, seed=0)
+        mine = multiview.views_of_batch(rank, WORLD, O_VIEWS)
+        settings, grads = [], []
+        for v in mine:
+            c = synthetic.Camera(O_W, O_H, view=v)
+            settings.append(dgr.GaussianRasterizationSettings(
+                O_H, O_W, c.tanfovx, c.tanfovy, torch.zeros(3, device=dev), 1.0, c.world_view_transform.to(dev),
+                c.full_proj_transform.to(dev), 3, c.camera_center.to(dev), False, False, False))
+            grads.append(tuple(g.to(dev) for g in synthetic.make_grads(O_H, O_W, seed=1 + v)))
+        out = {}
+        for mode in ("plain", "overlap", "deferred_overlap"):
+            params = {k: v.to(dev).clone().requires_grad_(True) for k, v in scene.items()}
+            ctx = multiview.overlapped_allreduce(chunks=3) if mode != "plain" else contextlib.nullcontext()
+            with ctx as st:
+                if mode == "deferred_overlap":
+                    with dgr.deferred_backward():
+                        for s, (gc, gi) in zip(settings, grads):
+                            m2 = torch.zeros_like(params["means3D"], requires_grad=True)
+                            c, _, i = dgr.GaussianRasterizer(s)(means2D=m2, **{
+                                "means3D": params["means3D"], "shs": params["shs"], "opacities": params["opacities"],
+                                "scales": params["scales"], "rotations": params["rotations"]})
+                            torch.autograd.backward([c, i], [gc, gi])
+                else:
+                    m2 = torch.zeros((len(settings), O_P, 3), device=dev, requires_grad=True)
+                    c, _, i = dgr.MultiViewRasterizer(settings)(
+                        means3D=params["means3D"], means2D=m2, shs=params["shs"], opacities=params["opacities"],
+                        scales=params["scales"], rotations=params["rotations"])
+                    torch.autograd.backward([c, i], [torch.stack([g[0] for g in grads]),
+                                                     torch.stack([g[1] for g in grads])])
+            if mode == "plain":
+                multiview.allreduce_grads(params)
+            else:
+                assert st["chunks"] == 3 and st["collectives"] == 15, st
+            torch.cuda.synchronize()
+            out[mode] = {k: p.grad.cpu().numpy() for k, p in params.items()}
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_equals_allreduce_after_backward():
+    """multiview.overlapped_allreduce (the batched BACKWARD::preprocess in 3 Gaussian ranges, each
+    range's gradient rows all-reduced while the next computes) against the unchunked backward
+    followed by allreduce_grads: bitwise equal, on 2 gloo ranks, for a MultiViewRasterizer batch
+    and for deferred_backward's flush; and equal on both ranks."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_oworker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    ref = res[0][1]["plain"]
+    for rank, out in res:
+        for mode in ("plain", "overlap"):
+            for k in ref:
+                np.testing.assert_array_equal(out[mode][k], ref[k], err_msg=f"rank {rank} {mode} {k}")
+        # the deferred flush sums the same views with the same kernel: bitwise too
+        for k in ref:
+            np.testing.assert_array_equal(out["deferred_overlap"][k], res[0][1]["deferred_overlap"][k],
+                                          err_msg=f"rank {rank} deferred {k}")
+            ok = np.abs(out["deferred_overlap"][k] - ref[k]).max() <= 1e-5 * np.abs(ref[k]).max() + 1e-9
+            assert ok, f"rank {rank} deferred vs batch {k}"

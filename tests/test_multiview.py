@@ -316,3 +316,44 @@ def test_expon_lr_matches_reference_formula():
     assert f(-1) == 0.0 and math.isclose(f(1000), 1e-4)
     d = multiview.expon_lr(1.0, 1.0, lr_delay_steps=10, lr_delay_mult=0.01)
     assert math.isclose(d(0), 0.01) and math.isclose(d(10), 1.0) and 0.01 < d(5) < 1.0
+
+
+def _overlap_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import diff_gaussian_rasterization as dgr
+        P, M = 1000, 15
+        mine = _fake_params(P, M, rank)
+        want = {k: t.grad.clone() for k, t in mine.items()}
+        for t in want.values():
+            dist.all_reduce(t)
+        grads = {k: t.grad for k, t in mine.items()}
+        with multiview.overlapped_allreduce(chunks=3) as st:
+            chunks, fn, done = dgr._state.grad_chunks  # what a batched backward calls
+            step = 384
+            for g0 in range(0, P, step):
+                fn(g0, min(P, g0 + step), grads)
+            done()
+        q.put((rank, all(torch.equal(grads[k], want[k]) for k in want), dict(st)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_overlapped_allreduce_chunks_sum_like_one_allreduce():
+    """overlapped_allreduce's hook (what MultiViewRasterizer's backward calls per Gaussian range)
+    reduces each range's rows of every gradient: together equal to one all_reduce per tensor, on
+    gloo world 2 (CPU)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, st in res:
+        assert ok, rank
+        assert st == {"collectives": 15, "chunks": 3, "bytes": 4 * 1000 * (3 + 45 + 1 + 3 + 4)}, st

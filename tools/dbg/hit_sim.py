@@ -37,6 +37,29 @@ def main(path):
     for B, s in res.items():
         print(f"B={B:4d}: slots {s}  idle {1 - useful / s:.3f}")
     print(f"per-tile bound: slots {lb}  idle {1 - useful / lb:.3f}")
+    # launch tail: per-tile cost (iterations of the current B=64 scheme + a per-batch and per-tile
+    # overhead, in iteration units), list-scheduled longest-first on S wave slots
+    import heapq
+    costs = []
+    for (a, _), w in zip(ranges, work):
+        if w <= 0:
+            costs.append(2.0)
+            continue
+        starts = np.arange(0, w, 64)
+        ends = np.minimum(starts + 64, w)
+        cnt = cs[a + ends] - cs[a + starts]
+        costs.append(float(cnt.max(1).sum()) + 4.0 * len(starts) + 8.0)
+    costs = np.array(costs)
+    print(f"tiles {len(costs)}  cost mean {costs.mean():.1f}  max {costs.max():.1f}  p99 {np.quantile(costs, .99):.1f}")
+    for views in (1, 8):
+        for S in (4096,):
+            c = np.sort(np.tile(costs, views))[::-1]
+            heap = [0.0] * S
+            for x in c:
+                t = heapq.heappop(heap)
+                heapq.heappush(heap, t + x)
+            ms = max(heap)
+            print(f"views {views} slots {S}: makespan / ideal = {ms / (c.sum() / S):.3f} (max tile / ideal {c[0] / (c.sum() / S):.3f})")
 
 
 if __name__ == "__main__":

@@ -38,6 +38,7 @@ PY
            ;;
     hits) run hits 200 python -u tools/dbg/hit_dump.py ;;
     pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
+    dist) run dist 400 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
