@@ -792,29 +792,31 @@ def aux_ssim(H, W, dev, args, reps=20):
 
 
 def cpu_baseline(args, scene, s, grad):
-    """The CPU oracle (oracle/gsr_oracle.c, OpenMP) on the bench's first view: one
+    """The CPU restatement behind the product's own C ABI (oracle/libgsr_cpu.so: gsr_forward with
+    resize callbacks, then gsr_backward on the state buffers -- the host calling sequence of the
+    HIP library; the oracle's OpenMP code underneath) on the bench's first view: one
     forward+backward per run, --cpu-reps runs, the median reported."""
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle
+        import cpu_abi
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         gc, gi = grad
         gc, gi = gc.cpu(), gi.cpu()
+        cpu = cpu_abi.CpuRasterizer(nthreads=threads)
         times = []
         for _ in range(max(1, args.cpu_reps)):
             t = time.perf_counter()
-            o = oracle.OracleRaster(scene["means3D"], scene["opacities"], s.bg.cpu(), s.viewmatrix.cpu(),
-                                    s.projmatrix.cpu(), s.campos.cpu(), s.tanfovx, s.tanfovy, s.image_height,
-                                    s.image_width, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
-                                    rotations=scene["rotations"], antialiasing=args.antialiasing, nthreads=threads)
-            o.backward(gc, gi)
+            cpu.forward_backward(scene["means3D"], scene["opacities"], s.bg.cpu(), s.viewmatrix.cpu(),
+                                 s.projmatrix.cpu(), s.campos.cpu(), s.tanfovx, s.tanfovy, s.image_height,
+                                 s.image_width, gc, gi, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
+                                 rotations=scene["rotations"], antialiasing=args.antialiasing)
             times.append(time.perf_counter() - t)
-            del o
         dt = statistics.median(times)
         return {"value": round(s.image_height * s.image_width / dt / 1e6, 3), "unit": "Mpix/s", "cores": threads,
                 "kind": "port", "seconds": round(dt, 3), "runs_s": [round(x, 3) for x in times],
                 "sample": f"one full fwd+bwd of one bench view ({args.P} Gaussians, {s.image_width}x"
-                          f"{s.image_height}) by the C/OpenMP oracle, median of {len(times)} runs"}
+                          f"{s.image_height}) by the C/OpenMP restatement through gsr_forward/gsr_backward "
+                          f"(oracle/libgsr_cpu.so), median of {len(times)} runs"}
     except Exception as e:  # the baseline must never take the GPU result down
         return {"value": None, "unit": "Mpix/s", "cores": 0, "kind": "port", "sample": f"failed: {e}"}
 

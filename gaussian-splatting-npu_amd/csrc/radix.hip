@@ -14,7 +14,7 @@
 // Gaussian index) -- the reference's order -- and the sorted key array
 // (tile << 32 | depth bits) is bit-identical to the reference's.
 //
-// One pass = three kernels, no inter-workgroup waiting: (1) every 4096-element chunk counts
+// One pass = three kernels, no inter-workgroup waiting: (1) every 2048-element chunk counts
 // its digits (digit-major count matrix); (2) one workgroup per digit scans that digit's row
 // over the chunks; (3) every chunk ranks its elements stably per digit (wave-level ballot
 // match + per-wave running counters in LDS), adds the digit's offset (exclusive scan of the

@@ -231,3 +231,25 @@ def test_oracle_reproduces_golden(fname):
         # fp32, different op order: relative to the largest covariance entry (off-diagonals cancel)
         np.testing.assert_allclose(o.get("cov3D"), z["ref_cov3D"], rtol=1e-5,
                                    atol=1e-6 * float(np.abs(z["ref_cov3D"]).max()))
+
+
+def test_cpu_abi_matches_oracle():
+    """oracle/libgsr_cpu.so -- the C oracle behind include/gsr.h's gsr_forward / gsr_backward
+    (resize callbacks, state in the caller's buffers; bench.py's CPU baseline) -- equals the
+    oracle's own API bit for bit on config 1 (one thread each: the OpenMP backward's per-Gaussian
+    sums follow the thread schedule)."""
+    import cpu_abi
+    case = common.make_case(P=1000, H=256, W=256)
+    o, og = common.run_oracle(case, antialiasing=True)
+    sc, cam = case["scene"], case["cam"]
+    L, color, inv, radii, g = cpu_abi.CpuRasterizer(nthreads=1).forward_backward(
+        sc["means3D"], sc["opacities"], case["bg"], cam.world_view_transform, cam.full_proj_transform,
+        cam.camera_center, cam.tanfovx, cam.tanfovy, 256, 256, case["grad_color"], case["grad_invdepth"],
+        shs=sc["shs"], sh_degree=3, scales=sc["scales"], rotations=sc["rotations"], antialiasing=True)
+    assert L == o.num_rendered
+    np.testing.assert_array_equal(radii, o.radii)
+    np.testing.assert_array_equal(color, o.color)
+    np.testing.assert_array_equal(inv, o.invdepth)
+    for k in ("dL_dmean2D", "dL_dopacity", "dL_dcolors", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+              "dL_drotations"):
+        np.testing.assert_array_equal(g[k], og[k].reshape(g[k].shape), err_msg=k)
