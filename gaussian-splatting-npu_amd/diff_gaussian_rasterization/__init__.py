@@ -53,19 +53,24 @@ def grad_chunk_hook(chunks, fn, done):
     context split their BACKWARD::preprocess into `chunks` launches over Gaussian ranges and call
     fn(g0, g1, grads) after each (grads: {input name: the gradient tensor that input receives},
     rows [g0, g1) final in stream order), then done() before the backward returns -- the hook
-    multiview.overlapped_allreduce uses to reduce each range while the next one computes."""
-    prev = getattr(_state, "grad_chunks", None)
-    _state.grad_chunks = (int(chunks), fn, done)
+    multiview.overlapped_allreduce uses to reduce each range while the next one computes.
+    Process-wide, not per thread: autograd runs a CUDA backward on its own device thread."""
+    global _grad_chunks
+    prev = _grad_chunks
+    _grad_chunks = (int(chunks), fn, done)
     try:
         yield
     finally:
-        _state.grad_chunks = prev
+        _grad_chunks = prev
+
+
+_grad_chunks = None  # the active grad_chunk_hook (process-wide)
 
 
 def _chunk_hook(wanted):
     """(on_chunk for _C, done) from the active grad_chunk_hook, restricted to the gradients of the
     inputs in `wanted` (names); (None, None) outside the context."""
-    h = getattr(_state, "grad_chunks", None)
+    h = _grad_chunks
     if h is None or not wanted:
         return None, None
     chunks, fn, done = h

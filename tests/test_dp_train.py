@@ -31,6 +31,29 @@ def _free_port():
     return p
 
 
+def _collect(q, procs, timeout=240):
+    """The workers' results; fails fast (instead of waiting out the timeout) when a worker dies --
+    its peer may then wait in a collective forever, so every worker is terminated."""
+    import queue
+    import time
+    res, t0 = [], time.monotonic()
+    try:
+        while len(res) < len(procs):
+            try:
+                res.append(q.get(timeout=2))
+            except queue.Empty:
+                dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+                assert not dead, f"a worker failed (exit codes {[p.exitcode for p in procs]})"
+                assert time.monotonic() - t0 < timeout, "workers timed out"
+    finally:
+        for p in procs:
+            p.join(timeout=30 if len(res) == len(procs) else 1)
+            if p.is_alive():
+                p.terminate()
+                p.join(timeout=10)
+    return sorted(res, key=lambda r: r[0])
+
+
 def _setup(dev):
     """Trainer (perturbed start of the seed-0 cloud), settings per view and ground-truth images."""
     import synthetic
@@ -99,11 +122,7 @@ def test_two_ranks_match_single_process():
     procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    try:
-        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
-    finally:
-        for p in procs:
-            p.join(timeout=60)
+    res = _collect(q, procs)
     assert all(p.exitcode == 0 for p in procs)
 
     # the single-process run of the same step: both ranks' views, their buffers summed here
@@ -278,11 +297,7 @@ def test_two_ranks_densify_and_reset_match_single_process():
     procs = [ctx.Process(target=_dworker, args=(r, port, threshold, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    try:
-        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
-    finally:
-        for p in procs:
-            p.join(timeout=60)
+    res = _collect(q, procs)
     assert all(p.exitcode == 0 for p in procs)
 
     emu, did = _emulate(dev, threshold)
@@ -327,7 +342,9 @@ def _oworker(rank, port, q):
                 c.full_proj_transform.to(dev), 3, c.camera_center.to(dev), False, False, False))
             grads.append(tuple(g.to(dev) for g in synthetic.make_grads(O_H, O_W, seed=1 + v)))
         out = {}
+        log = open(os.path.join(root, "gpurun_out", f"overlap_rank{rank}.log"), "w")
         for mode in ("plain", "overlap", "deferred_overlap"):
+            print(f"rank {rank} mode {mode} start", file=log, flush=True)
             params = {k: v.to(dev).clone().requires_grad_(True) for k, v in scene.items()}
             ctx = multiview.overlapped_allreduce(chunks=3) if mode != "plain" else contextlib.nullcontext()
             with ctx as st:
@@ -351,6 +368,7 @@ def _oworker(rank, port, q):
             else:
                 assert st["chunks"] == 3 and st["collectives"] == 15, st
             torch.cuda.synchronize()
+            print(f"rank {rank} mode {mode} done {st}", file=log, flush=True)
             out[mode] = {k: p.grad.cpu().numpy() for k, p in params.items()}
         q.put((rank, out))
     finally:
@@ -365,14 +383,11 @@ def test_overlapped_allreduce_equals_allreduce_after_backward():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    os.makedirs(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out"), exist_ok=True)
     procs = [ctx.Process(target=_oworker, args=(r, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    try:
-        res = sorted([q.get(timeout=240) for _ in range(WORLD)], key=lambda r: r[0])
-    finally:
-        for p in procs:
-            p.join(timeout=60)
+    res = _collect(q, procs)
     assert all(p.exitcode == 0 for p in procs)
     ref = res[0][1]["plain"]
     for rank, out in res:

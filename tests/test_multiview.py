@@ -331,7 +331,7 @@ def _overlap_worker(rank, world, port, q):
             dist.all_reduce(t)
         grads = {k: t.grad for k, t in mine.items()}
         with multiview.overlapped_allreduce(chunks=3) as st:
-            chunks, fn, done = dgr._state.grad_chunks  # what a batched backward calls
+            chunks, fn, done = dgr._grad_chunks  # what a batched backward calls
             step = 384
             for g0 in range(0, P, step):
                 fn(g0, min(P, g0 + step), grads)
