@@ -229,7 +229,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
 }
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
-template <int ITEMS, bool PAIR, typename KIND>
+template <int ITEMS, bool PAIR, typename KIND, int NBITS>
 __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
@@ -244,7 +244,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     __shared__ uint32_t s_w0[4], s_w1[4];      // wave totals of the two block scans
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t nb = 1u << a.nbits, mask = nb - 1u;
+    const uint32_t nb = 1u << NBITS, mask = nb - 1u;  // the digit width (== a.nbits): unrolled ranking
     const uint32_t chunk = blockIdx.x;
     for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
     // digit offsets: exclusive scan of the totals (in s_base), plus this chunk's row prefix
@@ -276,7 +276,8 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
         const bool valid = li < nvalid;
         const uint32_t d = digit_of(key[i], a.shift, mask);
         uint64_t peers = __ballot(valid);
-        for (int b = 0; b < a.nbits; b++) {
+#pragma unroll
+        for (int b = 0; b < NBITS; b++) {
             const uint64_t bal = __ballot((d >> b) & 1u);
             peers &= ((d >> b) & 1u) ? bal : ~bal;
         }
@@ -461,10 +462,10 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_count_kernel(const Vie
     if ((uint32_t)tid < nb) J.counts[(size_t)tid * J.nchunks + c] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
-template <int ITEMS>
-__global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const ViewBatch<FusedPassArgs> B, uint32_t gx,
-                                                                        int nbits)
+template <int ITEMS, int NBITS>
+__global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const ViewBatch<FusedPassArgs> B, uint32_t gx)
 {
+    constexpr int nbits = NBITS;  // the digit width, a compile-time constant (unrolled ballot ranking)
     constexpr int TILE = RS_THREADS * ITEMS;
     const FusedPassArgs& J = B.v[blockIdx.y];
     const int c = (int)blockIdx.x;
@@ -538,10 +539,15 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
         // only the digit is kept per element (the sorted slots stage round positions, and the
         // write-out derives tile, slot and id again): 2 B of LDS per element instead of 12, and
         // no payload registers
+        // a partial round (most rounds: a chunk holds ~1,500 instances of its 2,048 slots) leaves
+        // whole 64-element items of the last waves empty: they skip the digit derivation and the
+        // ballots (wave-uniform test)
         uint32_t key[ITEMS], rank[ITEMS];
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const int li = w * (ITEMS * 64) + i * 64 + lane;
+            key[i] = 0u;
+            if (w * (ITEMS * 64) + i * 64 >= nvalid) continue;
             const uint32_t sl = r0 + (uint32_t)min(li, nvalid - 1);
             const int j = s_own[min(li, nvalid - 1)];
             uint32_t local;
@@ -550,10 +556,13 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             const int li = w * (ITEMS * 64) + i * 64 + lane;
+            rank[i] = 0xFFFFFFFFu;
+            if (w * (ITEMS * 64) + i * 64 >= nvalid) continue;
             const bool valid = li < nvalid;
             const uint32_t d = key[i];
             uint64_t peers = __ballot(valid);
-            for (int b = 0; b < nbits; b++) {
+#pragma unroll
+            for (int b = 0; b < NBITS; b++) {
                 const uint64_t bal = __ballot((d >> b) & 1u);
                 peers &= ((d >> b) & 1u) ? bal : ~bal;
             }
@@ -755,8 +764,15 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 hipLaunchKernelGGL(radix_rowscan_lds_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
             else
                 hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
-            if (pair) hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND>), g, b, 0, s, sb);
-            else hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND>), g, b, 0, s, sb);
+            switch (w * 2 + (pair ? 1 : 0)) {
+#define GSR_SCATTER_W(W_)                                                                                   \
+    case 2 * W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, W_>), g, b, 0, s, sb); break; \
+    case 2 * W_ + 1: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, W_>), g, b, 0, s, sb); break;
+                GSR_SCATTER_W(1) GSR_SCATTER_W(2) GSR_SCATTER_W(3) GSR_SCATTER_W(4)
+                GSR_SCATTER_W(5) GSR_SCATTER_W(6) GSR_SCATTER_W(7) GSR_SCATTER_W(8)
+#undef GSR_SCATTER_W
+            default: return hipErrorInvalidValue;
+            }
             shift += w;
         }
         return hipGetLastError();
@@ -825,7 +841,13 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
                 hipLaunchKernelGGL(radix_rowscan_kernel<TileSort>, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
         }
         if (!(phases & FUSED_SCATTER)) return hipGetLastError();
-        hipLaunchKernelGGL(fused_pass1_scatter_kernel<RS_ITEMS>, g, b, 0, s, fb, gx, w1);
+        switch (w1) {  // the first pass's digit width: ceil(msb(T) / passes) -- 7 at 1080p
+#define GSR_FUSED_W(W_) case W_: hipLaunchKernelGGL((fused_pass1_scatter_kernel<RS_ITEMS, W_>), g, b, 0, s, fb, gx); break;
+            GSR_FUSED_W(1) GSR_FUSED_W(2) GSR_FUSED_W(3) GSR_FUSED_W(4)
+            GSR_FUSED_W(5) GSR_FUSED_W(6) GSR_FUSED_W(7) GSR_FUSED_W(8)
+#undef GSR_FUSED_W
+        default: return hipErrorInvalidValue;
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || npass == 1) return e;
         // the later passes: key bits [w1, nbits), ping-pong k1/v1 -> k0/v0 -> ...

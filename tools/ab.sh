@@ -13,7 +13,7 @@ for r in $(seq "$R"); do
   for v in ab/*.so; do
     n=$(basename "$v" .so)
     cp "$v" "$LIB"
-    timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-aux --no-pmc ${BENCH_EXTRA:-} > "gpurun_out/ab/$n.$r.log" 2>&1 || { cp /tmp/lib_orig.so "$LIB"; tail -5 "gpurun_out/ab/$n.$r.log"; exit 1; }
+    timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-aux --no-pmc --no-single-view ${BENCH_EXTRA:-} > "gpurun_out/ab/$n.$r.log" 2>&1 || { cp /tmp/lib_orig.so "$LIB"; tail -5 "gpurun_out/ab/$n.$r.log"; exit 1; }
     python3 - "gpurun_out/ab/$n.$r.log" "$n" "$KS" <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])

@@ -39,6 +39,7 @@ PY
     hits) run hits 200 python -u tools/dbg/hit_dump.py ;;
     pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
     dist) run dist 400 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
+    ab:*) run ab 900 bash tools/ab.sh ${st#ab:} ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
