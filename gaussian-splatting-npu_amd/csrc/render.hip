@@ -591,10 +591,12 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
 
     __shared__ float4 s_recw[BWD_TPW][3][64];
     __shared__ uint8_t s_lqw[BWD_TPW][4][64];
-    __shared__ float s_accw[BWD_TPW][GF_NUM][64];
+    // rows padded to 65 floats: the 16 lanes of a group add the ten fields of one entry (same
+    // column e) at once, which a 64-float row stride would put in one LDS bank
+    __shared__ float s_accw[BWD_TPW][GF_NUM][65];
     float4 (&s_rec)[3][64] = s_recw[wv];
     uint8_t (&s_lq)[4][64] = s_lqw[wv];  // per quadrant: the batch entries it evaluates, in list order
-    float (&s_acc)[GF_NUM][64] = s_accw[wv];  // per batch entry: sums of its quadrant partials
+    float (&s_acc)[GF_NUM][65] = s_accw[wv];  // per batch entry: sums of its quadrant partials
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
