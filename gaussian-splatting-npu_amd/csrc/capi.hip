@@ -511,7 +511,8 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
 
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix);
+                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix,
+                               bool counted = false);
 
 // The tile sort of one view (L > 0 instances) with the instance emission fused into its first
 // pass: the instances are generated from the depth-ordered rects; the sort's ping-pong buffers live
@@ -586,9 +587,10 @@ static RenderFwdArgs render_fwd_args(char* gb, char* bb, char* ib, int P, int L,
 
 // Forward, second half: the tile sort (emission fused in), tile ranges and tile order on the
 // prefix stream, render_fwd on the caller's.
+// counted: the tile sort's first-pass histograms already ran (enqueued before the L read-back)
 static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char* image_buffer, int P,
                                int num_rendered, const float* background, int width, int height, float* out_color,
-                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix)
+                               float* depth, bool debug, gsr_stream_t stream, hipStream_t prefix, bool counted)
 {
     // (colors_precomp was folded into the render record by preprocess)
     hipStream_t s = prefix;
@@ -609,8 +611,8 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
         // stable sort by tile id over bits [0, msb(T)) of the depth-ordered instances
         // (rasterizer_impl.cu:303-311 sorts [0, 32 + msb(T)) of the tile|depth keys)
         const TileSortJob j = fused_tile_sort_job(gb, bb, ib, P, L, width, height);
-        ProfScope ps_(PK_TILE_SORT, s);
-        HIP_TRY(tile_sort_fused_batch(&j, 1, gx, T, s));
+        ProfScope ps_(PK_TILE_SORT, s, counted);
+        HIP_TRY(tile_sort_fused_batch(&j, 1, gx, T, s, counted ? FUSED_SCATTER : FUSED_ALL));
     }
     DEBUG_SYNC(s);
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
@@ -688,6 +690,22 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
                                  viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
                                  radii, debug, ps, &h);
     if (rc) return rc;
+    {
+        // the tile sort's first-pass histograms need only the depth-ordered rects and offsets (not L
+        // or the binning buffer): enqueued before the read-back, they run while the host waits
+        const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
+        const int T = (int)(gx * (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y));
+        const TileSortJob cj = fused_tile_sort_job(geometry_buffer, nullptr, image_buffer, P, 0, width, height);
+        hipError_t e;
+        {
+            ProfScope ps_(PK_TILE_SORT, ps);
+            e = tile_sort_fused_batch(&cj, 1, gx, T, ps, FUSED_COUNT);
+        }
+        if (e != hipSuccess) {
+            prefix_end((hipStream_t)stream, ps);
+            return fail_hip(e, __LINE__);
+        }
+    }
     int L = 0;
     rc = forward_geometry_wait(h, ps, &L);
     *num_rendered = L;
@@ -698,7 +716,7 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity)  // caller allocates
         return prefix_end((hipStream_t)stream, ps);
     rc = forward_render_impl(geometry_buffer, binning_buffer, image_buffer, P, L, background, width, height,
-                             out_color, depth, debug, stream, ps);
+                             out_color, depth, debug, stream, ps, true);
     if (rc) return rc;
     *rendered = 1;
     return GSR_OK;

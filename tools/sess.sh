@@ -40,6 +40,11 @@ PY
     pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
     dist) run dist 400 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
     ab:*) run ab 900 bash tools/ab.sh ${st#ab:} ;;
+    ab1:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred" run ab1 900 bash tools/ab.sh ${st#ab1:} ;;
+    ab1np:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred --no-prefix-stream" run ab1np 900 bash tools/ab.sh ${st#ab1np:} ;;
+    pmcv) run pmcv 500 bash tools/pmc_views.sh "$TAG/pmcv" ;;
+    pmc1) BENCH_ARGS="--views-total 1 --per-view --no-deferred" run pmc1 500 bash tools/pmc_views.sh "$TAG/pmc1" ;;
+    trace1) run trace1 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof1" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-aux --no-single-view --no-pmc --views-total 1 --per-view --no-deferred ;;
     *) echo "unknown step $st"; exit 2 ;;
   esac
 done
