@@ -429,72 +429,88 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
 // The reference replays each pixel's list back to front, rebuilding T by division and the
 // colour behind entry j (accum_rec) incrementally.  The same gradient in forward order:
 // with T_j the transmittance in front of j, cd_j = c_j . dL/dpixel (+ invdepth_j . dL/dinvdepth),
-// Fd_j = sum_{k <= j} alpha_k T_k cd_k and R = out_color . dL/dpixel (+ invdepth . dL/dinvdepth)
-// (out_color includes the background term T_final * bg),
-//     dL/dalpha_j = T_j cd_j - (R - Fd_j) / (1 - alpha_j)            (backward.cu:577-615)
-// because R - Fd_j = (colour behind j) . dL + T_final * (bg . dL).  T_j is then the forward's
-// own running product (bit-identical to forward.cu:372-383), no division by (1 - alpha) is
-// needed to rebuild it, and the per-pixel state shrinks to T, Fd, R and dL/dpixel.
+// and B_j = R - sum_{k <= j} alpha_k T_k cd_k, R = out_color . dL/dpixel (+ invdepth .
+// dL/dinvdepth) (out_color includes the background term T_final * bg),
+//     dL/dalpha_j = T_j cd_j - B_j / (1 - alpha_j)                  (backward.cu:577-615)
+// because B_j = (colour behind j) . dL + T_final * (bg . dL).  T_j is then the forward's own
+// running product (bit-identical to forward.cu:372-383), no division by (1 - alpha) is needed to
+// rebuild it, and the per-pixel state shrinks to T, B and dL/dpixel.
 struct BwdPair {
-    v2f T, R, Fd, dp0, dp1, dp2, dinv;
+    v2f T, B, dp0, dp1, dp2, dinv;
     uint32_t lc0, lc1;  // last_contributor
 };
 
+// A lane's sums over its two pixel pairs for one Gaussian: the colour and invdepth terms per
+// pixel, and u = G * dL/dalpha with its dx, dx^2 moments.  The lane's four pixels share one row, so
+// the dy-moments need no per-pixel sums: sum u dy = dy sum u, sum u dx dy = dy sum u dx and
+// sum u dy^2 = dy^2 sum u (bwd_lane_terms).
+struct BwdAcc {
+    v2f col0, col1, col2, inv, u, udx, udx2;
+};
+
 // Two pixels x one Gaussian, branch-free: a pixel the Gaussian does not contribute to gets
-// alpha = G = 0, which leaves its state bitwise unchanged (T * (1 - 0) = T, Fd + 0 * cd = Fd)
+// alpha = G = 0, which leaves its state bitwise unchanged (T * (1 - 0) = T, B - 0 * cd = B)
 // and adds exact zeros.  Per-Gaussian constant factors are left to preprocess_bwd (see
-// GradField): with u = G * dL/dalpha the record holds sum u (opacity), sum u*dx and sum u*dy
-// (mean2D: (a Sx + b Sy, b Sx + c Sy) times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy,
-// u*dy*dy (conic, times -opacity/2).
-// FIRST: o[] is assigned, not accumulated (the entry's first half: no zero-initialisation).
+// GradField): the record holds sum u (opacity), sum u*dx and sum u*dy (mean2D: (a Sx + b Sy,
+// b Sx + c Sy) times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy, u*dy*dy (conic, times
+// -opacity/2).  FIRST: the sums are assigned, not accumulated (no zero-initialisation).
 template <bool HAS_INV, bool FIRST>
-__device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, float pfy, uint32_t pos, const float4 xy,
-                                         const Falloff f, const float4 co, const float4 col, v2f* o)
+__device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, const float4 xy, float bq, float cq,
+                                         const Falloff f, const float4 co, const float4 col, BwdAcc& o)
 {
     const v2f dx = (v2f)(xy.x) - pfx;
-    const float dy = xy.y - pfy;
-    const v2f p2 = falloff_p2(f, dx, dy);
+    const v2f p2 = fma2(fma2((v2f)(f.ka), dx, (v2f)(bq)), dx, (v2f)(cq));
     const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
     const v2f al = G * co.w;
-    const float alx = fminf(0.99f, al.x), aly = fminf(0.99f, al.y);
-    const bool c0 = pos < s.lc0 && !(p2.x > 0.0f) && !(alx < 1.0f / 255.0f);
-    const bool c1 = pos < s.lc1 && !(p2.y > 0.0f) && !(aly < 1.0f / 255.0f);
-    const v2f alpha = {c0 ? alx : 0.f, c1 ? aly : 0.f};
+    const bool c0 = pos < s.lc0 && !(p2.x > 0.0f) && !(al.x < 1.0f / 255.0f);
+    const bool c1 = pos < s.lc1 && !(p2.y > 0.0f) && !(al.y < 1.0f / 255.0f);
     const v2f Gc = {c0 ? G.x : 0.f, c1 ? G.y : 0.f};
+    const v2f a = Gc * co.w;  // alpha before the 0.99 clamp (0 where the pixel is not reached)
+    const v2f alpha = {fminf(0.99f, a.x), fminf(0.99f, a.y)};
     const v2f one_m = 1.f - alpha;
     // v_rcp_f32 (1 ulp) in place of the IEEE division of backward.cu:615
     const v2f r_om = {__builtin_amdgcn_rcpf(one_m.x), __builtin_amdgcn_rcpf(one_m.y)};
     v2f cd = fma2((v2f)(col.z), s.dp2, fma2((v2f)(col.y), s.dp1, (v2f)(col.x) * s.dp0));
     if constexpr (HAS_INV) cd = fma2((v2f)(col.w), s.dinv, cd);
     const v2f aT = alpha * s.T;  // dL/dcolour / dL/dpixel (backward.cu:586-590)
-    s.Fd = fma2(aT, cd, s.Fd);
-    const v2f dL = fma2(s.T, cd, -(s.R - s.Fd) * r_om);
+    s.B = fma2(-aT, cd, s.B);
+    const v2f dL = fma2(s.T, cd, -s.B * r_om);
     s.T = s.T * one_m;
     const v2f u = Gc * dL;
-    const v2f ux = u * dx, uy = u * dy;
+    const v2f ux = u * dx;
     if constexpr (FIRST) {
-        o[GF_COLOR_R] = aT * s.dp0;
-        o[GF_COLOR_G] = aT * s.dp1;
-        o[GF_COLOR_B] = aT * s.dp2;
-        o[GF_INVDEPTH] = HAS_INV ? aT * s.dinv : (v2f)(0.f);
-        o[GF_OPACITY] = u;
-        o[GF_MEAN2D_X] = ux;  // sum u dx, sum u dy: the conic (a, b, c) is applied per Gaussian
-        o[GF_MEAN2D_Y] = uy;
-        o[GF_CONIC_A] = ux * dx;
-        o[GF_CONIC_B] = ux * dy;
-        o[GF_CONIC_C] = uy * dy;
+        o.col0 = aT * s.dp0;
+        o.col1 = aT * s.dp1;
+        o.col2 = aT * s.dp2;
+        o.inv = HAS_INV ? aT * s.dinv : (v2f)(0.f);
+        o.u = u;
+        o.udx = ux;
+        o.udx2 = ux * dx;
     } else {
-        o[GF_COLOR_R] = fma2(aT, s.dp0, o[GF_COLOR_R]);
-        o[GF_COLOR_G] = fma2(aT, s.dp1, o[GF_COLOR_G]);
-        o[GF_COLOR_B] = fma2(aT, s.dp2, o[GF_COLOR_B]);
-        if constexpr (HAS_INV) o[GF_INVDEPTH] = fma2(aT, s.dinv, o[GF_INVDEPTH]);
-        o[GF_OPACITY] += u;
-        o[GF_MEAN2D_X] += ux;
-        o[GF_MEAN2D_Y] += uy;
-        o[GF_CONIC_A] = fma2(ux, dx, o[GF_CONIC_A]);
-        o[GF_CONIC_B] = fma2(ux, (v2f)(dy), o[GF_CONIC_B]);
-        o[GF_CONIC_C] = fma2(uy, (v2f)(dy), o[GF_CONIC_C]);
+        o.col0 = fma2(aT, s.dp0, o.col0);
+        o.col1 = fma2(aT, s.dp1, o.col1);
+        o.col2 = fma2(aT, s.dp2, o.col2);
+        if constexpr (HAS_INV) o.inv = fma2(aT, s.dinv, o.inv);
+        o.u += u;
+        o.udx += ux;
+        o.udx2 = fma2(ux, dx, o.udx2);
     }
+}
+
+// The ten per-Gaussian values of one lane (its four pixels) for the transposed reduction.
+__device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float* v)
+{
+    const float su = o.u.x + o.u.y, sudx = o.udx.x + o.udx.y;
+    v[GF_OPACITY] = su;
+    v[GF_MEAN2D_X] = sudx;
+    v[GF_MEAN2D_Y] = dy * su;
+    v[GF_CONIC_A] = o.udx2.x + o.udx2.y;
+    v[GF_CONIC_B] = dy * sudx;
+    v[GF_CONIC_C] = (dy * dy) * su;
+    v[GF_COLOR_R] = o.col0.x + o.col0.y;
+    v[GF_COLOR_G] = o.col1.x + o.col1.y;
+    v[GF_COLOR_B] = o.col2.x + o.col2.y;
+    v[GF_INVDEPTH] = o.inv.x + o.inv.y;
 }
 
 // Backward: ONE wave per 16x16 tile, so there are no workgroup barriers in the main loop and no
@@ -561,7 +577,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     }
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
-    float R[4];
+    float R[4];  // out_color . dL/dpixel (+ invdepth . dL/dinvdepth): B before the first entry
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         if (!inside[p]) {
@@ -577,8 +593,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     for (int h = 0; h < 2; h++) {
         BwdPair& s = st[h];
         s.T = (v2f)(1.f);
-        s.R = {R[2 * h], R[2 * h + 1]};
-        s.Fd = (v2f)(0.f);
+        s.B = {R[2 * h], R[2 * h + 1]};
         s.dp0 = {dp0[2 * h], dp0[2 * h + 1]};
         s.dp1 = {dp1[2 * h], dp1[2 * h + 1]};
         s.dp2 = {dp2[2 * h], dp2[2 * h + 1]};
@@ -666,11 +681,13 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                     const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
                     const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
                     const Falloff f = falloff(co);
-                    v2f o[GF_NUM];
-                    bwd_pair<HAS_INV, true>(st[0], pfx0, pfy, pos, xy, f, co, col, o);
-                    bwd_pair<HAS_INV, false>(st[1], pfx1, pfy, pos, xy, f, co, col, o);
-#pragma unroll
-                    for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = o[q].x + o[q].y;
+                    // the falloff's dy terms, shared by the lane's two pairs (one row)
+                    const float dy = xy.y - pfy;
+                    const float bq = f.kb * dy, cq = (f.kc * dy) * dy;
+                    BwdAcc o;
+                    bwd_pair<HAS_INV, true>(st[0], pfx0, pos, xy, bq, cq, f, co, col, o);
+                    bwd_pair<HAS_INV, false>(st[1], pfx1, pos, xy, bq, cq, f, co, col, o);
+                    bwd_lane_terms(o, dy, &v[jj * GF_NUM]);
                 } else {
 #pragma unroll
                     for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = 0.f;
