@@ -375,17 +375,18 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
 }
 
 // ---- transposed wave reduction (CDNA4 cross-lane ops, no LDS) ------------------------------
+// The swaps exchange the two registers in place (both operands are read and written).  Through
+// the builtin the compiler copies one operand to a scratch register before each swap (a v_mov per
+// exchanged pair); as inline asm on two "+v" operands it swaps the values where they live.  The
+// s_nop 1 is the gfx950 hazard a VALU write -> v_permlane*_swap read requires (two wait states),
+// which the compiler cannot see inside the asm.
 __device__ __forceinline__ void xswap32(float& a, float& b)
 {
-    auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    a = __uint_as_float(r[0]);
-    b = __uint_as_float(r[1]);
+    asm("s_nop 1\n\tv_permlane32_swap_b32_e32 %0, %1" : "+v"(a), "+v"(b));
 }
 __device__ __forceinline__ void xswap16(float& a, float& b)
 {
-    auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
-    a = __uint_as_float(r[0]);
-    b = __uint_as_float(r[1]);
+    asm("s_nop 1\n\tv_permlane16_swap_b32_e32 %0, %1" : "+v"(a), "+v"(b));
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp(float x)
