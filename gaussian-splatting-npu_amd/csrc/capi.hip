@@ -376,6 +376,11 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
     a.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     a.dkey = at<uint32_t>(gb, g.off[GEOM_DKEY]);
     a.rect = at<uint2>(gb, g.off[GEOM_RECT]);
+    a.rect4 = nullptr;
+    if (rect_packable(a.grid_x, a.grid_y)) {  // the depth sort carries the packed rect as payload
+        a.rect4 = at<uint32_t>(gb, g.off[GEOM_RECT]);
+        a.rect = nullptr;
+    }
     *h_out = h;
     *hdev_out = h_dev;
     return GSR_OK;
@@ -406,16 +411,18 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
     if (e == hipSuccess) {
         char* tmp = gb + g.off[GEOM_DSORT_TMP];
         const size_t q = align_up(4 * (size_t)P, 256);
+        // keys u32, payload u32x2 (id, packed rect): k0 | v0 v0 | k1 | v1 v1
         uint32_t* k0 = reinterpret_cast<uint32_t*>(tmp);
         uint32_t* v0 = reinterpret_cast<uint32_t*>(tmp + q);
-        uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + 2 * q);
-        uint32_t* v1 = reinterpret_cast<uint32_t*>(tmp + 3 * q);
+        uint32_t* k1 = reinterpret_cast<uint32_t*>(tmp + 3 * q);
+        uint32_t* v1 = reinterpret_cast<uint32_t*>(tmp + 4 * q);
         ProfScope ps_(PK_DEPTH_SORT, s);
         // the last pass also lays the tile rects and tile counts out in depth order (the counts
         // into point_offsets, which the scan then turns into offsets in place)
-        e = radix_sort(P, DEPTH_BITS, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr,
-                       gb + g.off[GEOM_RADIX_SCRATCH], s, a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]),
-                       at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]));
+        SortJob j = {P, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH],
+                     a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
+                     a.rect4};
+        e = radix_sort_batch(&j, 1, DEPTH_BITS, s);
     }
     if (debug && e == hipSuccess) e = hipStreamSynchronize(s);
 
@@ -787,10 +794,11 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                   nullptr};
         char* tmp = gb + g.off[GEOM_DSORT_TMP];
         const size_t q = align_up(4 * (size_t)P, 256);
+        // keys u32, payload u32x2 (id, packed rect): k0 | v0 v0 | k1 | v1 v1
         dsort[v] = {P, a.dkey, nullptr, reinterpret_cast<uint32_t*>(tmp), reinterpret_cast<uint32_t*>(tmp + q),
-                    reinterpret_cast<uint32_t*>(tmp + 2 * q), reinterpret_cast<uint32_t*>(tmp + 3 * q),
+                    reinterpret_cast<uint32_t*>(tmp + 3 * q), reinterpret_cast<uint32_t*>(tmp + 4 * q),
                     at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH], a.rect,
-                    at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS])};
+                    at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), a.rect4};
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
     }

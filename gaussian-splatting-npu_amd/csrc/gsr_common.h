@@ -172,9 +172,11 @@ enum GeomArray {
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
     GEOM_EMIT_START,      // u32[P] first gradient-record slot of each Gaussian (index-order exclusive scan
                           // of tiles_touched)
-    GEOM_RECT,            // u16x4[P] tile rect {x0, y0, x1, y1} (getRect), zero if culled
+    GEOM_RECT,            // u16x4[P] tile rect {x0, y0, x1, y1} (getRect), zero if culled; on grids of
+                          // <= 255 x 255 tiles the first 4P bytes hold it packed instead (u8x4, rect_pack)
     GEOM_SORTED_RECT,     // u16x4[P] the rects in depth order (last depth-sort pass)
-    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, v0, k1, v1; then the count matrix of the
+    GEOM_DSORT_TMP,       // depth-sort ping-pong: u32[P] k0, u32x2[P] v0, u32[P] k1, u32x2[P] v1 (payload:
+                          // id, packed rect); then the count matrix of the
                           // fused emission + first tile-sort pass (gsr_forward_views)
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
     GEOM_SCAN_SCRATCH,    // 2 x u64[scan chunks + 1] look-back status words + chunk ticket of the two
@@ -208,6 +210,20 @@ enum BinArray {
 constexpr int SCAN_ITEMS = 4096;  // items per scan block (256 threads x 16)
 constexpr int DEPTH_BITS = 32;  // depth keys are full float bit patterns
 
+// A tile rect packed into one word (x0, y0, x1, y1: one byte each), for grids of at most 255 x 255
+// tiles (4080 x 4080 pixels): the depth sort carries it as payload beside the Gaussian id, so its
+// last pass writes the depth-ordered rects without gathering them by id.
+__host__ __device__ inline bool rect_packable(uint32_t grid_x, uint32_t grid_y) { return grid_x <= 255u && grid_y <= 255u; }
+__host__ __device__ inline uint32_t rect_pack(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1)
+{
+    return x0 | (y0 << 8) | (x1 << 16) | (y1 << 24);
+}
+// the unpacked u16x4 form {x0 | y0 << 16, x1 | y1 << 16}
+__host__ __device__ inline uint2 rect_unpack(uint32_t r)
+{
+    return make_uint2((r & 0xFFu) | (((r >> 8) & 0xFFu) << 16), ((r >> 16) & 0xFFu) | ((r >> 24) << 16));
+}
+
 struct GeomLayout { size_t off[GEOM_COUNT + 1]; };
 struct ImageLayout { size_t off[IMG_COUNT + 1]; };
 struct BinLayout { size_t off[BIN_COUNT + 1]; };
@@ -221,7 +237,7 @@ inline GeomLayout geom_layout(int P)
     size_t sizes[GEOM_COUNT] = {4 * p, 4 * p, p, 8 * p, 16 * p, 12 * p, 4 * p, 4 * p, 48 * p,
                                 4 * p, 4 * p, 4 * p, 8 * p, 8 * p,
                                 // (after the depth sort, the fused tile-sort pass's count matrix)
-                                std::max(16 * p + 1024, fused_pass1_scratch_bytes(P)), radix_status_bytes(P, 4),
+                                std::max(24 * p + 2048, fused_pass1_scratch_bytes(P)), radix_status_bytes(P, 4),
                                 16 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
     GeomLayout l;
     size_t o = 0;

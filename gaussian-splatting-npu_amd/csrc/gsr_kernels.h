@@ -36,7 +36,8 @@ struct PreprocessArgs {
     int scan_status_words;
     float4* splat;  // 3 x float4 per Gaussian (GEOM_SPLAT)
     uint32_t* dkey; // depth-sort key per Gaussian
-    uint2* rect;    // {x0 | y0 << 16, x1 | y1 << 16} per Gaussian (zero if culled)
+    uint2* rect;    // {x0 | y0 << 16, x1 | y1 << 16} per Gaussian (zero if culled); null with rect4
+    uint32_t* rect4;  // the rect packed (rect_pack) instead, on grids of <= 255 x 255 tiles
 };
 
 struct RenderFwdArgs {
@@ -222,6 +223,9 @@ struct SortJob {  // radix_sort's arguments for one view
     const uint2* rects;
     uint2* sorted_rects;
     uint32_t* sorted_counts;
+    // packed rects (rect_pack) in key order: carried as payload beside the id (v0 / v1 then hold
+    // u32x2), the last pass unpacks them into sorted_rects -- no gather by id
+    const uint32_t* rects4 = nullptr;
 };
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };

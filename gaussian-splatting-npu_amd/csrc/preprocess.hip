@@ -126,7 +126,8 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     auto cull = [&]() {
         a.radii[idx] = 0;
         a.tiles_touched[idx] = 0;
-        a.rect[idx] = make_uint2(0u, 0u);
+        if (a.rect4) a.rect4[idx] = 0u;
+        else a.rect[idx] = make_uint2(0u, 0u);
         a.dkey[idx] = 0xFFFFFFFFu;  // culled Gaussians sort behind every visible one
     };
 
@@ -197,7 +198,8 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     const float opacity = opacity_in * h_convolution_scaling;
     reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
-    a.rect[idx] = make_uint2(rminx | (rminy << 16), rmaxx | (rmaxy << 16));
+    if (a.rect4) a.rect4[idx] = rect_pack(rminx, rminy, rmaxx, rmaxy);
+    else a.rect[idx] = make_uint2(rminx | (rminy << 16), rmaxx | (rmaxy << 16));
 
     // Render record.  cullK bounds the ellipse d^T Q d <= K = 2 ln(255 opacity) outside which
     // alpha = opacity * exp(power) < 1/255 (Q = the fp32 conic the render kernels evaluate),

@@ -208,6 +208,9 @@ struct SortPassArgs {
     uint32_t* sorted_counts;
     const uint32_t* row_prefix;  // (nbins, nchunks) exclusive row scans
     const uint32_t* totals;      // (nbins) digit totals
+    // PAIR, first pass: the payload is (input index, rects4_in[index]) -- the packed rect carried
+    // beside the id (the depth sort); the last pass then unpacks v.y into sorted_rects / sorted_counts
+    const uint32_t* rects4_in;
 };
 
 // Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
@@ -261,7 +264,12 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
-    if (PAIR || a.vals_in) {  // PAIR: the caller's pairs in the first pass
+    if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            if constexpr (PAIR) val[i] = make_uint2((uint32_t)gidx(i), a.rects4_in[gidx(i)]);
+        }
+    } else if (PAIR || a.vals_in) {  // PAIR: the caller's pairs in the first pass
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
     } else {
@@ -328,6 +336,11 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
                 if constexpr (PAIR) {
                     if (a.out_x) a.out_x[dst] = v.x;
                     if (a.out_y) a.out_y[dst] = v.y;
+                    if (a.sorted_rects) {  // the carried packed rect (no gather by id)
+                        const uint2 rc = rect_unpack(v.y);
+                        a.sorted_rects[dst] = rc;
+                        a.sorted_counts[dst] = ((rc.y & 0xFFFFu) - (rc.x & 0xFFFFu)) * ((rc.y >> 16) - (rc.x >> 16));
+                    }
                 } else {
                     if (a.out_x) a.out_x[dst] = v;
                     if (a.rects) {
@@ -716,8 +729,10 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
         bool pair = false;
         for (int v = 0; v < nv; v++) {
             maxc = max(maxc, (int)rs_chunks(jobs[v0 + v].n));
-            pair = jobs[v0 + v].pairs != nullptr;
+            pair = jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr;
         }
+        for (int v = 0; v < nv; v++)  // one payload width per launch
+            if ((jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr) != pair) return hipErrorInvalidValue;
         if (maxc == 0) return hipSuccess;
         const uint32_t* kin[VIEW_BATCH];
         const uint32_t* vin[VIEW_BATCH];
@@ -751,7 +766,8 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.out_y = j.out_y;
                 a.sorted_keys = j.sorted_keys;
                 a.rects = (last && !pair) ? j.rects : nullptr;
-                a.sorted_rects = j.sorted_rects;
+                a.rects4_in = p == 0 ? j.rects4 : nullptr;
+                a.sorted_rects = (last && (!pair || j.rects4)) ? j.sorted_rects : nullptr;
                 a.sorted_counts = j.sorted_counts;
                 a.row_prefix = sort_counts(j);
                 a.totals = sort_totals(j);
