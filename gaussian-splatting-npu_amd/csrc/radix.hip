@@ -498,8 +498,9 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     const uint32_t rowp = (uint32_t)tid < nb ? J.counts[(size_t)tid * J.nchunks + c] : 0u;
     const uint32_t gbase = block_excl_scan256(tot, s_w0) + rowp;
     s_base[tid] = gbase;
+    reinterpret_cast<uint64_t*>(s_own)[tid] = 0ull;  // the first round's owner marks start from zero
     uint32_t wbeg, wend;
-    fe_stage<true>(J, c, s, wbeg, wend);  // its barrier also publishes s_cnt = 0 and s_base
+    fe_stage<true>(J, c, s, wbeg, wend);  // its barrier also publishes s_cnt = 0, s_base and s_own
     const uint64_t lt = (1ull << lane) - 1ull;
     const bool last = J.keys_out == nullptr;
     // this thread's staged rank: start and end of its instances
@@ -512,10 +513,8 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     for (uint32_t r0 = wbeg; r0 < wend; r0 += TILE) {
         const int nvalid = (int)min((uint32_t)TILE, wend - r0);
         // owners of the round's positions without a search per instance: every rank starting inside
-        // the round marks its first position, and an inclusive max-scan (ranks increase with the
-        // position) seeded with the owner of r0 fills the rest
-        reinterpret_cast<uint64_t*>(s_own)[tid] = 0ull;
-        __syncthreads();
+        // the round marks its first position (s_own is zero here), and an inclusive max-scan (ranks
+        // increase with the position) seeded with the owner of r0 fills the rest
         if (my_end > my_start && my_start >= r0 && my_start < r0 + (uint32_t)nvalid)
             s_own[my_start - r0] = (uint8_t)tid;
         __syncthreads();
@@ -624,9 +623,12 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
                 }
             }
         }
+        // most chunks take one round: they skip the next round's set-up and its two barriers
+        if (r0 + (uint32_t)TILE >= wend) break;
         __syncthreads();
         s_base[tid] += total;  // the next round's elements follow this round's in every digit
         s_cnt[0][tid] = s_cnt[1][tid] = s_cnt[2][tid] = s_cnt[3][tid] = 0;
+        reinterpret_cast<uint64_t*>(s_own)[tid] = 0ull;
         __syncthreads();
     }
 }
