@@ -611,7 +611,6 @@ constexpr int VIEW_REC_BATCH = GSR_VIEW_REC_BATCH;
 // A lane's view inputs, loaded in the kernel's prologue (unconditionally, clamped), so that their
 // round trip overlaps the SH staging and the record gather is the only dependent one after it.
 struct ViewIn {
-    int radius;
     float4 co;
     uint8_t cl;
     uint32_t e0, n;  // record slots [e0, e0 + n)
@@ -620,7 +619,6 @@ struct ViewIn {
 __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int idx, int v, ViewIn& vi)
 {
     const BwdView& bv = A.v[v < A.V ? v : 0];
-    vi.radius = bv.radii[idx];
     vi.co = bv.conic_opacity[idx];
     vi.cl = bv.clamped[idx];
     vi.e0 = bv.emit_start[idx];
@@ -667,7 +665,9 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     const size_t i = (size_t)idx;
     const bool has_view = live && v < A.V;
     const BwdView& bv = A.v[v < A.V ? v : 0];
-    const bool vis = has_view && vi.radius > 0;
+    // visible <=> radius > 0 (backward.cu:163,420) <=> a tile count > 0: preprocess culls a Gaussian whose
+    // rect is empty and writes radius 0 and no tiles for every culled one (4 B per view less to read)
+    const bool vis = has_view && vi.n > 0;
     float gs[GF_NUM];
     if (vis) {
         gather_range<VIEW_REC_BATCH>(vi.e0, vi.e0 + vi.n, bv.valid, bv.grad_inst, gs);
