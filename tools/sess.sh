@@ -27,7 +27,7 @@ for st in "$@"; do
     bench) run bench 600 python -u bench.py
            cp -f gpurun_out/pmc_step.json gpurun_out/pmc_single.json "$OUT/" 2>/dev/null ;;
     benchq) run benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-aux --no-pmc --no-single-view ;;
-    trace) run trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-aux --no-single-view
+    trace) run trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-aux --no-single-view --no-pmc
            python3 - "$OUT" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/prof/**/*kernel_stats.csv", recursive=True)[0]
