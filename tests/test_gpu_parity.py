@@ -251,6 +251,30 @@ def test_8k_view_three_pass_tile_sort():
     common.check_render("8k 3k", _hip_render(s, kw, color.cpu().numpy(), inv.cpu().numpy()), _ora_render(o))
 
 
+@pytest.mark.parametrize("H,W", [(256, 4080), (256, 4096), (4080, 256), (4096, 256)])
+def test_packed_rect_boundary_keys_bit_exact(H, W):
+    """The depth sort carries the tile rect packed into one word (a byte per bound) on grids of at
+    most 255 x 255 tiles and gathers the u16x4 rect by id above that: 255 and 256 tiles along
+    either axis (rect bounds up to 255 / 256) give keys, ids and ranges bit-identical to the oracle."""
+    dgr = _dgr()
+    case = common.make_case(P=3000, H=H, W=W)
+    o, _ = common.run_oracle(case, nthreads=8, backward=False)
+    s = _settings(case)
+    sc = {k: v.to(DEV) for k, v in case["scene"].items()}
+    L, color, radii, geom, binning, img, inv = dgr._C.rasterize_gaussians(
+        s.bg, sc["means3D"], torch.Tensor([]), sc["opacities"], sc["scales"], sc["rotations"], 1.0,
+        torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width,
+        sc["shs"], s.sh_degree, s.campos, False, False, False)
+    torch.cuda.synchronize()
+    P = sc["means3D"].shape[0]
+    assert L == o.num_rendered and L > 0
+    np.testing.assert_array_equal(radii.cpu().numpy(), o.radii)
+    keys, vals, ranges = dgr._C.sorted_keys(geom, binning, img, P, L, s.image_width, s.image_height)
+    np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
+    np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+
+
 def test_mark_visible():
     import oracle
     dgr = _dgr()
