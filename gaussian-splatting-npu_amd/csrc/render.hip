@@ -302,11 +302,13 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
             uint64_t hitbits = 0;  // wave-uniform
-            // two entries per iteration with ping-pong record registers (no rotation copies)
+            // two entries per iteration with ping-pong record registers (no rotation copies).  take():
+            // the lowest set bit (s_ff1, -1 once none is left) and its clear (one s_bitset0; with
+            // none left it clears bit 63 of a zero mask)
             auto take = [&]() -> int {
-                const int jj = rem ? r * 64 + (int)__builtin_ctzll(rem) : -1;
-                rem &= rem - 1;
-                return jj;
+                int jl;
+                asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(jl), "+s"(rem));
+                return jl < 0 ? -1 : r * 64 + jl;
             };
             // Branch-free blend: every test is a compare feeding a select (no exec-mask branch, no
             // scalar mask algebra -- the scalar unit, shared by the CU's four SIMDs, is the busier
@@ -323,7 +325,15 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 live = stop ? 0.0f : live;
                 const float ae = stop ? 0.0f : (contrib ? a : 0.0f);
                 const bool blended = ae > 0.0f;
-                hitbits |= __ballot(blended) ? (1ull << (j & 63)) : 0ull;  // scalar select
+                {  // hitbits |= (any lane blended) ? bit j : 0 -- as one 64-bit scalar select (the
+                   // compiler splits it into two 32-bit ones: one scalar instruction more per entry)
+                    uint64_t t;
+                    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b64 %0, %2, 0"
+                        : "=s"(t)
+                        : "s"(__ballot(blended)), "s"(1ull << (j & 63))
+                        : "scc");
+                    hitbits |= t;
+                }
                 const float aT = ae * T;  // 0 leaves the sums unchanged
                 C0 += col.x * aT;
                 C1 += col.y * aT;
@@ -403,23 +413,48 @@ constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141;
 // coset of l & 15 under {0, 7, 8, 15}, across the four rows.  66 instructions for 4 x 32 totals,
 // against 32 x 4 shuffle+add pairs of per-value butterflies.
 __device__ __forceinline__ int quad_group(int lane) { return (lane & 4) ? 3 - (lane & 3) : (lane & 3); }
+// Eight swaps back to back behind ONE s_nop 1: every swapped register was written before the block,
+// so the two wait states cover them all (one per swap otherwise).
+#define GSR_SWAP8(OP, a, b)                                                                              \
+    asm("s_nop 1\n\t" OP " %0, %8\n\t" OP " %1, %9\n\t" OP " %2, %10\n\t" OP " %3, %11\n\t" OP           \
+        " %4, %12\n\t" OP " %5, %13\n\t" OP " %6, %14\n\t" OP " %7, %15"                                  \
+        : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]),      \
+          "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]), "+v"(b[4]), "+v"(b[5]), "+v"(b[6]), "+v"(b[7]))
 __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lane, float& r0, float& r1)
 {
+    GSR_SWAP8("v_permlane32_swap_b32_e32", (&v[0]), (&v[16]));
+    GSR_SWAP8("v_permlane32_swap_b32_e32", (&v[8]), (&v[24]));
 #pragma unroll
-    for (int i = 0; i < 16; i++) { xswap32(v[i], v[i + 16]); v[i] = v[i] + v[i + 16]; }
+    for (int i = 0; i < 16; i++) v[i] = v[i] + v[i + 16];
+    GSR_SWAP8("v_permlane16_swap_b32_e32", (&v[0]), (&v[8]));
 #pragma unroll
-    for (int i = 0; i < 8; i++) { xswap16(v[i], v[i + 8]); v[i] = v[i] + v[i + 8]; }
-    const bool b3 = lane & 8, b2 = lane & 4;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float keep = b3 ? v[i + 4] : v[i], send = b3 ? v[i] : v[i + 4];
-        v[i] = keep + dpp<DPP_ROW_MIRROR>(send);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-        const float keep = b2 ? v[i + 2] : v[i], send = b2 ? v[i] : v[i + 2];
-        v[i] = keep + dpp<DPP_ROW_HALF_MIRROR>(send);
-    }
+    for (int i = 0; i < 8; i++) v[i] = v[i] + v[i + 8];
+    // The last two stages pair lane l with its row mirror (l ^ 15: bit 3 flips) and then its half-row
+    // mirror (l ^ 7: bit 2 flips).  Lanes on either side keep different halves, so each output is
+    // two v_add_f32_dpp restricted by bank_mask to one side (a 4-lane bank = lane bits 3:2) instead
+    // of two selects and an add: lanes with bit 3 clear take v[i] + mirror(v[i]), the others
+    // v[i + 4] + mirror(v[i + 4]) (the partner of a clear lane holds its v[i] at the other side).
+    // The leading s_nop 1 gives the DPP reads of the registers the adds above wrote their two
+    // wait states.
+    (void)lane;
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %0, %4, %4 row_mirror row_mask:0xf bank_mask:0xc\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %1, %5, %5 row_mirror row_mask:0xf bank_mask:0xc\n\t"
+        "v_add_f32_dpp %2, %2, %2 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %2, %6, %6 row_mirror row_mask:0xf bank_mask:0xc\n\t"
+        "v_add_f32_dpp %3, %3, %3 row_mirror row_mask:0xf bank_mask:0x3\n\t"
+        "v_add_f32_dpp %3, %7, %7 row_mirror row_mask:0xf bank_mask:0xc"
+        : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3])
+        : "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+    asm("s_nop 1\n\t"
+        "v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %0, %2, %2 row_half_mirror row_mask:0xf bank_mask:0xa\n\t"
+        "v_add_f32_dpp %1, %1, %1 row_half_mirror row_mask:0xf bank_mask:0x5\n\t"
+        "v_add_f32_dpp %1, %3, %3 row_half_mirror row_mask:0xf bank_mask:0xa"
+        : "+v"(v[0]), "+v"(v[1])
+        : "v"(v[2]), "v"(v[3]));
     r0 = v[0];
     r1 = v[1];
 }
