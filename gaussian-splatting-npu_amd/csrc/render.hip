@@ -558,7 +558,7 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // i then evaluates the i-th entry of every quadrant at once (pixels of different quadrants share no
 // state; a group past its list evaluates a staged record at position "never", which adds zeros),
 // three iterations per transposed reduction; the groups add their partial totals into the
-// entries' LDS sums one group after the other, and at the end of the batch every contributing
+// entries' LDS sums two groups at a time (two sets of sums), and at the end of the batch every contributing
 // entry's lane stores its record (10 floats) at its record slot and flags it valid.  Against one
 // 64-lane pass per entry over the half-tiles it reaches, this skips the pixel pairs of quadrants
 // an entry does not reach (25 % of them) and reduces over 16 lanes: render_bwd -11 %.
@@ -643,11 +643,13 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     __shared__ float4 s_recw[BWD_TPW][3][64];
     __shared__ uint8_t s_lqw[BWD_TPW][4][64];
     // rows padded to 65 floats: the 16 lanes of a group add the ten fields of one entry (same
-    // column e) at once, which a 64-float row stride would put in one LDS bank
-    __shared__ float s_accw[BWD_TPW][GF_NUM][65];
+    // column e) at once, which a 64-float row stride would put in one LDS bank; column 64 takes the
+    // writes of lanes that hold no sum.  Two sets: groups 0 / 2 add into set 0, groups 1 / 3 into
+    // set 1, so two read-add-write phases per reduction instead of four (4 x 8.4 KB per workgroup).
+    __shared__ float s_accw[BWD_TPW][2][GF_NUM][65];
     float4 (&s_rec)[3][64] = s_recw[wv];
     uint8_t (&s_lq)[4][64] = s_lqw[wv];  // per quadrant: the batch entries it evaluates, in list order
-    float (&s_acc)[GF_NUM][65] = s_accw[wv];  // per batch entry: sums of its quadrant partials
+    float (&s_acc)[2][GF_NUM][65] = s_accw[wv];  // per batch entry: sums of its quadrant partials
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
@@ -691,7 +693,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             cq[q] = __popcll(bq);
         }
 #pragma unroll
-        for (int f = 0; f < GF_NUM; f++) s_acc[f][lane] = 0.f;
+        for (int f = 0; f < GF_NUM; f++) s_acc[0][f][lane] = s_acc[1][f][lane] = 0.f;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -742,18 +744,19 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             const bool ok1 = k1 < G * GF_NUM && (j1 == 0 ? act[0] : j1 == 1 ? act[1] : act[2]);
             const int e0 = j0 == 0 ? ej[0] : j0 == 1 ? ej[1] : ej[2];
             const int e1 = j1 == 0 ? ej[0] : j1 == 1 ? ej[1] : ej[2];
-            float* a0 = &s_acc[min(k0 - j0 * GF_NUM, GF_NUM - 1)][e0];
-            float* a1 = &s_acc[min(k1 - j1 * GF_NUM, GF_NUM - 1)][e1];
-            // the four groups add their partials into the entries' sums one group per phase (fixed
-            // order: reproducible); a group's 16 lanes hold distinct (field, entry) sums, so a plain LDS
-            // read-add-write is race-free (a wave's LDS operations complete in issue order) -- the LDS
-            // float atomics it replaces cost 6 % of render_bwd
+            float (&sa)[GF_NUM][65] = s_acc[grp & 1];
+            float* a0 = ok0 ? &sa[k0 - j0 * GF_NUM][e0] : &sa[0][64];
+            float* a1 = ok1 ? &sa[k1 - j1 * GF_NUM][e1] : &sa[1][64];
+            // groups 0 and 1, then 2 and 3, add their partials into their set's sums (fixed order:
+            // reproducible); the 32 lanes of a phase hold distinct (set, field, entry) sums, so a
+            // plain LDS read-add-write is race-free (a wave's LDS operations complete in issue
+            // order) -- the LDS float atomics it replaces cost 6 % of render_bwd
 #pragma unroll
-            for (int gg = 0; gg < 4; gg++) {
-                if (grp == gg) {
+            for (int ph = 0; ph < 2; ph++) {
+                if ((grp >> 1) == ph) {
                     const float o0 = *a0, o1 = *a1;
-                    if (ok0) *a0 = o0 + r0;
-                    if (ok1) *a1 = o1 + r1;
+                    *a0 = o0 + r0;
+                    *a1 = o1 + r1;
                 }
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                 __builtin_amdgcn_wave_barrier();
@@ -766,9 +769,12 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         // one 48-B record per contributing entry, stored by its own lane
         if (m != 0) {
             float* rec = a.grad_inst + (size_t)myslot * GRAD_REC;
-            reinterpret_cast<float4*>(rec)[0] = make_float4(s_acc[0][lane], s_acc[1][lane], s_acc[2][lane], s_acc[3][lane]);
-            reinterpret_cast<float4*>(rec)[1] = make_float4(s_acc[4][lane], s_acc[5][lane], s_acc[6][lane], s_acc[7][lane]);
-            reinterpret_cast<float2*>(rec)[4] = make_float2(s_acc[8][lane], s_acc[9][lane]);
+            float t[GF_NUM];
+#pragma unroll
+            for (int f = 0; f < GF_NUM; f++) t[f] = s_acc[0][f][lane] + s_acc[1][f][lane];
+            reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
+            reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
+            reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
             atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
