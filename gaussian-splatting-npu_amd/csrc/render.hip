@@ -533,20 +533,29 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, cons
     }
 }
 
+// x + y of a packed pair as ONE v_add_f32: left to itself the compiler emits v_pk_add_f32 with
+// op_sel (both halves computed, two issue slots for one useful sum)
+__device__ __forceinline__ float hsum(v2f a)
+{
+    float r;
+    asm("v_add_f32_e32 %0, %1, %2" : "=v"(r) : "v"(a.x), "v"(a.y));
+    return r;
+}
+
 // The ten per-Gaussian values of one lane (its four pixels) for the transposed reduction.
 __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float* v)
 {
-    const float su = o.u.x + o.u.y, sudx = o.udx.x + o.udx.y;
+    const float su = hsum(o.u), sudx = hsum(o.udx);
     v[GF_OPACITY] = su;
     v[GF_MEAN2D_X] = sudx;
     v[GF_MEAN2D_Y] = dy * su;
-    v[GF_CONIC_A] = o.udx2.x + o.udx2.y;
+    v[GF_CONIC_A] = hsum(o.udx2);
     v[GF_CONIC_B] = dy * sudx;
     v[GF_CONIC_C] = (dy * dy) * su;
-    v[GF_COLOR_R] = o.col0.x + o.col0.y;
-    v[GF_COLOR_G] = o.col1.x + o.col1.y;
-    v[GF_COLOR_B] = o.col2.x + o.col2.y;
-    v[GF_INVDEPTH] = o.inv.x + o.inv.y;
+    v[GF_COLOR_R] = hsum(o.col0);
+    v[GF_COLOR_G] = hsum(o.col1);
+    v[GF_COLOR_B] = hsum(o.col2);
+    v[GF_INVDEPTH] = hsum(o.inv);
 }
 
 // Backward: ONE wave per 16x16 tile, so there are no workgroup barriers in the main loop and no
