@@ -304,11 +304,11 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             uint64_t hitbits = 0;  // wave-uniform
             // two entries per iteration with ping-pong record registers (no rotation copies).  take():
             // the lowest set bit (s_ff1, -1 once none is left) and its clear (one s_bitset0; with
-            // none left it clears bit 63 of a zero mask)
+            // none left it clears bit 63 of a zero mask), as the batch position r * 64 + bit
             auto take = [&]() -> int {
                 int jl;
                 asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(jl), "+s"(rem));
-                return jl < 0 ? -1 : r * 64 + jl;
+                return r * 64 + jl;  // r * 64 - 1 once none is left (clamped by the caller)
             };
             // Branch-free blend: every test is a compare feeding a select (no exec-mask branch, no
             // scalar mask algebra -- the scalar unit, shared by the CU's four SIMDs, is the busier
@@ -342,21 +342,26 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 T = blended ? test_T : T;
                 last_contributor = blended ? (uint32_t)(base + j + 1) : last_contributor;
             };
+            // cnt entries to walk (rem != 0): a counted loop, so take() needs no end test; the
+            // look-ahead take() past the last entry returns -1, clamped to a valid record (unused).
+            // The all-finished exit is tested every second entry (blending into finished pixels
+            // is a no-op), at the end of each two-entry turn.
+            int left = __popcll(rem);
             int j = take();
             float4 axy = s_rec[j], aco = s_rec[BATCH + j], acol = s_rec[2 * BATCH + j];
             while (true) {
                 const int jb = take();
-                const int lb = jb >= 0 ? jb : j;
+                const int lb = max(jb, r * 64);
                 const float4 bxy = s_rec[lb], bco = s_rec[BATCH + lb], bcol = s_rec[2 * BATCH + lb];
                 blend(j, axy, aco, acol);
-                if (jb < 0 || __all(live == 0.0f)) break;
+                if (--left == 0) break;
                 j = take();
-                const int la = j >= 0 ? j : jb;
+                const int la = max(j, r * 64);
                 axy = s_rec[la];
                 aco = s_rec[BATCH + la];
                 acol = s_rec[2 * BATCH + la];
                 blend(jb, bxy, bco, bcol);
-                if (j < 0 || __all(live == 0.0f)) break;
+                if (--left == 0 || __all(live == 0.0f)) break;
             }
             if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
         }
