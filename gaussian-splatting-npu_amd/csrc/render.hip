@@ -257,7 +257,10 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
     const uint2 range = a.ranges[tile];
     const int todo = (int)(range.y - range.x);
 
-    __shared__ float4 s_rec[BATCH * 3];
+    // one record of padding in front: the walk's look-ahead past a round's last entry reads
+    // s_rec[r * 64 - 1] (unused), which for r = 0 is that pad
+    __shared__ float4 s_recp[1 + BATCH * 3];
+    float4* const s_rec = s_recp + 1;
     __shared__ uint8_t s_mask[BATCH];
     // per wave and 64-entry round of a batch: bit i = entry (round, i) contributed to some pixel of
     // the wave's quadrant (kept in scalar registers during the round, stored once per round)
@@ -343,7 +346,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 last_contributor = blended ? (uint32_t)(base + j + 1) : last_contributor;
             };
             // cnt entries to walk (rem != 0): a counted loop, so take() needs no end test; the
-            // look-ahead take() past the last entry returns -1, clamped to a valid record (unused).
+            // look-ahead take() past the last entry returns r * 64 - 1 (a record it never uses).
             // The all-finished exit is tested every second entry (blending into finished pixels
             // is a no-op), at the end of each two-entry turn.
             int left = __popcll(rem);
@@ -351,15 +354,13 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             float4 axy = s_rec[j], aco = s_rec[BATCH + j], acol = s_rec[2 * BATCH + j];
             while (true) {
                 const int jb = take();
-                const int lb = max(jb, r * 64);
-                const float4 bxy = s_rec[lb], bco = s_rec[BATCH + lb], bcol = s_rec[2 * BATCH + lb];
+                const float4 bxy = s_rec[jb], bco = s_rec[BATCH + jb], bcol = s_rec[2 * BATCH + jb];
                 blend(j, axy, aco, acol);
                 if (--left == 0) break;
                 j = take();
-                const int la = max(j, r * 64);
-                axy = s_rec[la];
-                aco = s_rec[BATCH + la];
-                acol = s_rec[2 * BATCH + la];
+                axy = s_rec[j];
+                aco = s_rec[BATCH + j];
+                acol = s_rec[2 * BATCH + j];
                 blend(jb, bxy, bco, bcol);
                 if (--left == 0 || __all(live == 0.0f)) break;
             }
