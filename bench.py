@@ -15,7 +15,12 @@ view v on rank v mod N -- 8 views on one GPU, 1 view + the all-reduce per GPU at
 and N=8 lines describe the same 8-view step.  `--views-per-rank K` (weak scaling): K views per
 rank at every N, the same K at N=1.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
+Run: python bench.py [--gpus N --steps K --warmup W].  With N > 1 and no WORLD_SIZE in the
+environment, this process runs the PMC passes (rank 0's workload) and then starts
+`python -m torch.distributed.run --nproc-per-node N ... bench.py ...` as a child (it never
+touches the GPU itself, and never re-execs), relays rank 0's JSON line and exits with the child's
+code; under an external torch.distributed.run WORLD_SIZE must equal N.  One rank per GPU over RCCL
+("nccl"); GSR_DIST_BACKEND=gloo is the one-GPU rehearsal of the same ranks.
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -48,7 +53,7 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2  # 1,228.8 G wave-instructions/s
 N_RING = 8  # distinct ring cameras (synthetic.Camera)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -93,7 +98,11 @@ def parse():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)  # workload under a --pmc pass
     # the pmc child of rank 0 of an N-rank run (started before the process group): rank 0's views
     ap.add_argument("--pmc-world", type=int, default=0, help=argparse.SUPPRESS)
-    return ap.parse_args()
+    # the ranks' copy of the launcher's PMC figures (JSON file), read by rank 0
+    ap.add_argument("--pmc-file", default="", help=argparse.SUPPRESS)
+    # launch check (CPU test): each rank prints {"rank", "world", "local_rank"} and exits, no GPU
+    ap.add_argument("--rank-probe", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
 def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1):
@@ -208,8 +217,77 @@ def single_view_leg(args, timeout=400):
         return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
 
-def main():
-    args = parse()
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(args, argv, port, pmc_file=None):
+    """The child command of `bench.py --gpus N` (N > 1): torch.distributed.run with one rank per
+    GPU on this node, each rank running this script with the same arguments (`argv`), plus the
+    launcher's PMC figures for rank 0 (or --no-pmc when there are none)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    if pmc_file:
+        cmd += ["--pmc-file", pmc_file]
+    elif "--no-pmc" not in argv:
+        cmd.append("--no-pmc")
+    return cmd
+
+
+def launch_ranks(args, argv, timeout=3000):
+    """`bench.py --gpus N` without WORLD_SIZE: the PMC passes of rank 0's workload first (child
+    processes under rocprofv3, before any rank exists), then N ranks through torch.distributed.run
+    as ONE child process of this one -- this process never initialises the GPU and never re-execs.
+    The ranks inherit stdout, so rank 0's JSON line is the line this command prints; returns the
+    child's exit code."""
+    backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        ndev = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs for RCCL, this node has {ndev} "
+                  "(GSR_DIST_BACKEND=gloo rehearses the ranks on fewer)", file=sys.stderr)
+            return 2
+    pmc_file = None
+    if not args.pmc_child and not args.no_pmc and not args.no_profile and not args.rank_probe:
+        pmc = pmc_traffic(args, args.gpus)
+        if pmc is not None:
+            fd, pmc_file = tempfile.mkstemp(prefix="gsr_pmc_", suffix=".json")
+            with os.fdopen(fd, "w") as f:
+                json.dump(pmc, f)
+    cmd = rank_launch_cmd(args, argv, free_port(), pmc_file)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    proc = subprocess.Popen(cmd, cwd=ROOT, env=env, start_new_session=True)
+    try:
+        return proc.wait(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(proc.pid, 9)
+        proc.wait()
+        print(f"bench.py: the {args.gpus}-rank run exceeded {timeout} s", file=sys.stderr)
+        return 124
+    finally:
+        if pmc_file:
+            os.unlink(pmc_file)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if not args.pmc_child:
+        if env_world is None and args.gpus > 1:
+            sys.exit(launch_ranks(args, argv))
+        if env_world is not None and int(env_world) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
+            sys.exit(2)
+    if args.rank_probe:
+        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "argv": argv}), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -219,7 +297,10 @@ def main():
     # PMC passes of this rank's workload, on rank 0 only, before the process group exists and before
     # this process touches the GPU (the child replays rank 0's views of the N-rank step)
     pmc = None
-    if rank == 0 and not args.pmc_child and not args.no_pmc and not args.no_profile:
+    if rank == 0 and args.pmc_file:  # measured by the `--gpus N` launcher before the ranks started
+        with open(args.pmc_file) as f:
+            pmc = json.load(f)
+    elif rank == 0 and not args.pmc_child and not args.no_pmc and not args.no_profile:
         pmc = pmc_traffic(args, world)
     # GSR_DIST_BACKEND=gloo (rehearsal only): several ranks on one GPU exercise the N>1 path of
     # this script on a one-GPU box; the driver's multi-GPU runs use the default, RCCL ("nccl").
@@ -527,15 +608,17 @@ def main():
                "sparse_adam": aux_sparse_adam(dgr, params, cams[0], grads[0], args),
                "train_iteration": aux_train_iteration(dgr, params, cams[0], H, W)}
 
+    coll = "RCCL (nccl)" if backend == "nccl" else f"{backend} (one-GPU rehearsal, not RCCL)"
     if mode == "strong":
         workload = (f"BASELINE config 4: {args.views_total} views per step of config 2 ({P} Gaussians, SH deg 3, "
                     f"{W}x{H}, fwd+bwd each), view v on rank v mod {world}"
-                    + ((", one RCCL grad all-reduce per step" + (f" overlapped with the backward ({args.allreduce_chunks} "
-                                                                  "Gaussian ranges)" if overlap_ar else ""))
+                    + ((f", one {coll} grad all-reduce per step" + (f" overlapped with the backward "
+                                                                     f"({args.allreduce_chunks} Gaussian ranges)"
+                                                                     if overlap_ar else ""))
                        if world > 1 else ", grads accumulated on one GPU"))
     else:
         workload = (f"{args.views_per_rank} views per rank per step of config 2 ({P} Gaussians, SH deg 3, {W}x{H}, "
-                    f"fwd+bwd each)" + (", one RCCL grad all-reduce per step" if world > 1 else ""))
+                    f"fwd+bwd each)" + (f", one {coll} grad all-reduce per step" if world > 1 else ""))
     res = {
         "metric": "rendered Mpix/s fwd+bwd, 1M Gaussians @1080p",
         "value": round(value, 2),
@@ -554,6 +637,8 @@ def main():
         "config": {"workload": workload, "P": P, "width": W, "height": H, "views_per_step": views_step,
                    "views_per_rank": len(views), "num_rendered": L, "num_rendered_per_view": Ls,
                    "visible": P_vis, "antialiasing": args.antialiasing, "parallelism": f"views-dp{world}",
+                   "backend": backend if world > 1 else None,
+                   "forward_views_reruns": dgr._C.views_reruns,
                    "execution": ("one MultiViewRasterizer batch: the binning prefix of all views batched "
                                  "(one launch per stage, grid.y = view), then every view's render forward, every "
                                  "view's render backward, one preprocess backward for the batch"

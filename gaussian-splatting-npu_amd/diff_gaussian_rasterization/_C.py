@@ -87,6 +87,7 @@ _contig_cache = {}  # small non-contiguous inputs (the transposed view matrices)
 # (the reference's binningBuffer resize lambda, rasterize_points.cu:27-33, rasterizer_impl.cu:286).
 _binning_hint = {}
 _binning_hint_views = {}  # per device: the last view batch's num_rendered per view
+views_reruns = 0  # batched forwards that outgrew their binning buffers and ran a second time
 
 
 def _contiguous(t):
@@ -254,14 +255,13 @@ def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rota
     gsz, isz = lib.gsr_geometry_buffer_size(P), lib.gsr_image_buffer_size(W, H)
     geoms = [torch.empty((gsz,), dtype=torch.uint8, device=dev) for _ in range(V)]
     imgs = [torch.empty((isz,), dtype=torch.uint8, device=dev) for _ in range(V)]
-    # per-view capacity from that view's last num_rendered (a batch of the same V views: the previous
-    # step's batch), else from the largest of them: the views' buffers (kept alive by autograd
-    # until the backward) stay within 25 % + 64K instances of what each view needs
+    # every view's capacity from the LARGEST num_rendered of the previous batch on this device (+25 %
+    # and 64K instances): the hint is not keyed by camera, and a training loop deals different
+    # cameras to the batch's slots every step, so a per-slot hint would overflow (and rerun the
+    # whole batch) whenever a slot's new view renders more than its old one did
     hints = _binning_hint_views.get(dev)
-    if hints is None or len(hints) != V:
-        h = _binning_hint.get(dev) if hints is None else max(hints)
-        hints = None if h is None else [h] * V
-    caps = [lib.gsr_binning_buffer_size(min(int(h * 1.25) + 65536, 0x7FFFFFFF)) for h in hints] if hints else [0] * V
+    h = max(hints) if hints else _binning_hint.get(dev)
+    caps = [lib.gsr_binning_buffer_size(min(int(h * 1.25) + 65536, 0x7FFFFFFF))] * V if h is not None else [0] * V
     bins = [torch.empty((c,), dtype=torch.uint8, device=dev) if c else None for c in caps]
     bg_p, means_p = p(background, "bg"), p(means3D, "means3D")
     colors_p, op_p = p(colors, "colors_precomp"), p(opacity, "opacities")
@@ -289,6 +289,8 @@ def rasterize_gaussians_views(background, means3D, colors, opacity, scales, rota
     if all(rendered[v] for v in range(V)):
         bins = [bins[v][:lib.gsr_binning_buffer_size(Ls[v])] for v in range(V)]  # views: the backward re-derives
     else:  # first call on this device, or the scene grew past the headroom: the batch again, exact buffers
+        global views_reruns
+        views_reruns += 1
         bins = [torch.empty((lib.gsr_binning_buffer_size(L),), dtype=torch.uint8, device=dev) for L in Ls]
         run([b.numel() for b in bins])
         if not all(rendered[v] for v in range(V)) or [int(nr[v]) for v in range(V)] != Ls:

@@ -67,17 +67,37 @@ def grad_chunk_hook(chunks, fn, done):
 _grad_chunks = None  # the active grad_chunk_hook (process-wide)
 
 
+_hook_busy = threading.Lock()  # one hooked backward in flight at a time (collective order)
+
+
 def _chunk_hook(wanted):
-    """(on_chunk for _C, done) from the active grad_chunk_hook, restricted to the gradients of the
-    inputs in `wanted` (names); (None, None) outside the context."""
+    """(on_chunk for _C, finish) from the active grad_chunk_hook, restricted to the gradients of
+    the inputs in `wanted` (names); (None, None) outside the context.  finish() runs the hook's
+    done() once -- the caller calls it in a `finally`, so a backward that fails after issuing
+    collectives still waits for them -- and releases the hook for the next backward.  A second
+    hooked backward while one is in flight (another thread or device of this process) would issue
+    collectives in an order the other ranks do not match: it raises instead."""
     h = _grad_chunks
     if h is None or not wanted:
         return None, None
     chunks, fn, done = h
+    if not _hook_busy.acquire(blocking=False):
+        raise RuntimeError("grad_chunk_hook: a hooked batched backward is already in flight in this process; "
+                           "concurrent hooked backward passes would issue collectives out of order across ranks")
+    finished = []
 
     def on(g0, g1, grads):
         fn(g0, g1, {k: t for k, t in grads.items() if k in wanted and t.numel()})
-    return (chunks, on), done
+
+    def finish():
+        if finished:
+            return
+        finished.append(True)
+        try:
+            done()
+        finally:
+            _hook_busy.release()
+    return (chunks, on), finish
 
 
 # Per device: an event recorded after the last backward run inside accumulate_grads_in_place.
@@ -148,25 +168,33 @@ class _DeferredBatch:
                 t.record_stream(stream)
         inputs = {"means3D": c_m3, "dc": c_dc, "sh": c_sh, "opacities": c_op, "scales": c_sc, "rotations": c_rot,
                   "cov3D_precomp": c_cov, "colors_precomp": c_col}
-        accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in inputs.items()) if g is not None}
-        if "dc" in accumulate and (dc is None or dc.numel() == 0):
-            del accumulate["dc"]
-        fence = _acc_fence.get(dev)
-        if accumulate and fence is not None:
-            stream.wait_event(fence)
-        for g in accumulate.values():
-            g.record_stream(stream)
         on_chunk, done = _chunk_hook({k for k, t in inputs.items()
                                       if t is not None and t.numel() and t.requires_grad})
-        grads = _C.rasterize_gaussians_preprocess_backward_views(
-            means3D, [v["radii"] for v in views], colors_precomp, opacities, scales, rotations, s0.scale_modifier,
-            cov3Ds_precomp, [v["settings"].viewmatrix for v in views], [v["settings"].projmatrix for v in views],
-            [v["settings"].tanfovx for v in views], [v["settings"].tanfovy for v in views], s0.image_height,
-            s0.image_width, sh, s0.sh_degree, [v["settings"].campos for v in views], [v["geom"] for v in views],
-            [v["num_rendered"] for v in views], [v["binning"] for v in views], any(v["has_inv"] for v in views),
-            s0.antialiasing, s0.debug, dc=dc, accumulate=accumulate, on_chunk=on_chunk)
-        if done is not None:
-            done()
+        try:
+            # under a chunk hook (overlapped all-reduce) the gradients go into FRESH buffers, which the
+            # hook reduces, and reach an existing .grad by autograd's add below: adding into a .grad
+            # that already holds reduced gradients (an earlier launch group, a late view) and then
+            # reducing it again would multiply those by the world size
+            accumulate = {} if on_chunk is not None else {
+                k: g for k, g in ((k, _accumulation_target(t)) for k, t in inputs.items()) if g is not None}
+            if "dc" in accumulate and (dc is None or dc.numel() == 0):
+                del accumulate["dc"]
+            fence = _acc_fence.get(dev)
+            if accumulate and fence is not None:
+                stream.wait_event(fence)
+            for g in accumulate.values():
+                g.record_stream(stream)
+            grads = _C.rasterize_gaussians_preprocess_backward_views(
+                means3D, [v["radii"] for v in views], colors_precomp, opacities, scales, rotations,
+                s0.scale_modifier, cov3Ds_precomp, [v["settings"].viewmatrix for v in views],
+                [v["settings"].projmatrix for v in views], [v["settings"].tanfovx for v in views],
+                [v["settings"].tanfovy for v in views], s0.image_height, s0.image_width, sh, s0.sh_degree,
+                [v["settings"].campos for v in views], [v["geom"] for v in views], [v["num_rendered"] for v in views],
+                [v["binning"] for v in views], any(v["has_inv"] for v in views), s0.antialiasing, s0.debug, dc=dc,
+                accumulate=accumulate, on_chunk=on_chunk)
+        finally:
+            if done is not None:
+                done()
         ev = torch.cuda.Event()
         ev.record(stream)
         _acc_fence[dev] = ev
@@ -451,8 +479,15 @@ class _RasterizeViews(torch.autograd.Function):
         if grad_colors is None:
             grad_colors = torch.zeros((V, 3, s0.image_height, s0.image_width), dtype=torch.float32,
                                       device=means3D.device)
+        # inputs of forward(): means3D 0, sh 2, colors_precomp 3, opacities 4, scales 5, rotations 6,
+        # cov3D_precomp 7, dc 9
+        names = {0: "means3D", 2: "sh", 3: "colors_precomp", 4: "opacities", 5: "scales", 6: "rotations",
+                 7: "cov3D_precomp", 9: "dc"}
+        on_chunk, done = _chunk_hook({n for i, n in names.items() if ctx.needs_input_grad[i]})
         accumulate = None
-        if ctx.acc_inputs is not None:
+        # no in-place accumulation under a chunk hook: the hook reduces what the kernel writes, and an
+        # existing .grad may already hold reduced gradients (see _DeferredBatch._launch)
+        if ctx.acc_inputs is not None and on_chunk is None:
             accumulate = {k: g for k, g in ((k, _accumulation_target(t)) for k, t in ctx.acc_inputs.items())
                           if g is not None}
             if "dc" in accumulate and (dc is None or dc.numel() == 0):
@@ -464,20 +499,17 @@ class _RasterizeViews(torch.autograd.Function):
                 stream.wait_event(fence)
             for g in accumulate.values():
                 g.record_stream(stream)
-        # inputs of forward(): means3D 0, sh 2, colors_precomp 3, opacities 4, scales 5, rotations 6,
-        # cov3D_precomp 7, dc 9
-        names = {0: "means3D", 2: "sh", 3: "colors_precomp", 4: "opacities", 5: "scales", 6: "rotations",
-                 7: "cov3D_precomp", 9: "dc"}
-        on_chunk, done = _chunk_hook({n for i, n in names.items() if ctx.needs_input_grad[i]})
-        grads = _C.rasterize_gaussians_backward_views(
-            s0.bg, means3D, [radii[v] for v in range(V)], colors_precomp, opacities, scales, rotations,
-            s0.scale_modifier, cov3Ds_precomp, [s.viewmatrix for s in ss], [s.projmatrix for s in ss],
-            [s.tanfovx for s in ss], [s.tanfovy for s in ss], grad_colors, grad_invdepths, sh, s0.sh_degree,
-            [s.campos for s in ss], bufs[0::3], ctx.num_rendered, bufs[1::3], bufs[2::3], s0.antialiasing, s0.debug,
-            dc=dc, accumulate=accumulate, on_chunk=on_chunk)
-        if done is not None:
-            done()
-        if ctx.acc_inputs is not None:
+        try:
+            grads = _C.rasterize_gaussians_backward_views(
+                s0.bg, means3D, [radii[v] for v in range(V)], colors_precomp, opacities, scales, rotations,
+                s0.scale_modifier, cov3Ds_precomp, [s.viewmatrix for s in ss], [s.projmatrix for s in ss],
+                [s.tanfovx for s in ss], [s.tanfovy for s in ss], grad_colors, grad_invdepths, sh, s0.sh_degree,
+                [s.campos for s in ss], bufs[0::3], ctx.num_rendered, bufs[1::3], bufs[2::3], s0.antialiasing,
+                s0.debug, dc=dc, accumulate=accumulate, on_chunk=on_chunk)
+        finally:
+            if done is not None:
+                done()
+        if accumulate is not None:
             ev = torch.cuda.Event()
             ev.record(stream)
             _acc_fence[dev] = ev

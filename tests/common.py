@@ -28,12 +28,13 @@ FLIP_MAX_ABS = 5e-3
 PARITY_LOG = []
 
 
-def check_render(name, hip, ora):
+def check_render(name, hip, ora, flips=None):
     """hip / ora: dicts with 'color' (3,H,W), 'invdepth' (1,H,W) and optionally 'final_T' (N)
     and 'n_contrib' (N).  Flipped pixels: n_contrib differs (when both have it) or some
     colour / invdepth / final_T value is off by more than IMG_ATOL.  Asserts: flipped fraction
     <= FLIP_FRACTION, every value of a flipped pixel within FLIP_MAX_ABS (final_T within
-    1/255 + IMG_ATOL), all others within IMG_ATOL with the same n_contrib."""
+    1/255 + IMG_ATOL), all others within IMG_ATOL with the same n_contrib.  `flips`: a list that
+    receives the flipped pixels' mask (bool (N,)), for flip_gaussians."""
     c = np.abs(np.asarray(hip["color"], np.float64) - np.asarray(ora["color"], np.float64))
     N = c.shape[-1] * c.shape[-2]
     err = c.reshape(c.shape[0], N).max(0)
@@ -52,6 +53,8 @@ def check_render(name, hip, ora):
         nc_diff = int(d.sum())
         flip |= d
     n_flip = int(flip.sum())
+    if flips is not None:
+        flips.append(flip)
     stats = {"name": name, "pixels": N, "flipped": n_flip, "frac": n_flip / max(N, 1), "n_contrib_diff": nc_diff,
              "max_err_flipped": float(err[flip].max()) if n_flip else 0.0,
              "max_err_other": float(err[~flip].max()) if n_flip < N else 0.0,
@@ -132,3 +135,64 @@ def allclose_rel(a, b, rtol=GRAD_RTOL, atol=GRAD_ATOL):
     scale = max(np.abs(b).max() if b.size else 0.0, 1e-30)
     err = np.abs(a - b)
     return bool(np.all(err <= rtol * scale + atol)), float(err.max() / scale if err.size else 0.0)
+
+
+# ---- attribution of gradient outliers to flipped pixels -------------------
+# A flipped pixel (check_render) changes the blend of every Gaussian its walk passes: the reference's
+# backward replays the pixel's list from its n_contrib down (backward.cu:452-638), and dL/dalpha of
+# each of those Gaussians holds the colour behind it and T in front of it (forward.cu:359-370: one
+# Gaussian blended or skipped at the 1/255 threshold, or the stop rule firing one entry earlier or
+# later, shifts both).  The Gaussians at list positions [0, max(n_contrib_hip, n_contrib_oracle))
+# of a flipped pixel's tile are the only ones whose gradients a flip can move.  Every gradient
+# element beyond GRAD_RTOL of max|ref| (or beyond REL_OUT relative to itself) must belong to such
+# a Gaussian; outside that set the plain tolerance holds, inside it GRAD_RTOL_ATTRIBUTED.
+GRAD_RTOL_ATTRIBUTED = 2e-3
+
+
+def flip_gaussians(flip, nc_hip, nc_ora, vals, ranges, W, H, P):
+    """bool (P,): the Gaussians in the walk of some flipped pixel (flip: bool (N,) from
+    check_render; nc_*: n_contrib (N,); vals / ranges: the oracle's sorted Gaussian ids and
+    per-tile [start, end) ranges)."""
+    out = np.zeros(P, dtype=bool)
+    tiles_x = (W + 15) // 16
+    vals = np.asarray(vals)
+    ranges = np.asarray(ranges).reshape(-1, 2)
+    nc_hip = np.asarray(nc_hip).reshape(-1)
+    nc_ora = np.asarray(nc_ora).reshape(-1)
+    for pix in np.flatnonzero(np.asarray(flip).reshape(-1)):
+        y, x = divmod(int(pix), W)
+        t = (y // 16) * tiles_x + x // 16
+        start, end = int(ranges[t, 0]), int(ranges[t, 1])
+        n = min(max(int(nc_hip[pix]), int(nc_ora[pix])), end - start)
+        out[vals[start:start + n]] = True
+    return out
+
+
+def check_grad_attributed(name, hip, ref, affected, rtol_attr=GRAD_RTOL_ATTRIBUTED):
+    """Per-Gaussian gradient (P, ...) against the oracle with outliers attributed to flips:
+    rows (Gaussians) holding an element beyond GRAD_RTOL * max|ref| + GRAD_ATOL, or beyond REL_OUT
+    relative to |ref| where |ref| > REL_FLOOR * max|ref|, must lie in `affected` (flip_gaussians);
+    every element of an affected row within rtol_attr * max|ref|.  Logs the attributed and
+    unattributed counts; asserts no unattributed row."""
+    P = affected.shape[0]
+    a = np.asarray(hip, np.float64).reshape(P, -1)
+    b = np.asarray(ref, np.float64).reshape(P, -1)
+    scale = max(float(np.abs(b).max()) if b.size else 0.0, 1e-30)
+    err = np.abs(a - b)
+    over = err > GRAD_RTOL * scale + GRAD_ATOL
+    sel = np.abs(b) > REL_FLOOR * scale
+    with np.errstate(divide="ignore", invalid="ignore"):
+        over_rel = sel & (err > REL_OUT * np.abs(b))
+    rows = (over | over_rel).any(axis=1)
+    unattr = rows & ~affected
+    st = {"name": name + " attributed", "elements": int(err.size), "affected_gaussians": int(affected.sum()),
+          "rows_over": int(rows.sum()), "attributed_rows": int((rows & affected).sum()),
+          "unattributed_rows": int(unattr.sum()),
+          "max_rel_to_max_outside": float(err[~affected].max() / scale) if (~affected).any() else 0.0,
+          "max_rel_to_max_inside": float(err[affected].max() / scale) if affected.any() else 0.0}
+    PARITY_LOG.append(st)
+    assert st["unattributed_rows"] == 0, (
+        f"{name}: {st['unattributed_rows']} Gaussians off beyond tolerance outside every flipped pixel's walk "
+        f"(rows {np.flatnonzero(unattr)[:8].tolist()}, {st})")
+    assert st["max_rel_to_max_inside"] <= rtol_attr, f"{name}: attributed error too large ({st})"
+    return st
