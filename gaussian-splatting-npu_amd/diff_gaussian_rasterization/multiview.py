@@ -213,6 +213,41 @@ def inverse_sigmoid(x):
     return torch.log(x / (1 - x))
 
 
+def view_from_camera(cam, bg, sh_degree=3, scale_modifier=1.0, debug=False, antialiasing=False, cam_index=None,
+                     device=None):
+    """One training view for DataParallelTrainer from a reference camera (scene/cameras.py Camera,
+    or MiniCam plus `original_image`): (GaussianRasterizationSettings, ground-truth image, extras),
+    the settings exactly as gaussian_renderer/__init__.py:32-50 builds them (tan of half the FoV,
+    int image size, world_view_transform / full_proj_transform / camera_center, prefiltered False),
+    and the extras train.py:113-141 reads from the camera: `alpha_mask` (the image is multiplied by
+    it), `invdepth` + `depth_mask` only when `depth_reliable` (the depth L1 term), and `cam` =
+    `cam_index` for the per-camera exposure.  `bg` (3,) on the device, as train.py's background."""
+    import math
+    import diff_gaussian_rasterization as dgr
+    dev = device if device is not None else bg.device
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=int(cam.image_height), image_width=int(cam.image_width), tanfovx=math.tan(cam.FoVx * 0.5),
+        tanfovy=math.tan(cam.FoVy * 0.5), bg=bg, scale_modifier=scale_modifier,
+        viewmatrix=cam.world_view_transform.to(dev), projmatrix=cam.full_proj_transform.to(dev), sh_degree=sh_degree,
+        campos=cam.camera_center.to(dev), prefiltered=False, debug=debug, antialiasing=antialiasing)
+    extras = {}
+    alpha = getattr(cam, "alpha_mask", None)
+    if alpha is not None:
+        extras["alpha_mask"] = alpha.to(dev)
+    if getattr(cam, "depth_reliable", False) and getattr(cam, "invdepthmap", None) is not None:
+        extras["invdepth"] = cam.invdepthmap.to(dev)
+        extras["depth_mask"] = cam.depth_mask.to(dev)
+    if cam_index is not None:
+        extras["cam"] = cam_index
+    return settings, cam.original_image.to(dev), extras
+
+
+def views_from_cameras(cameras, bg, sh_degree=3, **kw):
+    """view_from_camera over a Scene's train cameras (scene.getTrainCameras()), the camera's index
+    in the list as its exposure index (train.py's `vind`, gaussian_model.py:175-176)."""
+    return [view_from_camera(c, bg, sh_degree, cam_index=i, **kw) for i, c in enumerate(cameras)]
+
+
 class OptimizationDefaults:
     """The densification / schedule fields of arguments/__init__.py OptimizationParams (:74-100)
     that train.py's iteration reads."""

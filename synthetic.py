@@ -67,13 +67,20 @@ def ring_camera_RT(view, n_views=8, radius=4.0, height=-0.5):
 class Camera:
     """Minimal stand-in for scene/cameras.py::Camera (matrix part only)."""
 
-    def __init__(self, width, height, view=0, n_views=8, fovy_deg=50.0, znear=0.01, zfar=100.0):
+    def __init__(self, width, height, view=0, n_views=8, fovy_deg=50.0, znear=0.01, zfar=100.0, R=None, T=None,
+                 fovx=None, fovy=None):
+        """A ring view (`view` of `n_views`), or -- with R, T, fovx, fovy -- the camera of a dataset
+        (scene/cameras.py:19-89: R camera-to-world rotation as the readers store it, T the
+        world-to-camera translation, trans 0, scale 1)."""
         self.image_width = int(width)
         self.image_height = int(height)
-        self.FoVy = math.radians(fovy_deg)
-        self.FoVx = 2.0 * math.atan(math.tan(self.FoVy * 0.5) * width / height)
+        if R is None:
+            self.FoVy = math.radians(fovy_deg)
+            self.FoVx = 2.0 * math.atan(math.tan(self.FoVy * 0.5) * width / height)
+            R, T = ring_camera_RT(view, n_views)
+        else:
+            self.FoVx, self.FoVy = float(fovx), float(fovy)
         self.znear, self.zfar = znear, zfar
-        R, T = ring_camera_RT(view, n_views)
         self.R, self.T = R, T
         self.world_view_transform = torch.tensor(get_world2view2(R, T)).transpose(0, 1)
         self.projection_matrix = get_projection_matrix(znear, zfar, self.FoVx, self.FoVy).transpose(0, 1)

@@ -3,7 +3,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "gaussian-splatting-npu_amd"), os.path.join(ROOT, "oracle"),
-          os.path.join(ROOT, "tests")):
+          os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

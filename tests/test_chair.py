@@ -1,0 +1,59 @@
+"""The NeRF-synthetic chair fixture (tests/golden/nerf_chair.npz, make_chair.py) on CPU: the C
+oracle re-run from the committed inputs reproduces the committed digests (so the GPU test's oracle
+run on the box is the one generated here), with a different thread count than the generator's."""
+import os
+
+import numpy as np
+import pytest
+
+import nerf_synthetic as ns
+
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nerf_chair.npz")
+
+
+def load_chair():
+    """(fixture dict, activated Gaussians, [cases: (camera, sh_degree, antialiasing, bg, grad_seed)])."""
+    import make_chair
+    f = dict(np.load(FIX))
+    scene = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"])
+    cases = []
+    for i, (frame, deg, aa, bg) in enumerate(make_chair.CASES):
+        cam = ns.camera(f["R"][frame], f["T"][frame], float(f["fovx"][frame]), float(f["fovy"][frame]),
+                        int(f["width"]), int(f["height"]))
+        cases.append((cam, deg, aa, bg, 100 + i))
+    return f, scene, cases
+
+
+def test_chair_inputs():
+    f, scene, cases = load_chair()
+    assert f["xyz"].shape == (100_000, 3) and f["rgb"].shape == (100_000, 3)
+    assert np.all(np.abs(f["xyz"]) <= 1.3)  # the dataset's initial cloud: U(-1.3, 1.3)^3
+    assert np.all(f["dist2"] > 0)
+    # create_from_pcd: identity rotations, opacity 0.1, isotropic scales sqrt(dist2)
+    assert np.all(scene["rotations"].numpy() == np.array([1, 0, 0, 0], np.float32))
+    np.testing.assert_allclose(scene["opacities"].numpy(), 0.1, rtol=1e-6)
+    np.testing.assert_allclose(scene["scales"][:, 0].numpy() ** 2, np.maximum(f["dist2"], 1e-7), rtol=1e-5)
+    for cam, *_ in cases:
+        # a camera on the Blender sphere (radius ~4.03) looking at the origin: the origin projects
+        # near the image centre, in front of the camera
+        c = cam.camera_center.numpy()
+        assert 3.9 < np.linalg.norm(c) < 4.2
+        p = np.array([0, 0, 0, 1], np.float32) @ cam.full_proj_transform.numpy()
+        assert p[3] > 0 and abs(p[0] / p[3]) < 0.2 and abs(p[1] / p[3]) < 0.2
+
+
+@pytest.mark.parametrize("case", [0])
+def test_chair_oracle_reproduces_digests(case):
+    import make_chair
+    f, scene, cases = load_chair()
+    cam, deg, aa, bg, seed = cases[case]
+    o, g = make_chair.run_case(scene, cam, deg, aa, bg, seed, nthreads=3)
+    d = make_chair.digests(o, g)
+    for k, v in d.items():
+        want = f[f"case{case}_{k}"]
+        if k.startswith("sha") or k == "num_rendered":
+            assert str(v) == str(want), k
+        else:  # the oracle's backward sums per Gaussian in thread-count-dependent order
+            scale = float(f[f"case{case}_abs" + k[len("abs"):]] if k.startswith("abs")
+                          else f[f"case{case}_abs{k}"])
+            assert abs(float(v) - float(want)) <= 1e-6 * scale, (k, v, want)

@@ -343,14 +343,21 @@ def _oworker(rank, port, q):
             grads.append(tuple(g.to(dev) for g in synthetic.make_grads(O_H, O_W, seed=1 + v)))
         out = {}
         log = open(os.path.join(root, "gpurun_out", f"overlap_rank{rank}.log"), "w")
-        for mode in ("plain", "overlap", "deferred_overlap"):
+        for mode in ("plain", "overlap", "deferred_overlap", "deferred_overlap_18"):
             print(f"rank {rank} mode {mode} start", file=log, flush=True)
             params = {k: v.to(dev).clone().requires_grad_(True) for k, v in scene.items()}
+            reps = 1
+            if mode == "deferred_overlap_18":
+                # 18 views per rank: two batched launches (16 + 2), into a .grad that already holds
+                # gradients -- each launch's own contribution is reduced once
+                reps = 9
+                for p_ in params.values():
+                    p_.grad = torch.full_like(p_, 0.5)
             ctx = multiview.overlapped_allreduce(chunks=3) if mode != "plain" else contextlib.nullcontext()
             with ctx as st:
-                if mode == "deferred_overlap":
+                if mode.startswith("deferred_overlap"):
                     with dgr.deferred_backward():
-                        for s, (gc, gi) in zip(settings, grads):
+                        for s, (gc, gi) in zip(settings * reps, grads * reps):
                             m2 = torch.zeros_like(params["means3D"], requires_grad=True)
                             c, _, i = dgr.GaussianRasterizer(s)(means2D=m2, **{
                                 "means3D": params["means3D"], "shs": params["shs"], "opacities": params["opacities"],
@@ -365,6 +372,8 @@ def _oworker(rank, port, q):
                                                      torch.stack([g[1] for g in grads])])
             if mode == "plain":
                 multiview.allreduce_grads(params)
+            elif mode == "deferred_overlap_18":
+                assert st["chunks"] == 6 and st["collectives"] == 30, st
             else:
                 assert st["chunks"] == 3 and st["collectives"] == 15, st
             torch.cuda.synchronize()
@@ -400,3 +409,8 @@ def test_overlapped_allreduce_equals_allreduce_after_backward():
                                           err_msg=f"rank {rank} deferred {k}")
             ok = np.abs(out["deferred_overlap"][k] - ref[k]).max() <= 1e-5 * np.abs(ref[k]).max() + 1e-9
             assert ok, f"rank {rank} deferred vs batch {k}"
+            # 9 copies of the step's views in two launch groups on top of a .grad of 0.5: 0.5 + 9 x
+            # the reduced gradient (not multiplied by the world size anywhere)
+            want = 0.5 + 9.0 * ref[k].astype(np.float64)
+            err = np.abs(out["deferred_overlap_18"][k] - want).max()
+            assert err <= 1e-5 * np.abs(want).max() + 1e-6, f"rank {rank} 18 views {k}: {err}"

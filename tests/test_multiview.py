@@ -209,9 +209,12 @@ def test_views_of_batch_strong_scaling(world):
 
 
 # ---- densification surgery (DataParallelTrainer.densify_and_prune / reset_opacity) on CPU ------
-def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_size, gen, pd=0.01, N=2):
+def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_size, gen, pd=0.01, N=2, normal=None,
+                 counts=None):
     """gaussian_model.py:315-469 step by step on dicts (the reference's own sequence: clone's
-    postfix, split's postfix, split prune, final prune; tensors and Adam moments)."""
+    postfix, split's postfix, split prune, final prune; tensors and Adam moments).  `normal(stds)`:
+    the split's samples (default: torch.normal on `gen`); `counts`: a dict that receives the
+    cloned / split / pruned counts."""
     names = ("xyz", "f_dc", "f_rest", "opacity", "scaling", "rotation")
     T = {k: raw[k].clone() for k in names}
     S = {k: {"exp_avg": state[k][0].clone(), "exp_avg_sq": state[k][1].clone()} for k in names}
@@ -231,6 +234,7 @@ def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_si
     # densify_and_clone
     sel = torch.where(torch.norm(grads, dim=-1) >= max_grad, True, False)
     sel = torch.logical_and(sel, torch.max(torch.exp(T["scaling"]), dim=1).values <= pd * extent)
+    n_clone = int(sel.sum())
     cat({k: T[k][sel] for k in names})
     # densify_and_split
     n_init = T["xyz"].shape[0]
@@ -239,7 +243,8 @@ def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_si
     sel = torch.where(padded >= max_grad, True, False)
     sel = torch.logical_and(sel, torch.max(torch.exp(T["scaling"]), dim=1).values > pd * extent)
     stds = torch.exp(T["scaling"])[sel].repeat(N, 1)
-    samples = torch.normal(mean=torch.zeros((stds.size(0), 3)), std=stds, generator=gen)
+    samples = normal(stds) if normal is not None else torch.normal(mean=torch.zeros((stds.size(0), 3)), std=stds,
+                                                                    generator=gen)
     rots = multiview.build_rotation(T["rotation"][sel]).repeat(N, 1, 1)
     new = {"xyz": torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + T["xyz"][sel].repeat(N, 1),
            "scaling": torch.log(torch.exp(T["scaling"])[sel].repeat(N, 1) / (0.8 * N)),
@@ -252,6 +257,8 @@ def _ref_densify(raw, state, grads, max_grad, min_opacity, extent, max_screen_si
     if max_screen_size:
         mask = mask | (max_radii2D > max_screen_size) | (torch.exp(T["scaling"]).max(dim=1).values > 0.1 * extent)
     prune(mask)
+    if counts is not None:
+        counts.update(cloned=n_clone, split=int(sel.sum()), pruned=int(mask.sum()), P_after=int(T["xyz"].shape[0]))
     return T, S
 
 
