@@ -38,7 +38,8 @@ PY
            ;;
     hits) run hits 200 python -u tools/dbg/hit_dump.py ;;
     pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
-    dist) run dist 400 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
+    dist) run dist 700 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
+    calib) run calib 500 bash tools/hbm_calib.sh "$TAG/calib" ;;
     ab:*) run ab 900 bash tools/ab.sh ${st#ab:} ;;
     ab1:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred" run ab1 900 bash tools/ab.sh ${st#ab1:} ;;
     ab1np:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred --no-prefix-stream" run ab1np 900 bash tools/ab.sh ${st#ab1np:} ;;
