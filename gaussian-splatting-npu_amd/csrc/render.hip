@@ -584,6 +584,9 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
 // 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
 constexpr int BWD_TPW = 4;
+#ifndef GSR_BWD_STRAIGHT
+#define GSR_BWD_STRAIGHT 1
+#endif
 
 template <bool HAS_INV>
 __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_eu(4))) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
@@ -730,7 +733,11 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             float v[32];
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                if (i0 + jj < niter) {  // wave-uniform
+                // GSR_BWD_STRAIGHT: the G entries as ONE basic block (an entry past niter evaluates
+                // the staged record at position "never": zero terms), so the scheduler overlaps the
+                // independent falloff / exp / alpha work of the later entries with the T / B chain of
+                // the earlier ones; otherwise a wave-uniform branch per entry (a block per entry)
+                if (GSR_BWD_STRAIGHT || i0 + jj < niter) {
                     const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
                     const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
                     const Falloff f = falloff(co);

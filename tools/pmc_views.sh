@@ -21,4 +21,6 @@ run sq1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY
 run sq2 SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE
 run fetch FETCH_SIZE
 run write WRITE_SIZE
+run rdreq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum
+run wrreq TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum
 python3 tools/pmc_summary.py "$OUT" > "$OUT/summary.json" && echo summary ok
