@@ -381,6 +381,12 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
         a.rect4 = at<uint32_t>(gb, g.off[GEOM_RECT]);
         a.rect = nullptr;
     }
+    a.tile_diff = nullptr;
+    a.tile_diff_words = 0;
+    if (use_tile_diff(a.grid_x, a.grid_y)) {  // the tile ranges from the rects' difference array
+        a.tile_diff = at<int>(image_buffer, image_layout(width, height).off[IMG_TILE_DIFF]);
+        a.tile_diff_words = (int)((a.grid_x + 1) * (a.grid_y + 1));
+    }
     *h_out = h;
     *hdev_out = h_dev;
     return GSR_OK;
@@ -405,6 +411,11 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
     // ordered after the scan queued there, which writes into the caller's geometry buffer)
     hipError_t e = launch_inclusive_scan(a.tiles_touched, nullptr, at<uint32_t>(gb, g.off[GEOM_EMIT_START]), P,
                                          a.scan_status + scan_status_words(P), nullptr, aux, true);
+    if (e == hipSuccess && a.tile_diff) {  // the rects' difference array, beside the depth sort as well
+        ProfScope ps_(PK_RANGES, aux);
+        const TileHistJob hj = {a.rect4, P, a.tile_diff};
+        e = launch_tile_hist_batch(&hj, 1, a.grid_x, a.grid_y, aux);
+    }
 
     // 2. stable depth sort of the Gaussians (first half of the reference's tile|depth key sort)
     uint32_t* sorted_ids = at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]);
@@ -539,7 +550,11 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     j.sorted_rects = at<uint2>(gb, g.off[GEOM_SORTED_RECT]);
     j.rec_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     j.pass1_scratch = gb + g.off[GEOM_DSORT_TMP];
-    j.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
+    const bool diff = use_tile_diff((uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X),
+                                    (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y));
+    // with the difference array the tile order writes every range and nothing reads the sorted
+    // tile ids: no clearing of the ranges, no tile id written per instance
+    j.ranges = diff ? nullptr : at<uint2>(ib, im.off[IMG_RANGES]);
     if (!bb) return j;  // the histogram phase only (FUSED_COUNT): no binning buffer yet
     char* w = bb + b.off[BIN_GRAD_INST];
     j.k0 = reinterpret_cast<uint32_t*>(w + 2 * q);
@@ -549,7 +564,7 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     j.scratch = bb + b.off[BIN_RADIX_SCRATCH];
     j.out_slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
     j.out_ids = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
-    j.out_tiles = at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
+    j.out_tiles = diff ? nullptr : at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
     j.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
     return j;
 }
@@ -623,14 +638,22 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
     }
     DEBUG_SYNC(s);
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
-    {
-        ProfScope ps_(PK_RANGES, s);
-        HIP_TRY(launch_tile_ranges(L, sorted_tiles, ranges, T, s));
-    }
-    DEBUG_SYNC(s);
-
     uint32_t* tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
-    {
+    if (use_tile_diff(gx, gy)) {  // ranges and order from the rects' difference array (tile_hist)
+        ProfScope ps_(PK_TILE_ORDER, s);
+        OrderJob oj = {};
+        oj.order = tile_order;
+        oj.diff = at<int>(ib, im.off[IMG_TILE_DIFF]);
+        oj.ranges_out = ranges;
+        oj.grid_x = gx;
+        oj.grid_y = gy;
+        HIP_TRY(launch_tile_order_batch(&oj, 1, T, s));
+    } else {
+        {
+            ProfScope ps_(PK_RANGES, s);
+            HIP_TRY(launch_tile_ranges(L, sorted_tiles, ranges, T, s));
+        }
+        DEBUG_SYNC(s);
         ProfScope ps_(PK_TILE_ORDER, s);
         HIP_TRY(launch_tile_order(ranges, nullptr, T, tile_order, s));
     }
@@ -811,6 +834,12 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         // every exit after the fork joins the auxiliary stream back first: the caller's stream
         // must stay ordered after what is already queued there (it writes the caller's buffers)
         hipError_t e = launch_scan_batch(rec, V, true, aux);
+        if (e == hipSuccess && use_tile_diff(gx, gy)) {  // the rects' difference arrays, beside the depth sorts
+            TileHistJob hj[MAX_VIEWS];
+            for (int v = 0; v < V; v++) hj[v] = {pa[v].rect4, P, pa[v].tile_diff};
+            ProfScope ps_(PK_RANGES, aux);
+            e = launch_tile_hist_batch(hj, V, gx, gy, aux);
+        }
         if (e == hipSuccess) {
             ProfScope ps_(PK_DEPTH_SORT, ps);
             e = radix_sort_batch(dsort, V, DEPTH_BITS, ps);
@@ -860,6 +889,13 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         if (L[v] > 0) tsort[ns++] = fused_tile_sort_job(gb, bb, ib, P, L[v], width, height);
         rj[nf] = {L[v], L[v] > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr, at<uint2>(ib, im.off[IMG_RANGES])};
         oj[nf] = {at<uint2>(ib, im.off[IMG_RANGES]), nullptr, at<uint32_t>(ib, im.off[IMG_TILE_ORDER])};
+        if (use_tile_diff(gx, gy)) {  // the order kernel writes the ranges from the difference array
+            oj[nf].ranges = nullptr;
+            oj[nf].diff = at<int>(ib, im.off[IMG_TILE_DIFF]);
+            oj[nf].ranges_out = at<uint2>(ib, im.off[IMG_RANGES]);
+            oj[nf].grid_x = gx;
+            oj[nf].grid_y = gy;
+        }
         fit[nf++] = v;
     }
     if (ns) {
@@ -867,7 +903,7 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         HIP_TRY(tile_sort_fused_batch(tsort, ns, gx, T, ps, FUSED_SCATTER));
     }
     if (nf) {
-        {
+        if (!use_tile_diff(gx, gy)) {
             ProfScope ps_(PK_RANGES, ps);
             HIP_TRY(launch_tile_ranges_batch(rj, nf, T, ps));
         }
@@ -1385,7 +1421,11 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
     const uint32_t gy = (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     if (num_rendered > 0) {
         const uint32_t* point_list = at<uint32_t>(binning_buffer, b.off[BIN_POINT_LIST]);
-        if (keys_out)
+        if (keys_out && use_tile_diff(gx, gy))  // no tile ids were written: each tile's range carries its id
+            HIP_TRY(launch_debug_keys_from_ranges((int)(gx * gy), at<uint2>(image_buffer, im.off[IMG_RANGES]),
+                                                  point_list, at<uint32_t>(geometry_buffer, g.off[GEOM_DKEY]),
+                                                  keys_out, s));
+        else if (keys_out)
             HIP_TRY(launch_debug_keys(num_rendered, at<uint32_t>(binning_buffer, b.off[BIN_SORTED_TILES]), point_list,
                                       at<uint32_t>(geometry_buffer, g.off[GEOM_DKEY]), keys_out, s));
         if (vals_out)

@@ -191,6 +191,8 @@ enum ImageArray {
     IMG_ACCUM,            // f32x4[N] blended colour before the background + blended inverse depth
     IMG_TILE_ORDER,       // u32[T] render launch order: tiles by decreasing work (longest first)
     IMG_TILE_WORK,        // u32[T] largest n_contrib of each tile (written by render_fwd, orders render_bwd)
+    IMG_TILE_DIFF,        // i32[(grid_x + 1) (grid_y + 1)] 2-D difference array of the tile rects (tile_hist;
+                          // zeroed by preprocess): its 2-D prefix sums are the per-tile instance counts
     IMG_COUNT
 };
 
@@ -224,6 +226,20 @@ __host__ __device__ inline uint2 rect_unpack(uint32_t r)
     return make_uint2((r & 0xFFu) | (((r >> 8) & 0xFFu) << 16), ((r >> 16) & 0xFFu) | ((r >> 24) << 16));
 }
 
+// Tile ranges from the rects' 2-D difference array (tile_hist + tile_order) instead of a pass over
+// the sorted tile ids (tile_ranges): grids whose packed rects exist (<= 255 x 255 tiles), whose
+// difference array fits a workgroup's LDS and whose tiles one tile-order pass covers (<= 8,192:
+// 1080p and below).
+constexpr int TILE_DIFF_MAX_CELLS = 8704;
+#ifndef GSR_TILE_DIFF
+#define GSR_TILE_DIFF 1
+#endif
+__host__ __device__ inline bool use_tile_diff(uint32_t grid_x, uint32_t grid_y)
+{
+    return GSR_TILE_DIFF && rect_packable(grid_x, grid_y) && (grid_x + 1) * (grid_y + 1) <= (uint32_t)TILE_DIFF_MAX_CELLS &&
+           grid_x * grid_y <= 8192u;
+}
+
 struct GeomLayout { size_t off[GEOM_COUNT + 1]; };
 struct ImageLayout { size_t off[IMG_COUNT + 1]; };
 struct BinLayout { size_t off[BIN_COUNT + 1]; };
@@ -249,8 +265,9 @@ inline GeomLayout geom_layout(int P)
 inline ImageLayout image_layout(int W, int H)
 {
     size_t n = (size_t)W * H;
-    size_t t = (size_t)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X) * ((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
-    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n, 16 * n, 4 * t, 4 * t};
+    const size_t gx = (size_t)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X), gy = (size_t)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
+    size_t t = gx * gy;
+    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n, 16 * n, 4 * t, 4 * t, 4 * (gx + 1) * (gy + 1)};
     ImageLayout l;
     size_t o = 0;
     for (int i = 0; i < IMG_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

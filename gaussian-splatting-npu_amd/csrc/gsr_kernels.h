@@ -38,6 +38,8 @@ struct PreprocessArgs {
     uint32_t* dkey; // depth-sort key per Gaussian
     uint2* rect;    // {x0 | y0 << 16, x1 | y1 << 16} per Gaussian (zero if culled); null with rect4
     uint32_t* rect4;  // the rect packed (rect_pack) instead, on grids of <= 255 x 255 tiles
+    int* tile_diff;   // IMG_TILE_DIFF, zeroed here (tile_hist adds into it), or null
+    int tile_diff_words;
 };
 
 struct RenderFwdArgs {
@@ -271,9 +273,25 @@ struct OrderJob {
     const uint2* ranges;
     const uint32_t* work;
     uint32_t* order;
+    // the forward's order from the rects' difference array (use_tile_diff): the kernel derives the
+    // per-tile counts, WRITES the ranges (ranges_out) and orders by count; ranges and work unused
+    const int* diff;
+    uint2* ranges_out;
+    uint32_t grid_x, grid_y;
 };
-// every job with ranges (the forward's order) or every job with work (the backward's)
+// every job with ranges (the forward's order), every job with diff (the forward's, ranges written),
+// or every job with work (the backward's)
 hipError_t launch_tile_order_batch(const OrderJob* jobs, int V, int T, hipStream_t s);
+
+// The rects' 2-D difference array (+1 at (x0, y0) and (x1, y1), -1 at (x1, y0) and (x0, y1) of every
+// packed rect, rect_pack) added into diff (zeroed by preprocess): TILE_HIST_WGS workgroups per view
+// accumulate in LDS and add their arrays into diff with integer atomics (order-independent).
+struct TileHistJob {
+    const uint32_t* rect4;
+    int P;
+    int* diff;
+};
+hipError_t launch_tile_hist_batch(const TileHistJob* jobs, int V, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
 
 hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pairs, uint32_t* k0, uint32_t* v0,
                       uint32_t* k1, uint32_t* v1, uint32_t* out_x, uint32_t* out_y, uint32_t* sorted_keys,
@@ -283,6 +301,8 @@ hipError_t radix_sort(int n, int nbits, const uint32_t* keys_in, const uint2* pa
 hipError_t launch_tile_ranges(int L, const uint32_t* sorted_tiles, uint2* ranges, int T, hipStream_t s);
 hipError_t launch_debug_keys(int L, const uint32_t* sorted_tiles, const uint32_t* point_list, const uint32_t* dkeys,
                              uint64_t* keys, hipStream_t s);
+hipError_t launch_debug_keys_from_ranges(int T, const uint2* ranges, const uint32_t* point_list, const uint32_t* dkeys,
+                                         uint64_t* keys, hipStream_t s);
 
 // Longest-first launch order of the T tiles: order[] = tiles by decreasing work, work = range length
 // (ranges != null, the forward) or work[] (the backward's per-tile largest n_contrib).

@@ -248,6 +248,9 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
     const int V = NV == 1 ? 1 : A.V;
     for (int v = 0; v < V; v++)
         if (idx < A.a[v].scan_status_words) A.a[v].scan_status[idx] = 0;  // the scans run after this kernel
+    for (int v = 0; v < V; v++)  // tile_hist adds into it after this kernel (grid-stride: P may be small)
+        if (A.a[v].tile_diff)
+            for (int c = idx; c < A.a[v].tile_diff_words; c += (int)gridDim.x * PF_TPB) A.a[v].tile_diff[c] = 0;
     // the Gaussian's own inputs first: their loads are in flight during the SH staging
     GaussIn gi;
     if (idx < a.P) gi = load_gauss(a, idx);

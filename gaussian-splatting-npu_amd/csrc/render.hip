@@ -135,24 +135,89 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 constexpr int ORDER_BITS = 6;         // 64 work classes; tiles without work join the last one
 constexpr int ORDER_PER_THREAD = 8;   // tiles per thread and pass: 8,192 per pass (one pass at 1080p)
 
-template <bool FROM_RANGES>
+// what a tile's work is: its largest n_contrib (the backward), its range length (the forward), or
+// its instance count from the rects' 2-D difference array (the forward; the ranges are written here)
+enum OrderMode { ORD_WORK = 0, ORD_RANGES = 1, ORD_DIFF = 2 };
+
+// Inclusive prefix sums along one line of a row-major LDS grid (n cells, `stride` apart), by one wave.
+__device__ __forceinline__ void wave_line_scan(int* line, int n, int stride, int lane)
+{
+    int carry = 0;
+    for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        int v = i < n ? line[i * stride] : 0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(v, d, 64);
+            if (lane >= d) v += y;
+        }
+        v += carry;
+        if (i < n) line[i * stride] = v;
+        carry = __shfl(v, 63, 64);
+    }
+}
+
+template <int MODE>
 __global__ void __launch_bounds__(1024) tile_order_kernel(const ViewBatch<OrderJob> B, int T)
 {
-    const uint2* ranges = B.v[blockIdx.x].ranges;  // one workgroup per view
-    const uint32_t* work = B.v[blockIdx.x].work;
-    uint32_t* order = B.v[blockIdx.x].order;
+    const OrderJob& J = B.v[blockIdx.x];  // one workgroup per view
+    const uint2* ranges = J.ranges;
+    const uint32_t* work = J.work;
+    uint32_t* order = J.order;
     __shared__ uint32_t s_cnt[16][1 << ORDER_BITS];  // per-wave class counts, then per-wave starts
     __shared__ uint32_t s_order[1024 * ORDER_PER_THREAD];  // the pass's order, stored out coalesced
     __shared__ uint32_t s_max;
+    // ORD_DIFF: the difference array, turned into per-tile counts in place
+    __shared__ int s_d[MODE == ORD_DIFF ? TILE_DIFF_MAX_CELLS : 1];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t gx = J.grid_x, sx = J.grid_x + 1;
+    if constexpr (MODE == ORD_DIFF) {
+        // counts: 2-D inclusive prefix sums of the difference array (rows, then columns; the last
+        // row and column only hold the -1s of rects ending at the grid's edge), then the ranges:
+        // the exclusive scan of the counts in tile order, (0, 0) for an empty tile
+        // (identifyTileRanges' result, rasterizer_impl.cu:116-138 + the memset at :313)
+        const int gy = (int)J.grid_y, cells = (int)(sx * (J.grid_y + 1));
+        for (int c = tid; c < cells; c += 1024) s_d[c] = J.diff[c];
+        __syncthreads();
+        for (int r = wid; r < gy; r += 16) wave_line_scan(s_d + r * sx, (int)gx, 1, lane);
+        __syncthreads();
+        for (int x = wid; x < (int)gx; x += 16) wave_line_scan(s_d + x, gy, (int)sx, lane);
+        __syncthreads();
+        uint32_t c8[ORDER_PER_THREAD], sum = 0;
+#pragma unroll
+        for (int i = 0; i < ORDER_PER_THREAD; i++) {
+            const int t = tid * ORDER_PER_THREAD + i;
+            c8[i] = t < T ? (uint32_t)s_d[(uint32_t)t / gx * sx + (uint32_t)t % gx] : 0u;
+            sum += c8[i];
+        }
+        uint32_t inc = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= d) inc += y;
+        }
+        if (lane == 63) s_cnt[0][wid] = inc;
+        __syncthreads();
+        uint32_t start = inc - sum;
+        for (int q = 0; q < wid; q++) start += s_cnt[0][q];
+#pragma unroll
+        for (int i = 0; i < ORDER_PER_THREAD; i++) {
+            const int t = tid * ORDER_PER_THREAD + i;
+            if (t < T) J.ranges_out[t] = c8[i] ? make_uint2(start, start + c8[i]) : make_uint2(0u, 0u);
+            start += c8[i];
+        }
+        __syncthreads();  // s_cnt is reused below
+    }
     // unconditional (clamped) loads, so that a pass has all of them in flight at once
     auto load_work = [&](int t) -> uint32_t {
         const int tc = min(t, T - 1);
         uint32_t v;
-        if constexpr (FROM_RANGES) {
+        if constexpr (MODE == ORD_RANGES) {
             const uint2 r = ranges[tc];
             v = r.y - r.x;
+        } else if constexpr (MODE == ORD_DIFF) {
+            v = (uint32_t)s_d[(uint32_t)tc / gx * sx + (uint32_t)tc % gx];
         } else {
             v = work[tc];
         }
@@ -811,10 +876,16 @@ hipError_t launch_tile_order_batch(const OrderJob* jobs, int V, int T, hipStream
         ViewBatch<OrderJob> B;
         B.n = nv;
         for (int v = 0; v < nv; v++) B.v[v] = jobs[v0 + v];
-        if (B.v[0].ranges)
-            hipLaunchKernelGGL(tile_order_kernel<true>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
-        else
-            hipLaunchKernelGGL(tile_order_kernel<false>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        if (B.v[0].diff) {
+            for (int v = 0; v < nv; v++)
+                if (!B.v[v].diff || !use_tile_diff(B.v[v].grid_x, B.v[v].grid_y) || B.v[v].grid_x * B.v[v].grid_y != (uint32_t)T)
+                    return hipErrorInvalidValue;
+            hipLaunchKernelGGL(tile_order_kernel<ORD_DIFF>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        } else if (B.v[0].ranges) {
+            hipLaunchKernelGGL(tile_order_kernel<ORD_RANGES>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        } else {
+            hipLaunchKernelGGL(tile_order_kernel<ORD_WORK>, dim3((unsigned)nv), dim3(1024), 0, s, B, T);
+        }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Generates tests/golden/nerf_chair.npz: a real-geometry fixture from reference-held data
+"""Generates tests/golden/chair/nerf_chair.npz: a real-geometry fixture from reference-held data
  -- the NeRF-synthetic `chair` scene's initial point cloud and three of its
 training cameras at the dataset's 800 x 800 (GS-IRON's workload), read as the reference reads them
 (nerf_synthetic.py restates scene/dataset_readers.py:228-269, fetchPly and create_from_pcd; the
@@ -84,7 +84,7 @@ def main():
             out[f"case{i}_{k}"] = v
         print(f"case {i}: frame {frame} deg {deg} aa {aa} bg {bg}: L={o.num_rendered} "
               f"visible={(o.radii > 0).sum()}")
-    np.savez_compressed(os.path.join(HERE, "nerf_chair.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "chair", "nerf_chair.npz"), **out)
 
 
 if __name__ == "__main__":

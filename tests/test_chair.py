@@ -1,4 +1,4 @@
-"""The NeRF-synthetic chair fixture (tests/golden/nerf_chair.npz, make_chair.py) on CPU: the C
+"""The NeRF-synthetic chair fixture (tests/golden/chair/nerf_chair.npz, make_chair.py) on CPU: the C
 oracle re-run from the committed inputs reproduces the committed digests (so the GPU test's oracle
 run on the box is the one generated here), with a different thread count than the generator's."""
 import os
@@ -8,7 +8,7 @@ import pytest
 
 import nerf_synthetic as ns
 
-FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "nerf_chair.npz")
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "chair", "nerf_chair.npz")
 
 
 def load_chair():

@@ -1,4 +1,4 @@
-"""The HIP rasterizer on real geometry: the NeRF-synthetic chair fixture (tests/golden/nerf_chair.npz,
+"""The HIP rasterizer on real geometry: the NeRF-synthetic chair fixture (tests/golden/chair/nerf_chair.npz,
 VERDICT r03 item 9) -- the dataset's initial 100k-point cloud initialised as create_from_pcd does
 and three of its training cameras at 800 x 800 -- against the C oracle (needs an MI355X: -m gpu).
 
