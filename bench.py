@@ -105,11 +105,20 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1):
+def tile_diff_cells(W, H):
+    """(gx + 1) (gy + 1) when the library takes the tile ranges from the rects' difference array
+    (gsr_common.h use_tile_diff: <= 255 x 255 tiles, <= 8,704 cells, <= 8,192 tiles), else 0."""
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    cells = (gx + 1) * (gy + 1)
+    return cells if gx <= 255 and gy <= 255 and cells <= 8704 and gx * gy <= 8192 else 0
+
+
+def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1, diff_cells=0):
     """Compulsory HBM bytes per launch of each kernel (split per kernel).
     views_per_bwd: views whose preprocess backward one launch covers (deferred_backward batches a
     step's views: the parameters are read and their gradients written once, the per-view radii and
-    render gradients V times)."""
+    render gradients V times).  diff_cells: the tile ranges come from the rects' difference array
+    (tile_hist: packed rects in, 16 workgroups' arrays added out; the tile sort writes no tile ids)."""
     params = 4 * (11 + 3 * M)  # means 12 + scales 12 + rot 16 + opacity 4 + SH 12M
     return {
         # params in; key, radius, tile count, rect out per Gaussian; splat record 48 + conic 16 +
@@ -120,8 +129,10 @@ def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1):
         "scan": P * 8,                                          # depth-ordered tile counts in, offsets out
         # ids, offsets, rects, record starts in; (tile, (record slot, id)) per instance + valid bits out
         "emit_instances": P * 20 + L * 12 + L // 8,
-        "tile_sort": L * 24,                                    # (tile, slot, id) in and out
-        "tile_ranges": L * 4 + T * 8,
+        # (tile, slot, id) in, (slot, id) out -- (tile, slot, id) out without the difference array
+        "tile_sort": L * (20 if diff_cells else 24),
+        # tile_hist: packed rects in, 16 workgroup arrays added; else a pass over the sorted tile ids
+        "tile_ranges": P * 4 + 16 * 4 * diff_cells if diff_cells else L * 4 + T * 8,
         "tile_order": T * 12,                                   # per-tile work in, launch order out
         "render_fwd": L * 44 + N * 24 + T * 8,                  # id + 40 B record per instance; 24 B/pixel out
         "render_bwd": L * 44 + N * 24 + T * 8,                  # id + record per instance; 24 B/pixel in
@@ -535,7 +546,8 @@ def main(argv=None):
     roofline = None
     if kern:
         batched_bwd = args.batch_views or args.deferred
-        ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if batched_bwd else 1)
+        ab = algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=min(len(cams), 16) if batched_bwd else 1,
+                               diff_cells=tile_diff_cells(W, H))
         if args.batch_views:  # a batch's views share every launch (grid.y = view, up to 8 views per launch)
             vb = min(len(cams), 8)
             for k in ("depth_sort", "scan", "emit_instances", "tile_sort", "tile_ranges", "tile_order", "render_fwd",
