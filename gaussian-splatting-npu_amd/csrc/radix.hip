@@ -386,9 +386,21 @@ struct FusedPassArgs {
     uint2* ranges;
 };
 
+// GSR_FE_AOS: a rank's fields as one 16-B {start, x0 | y0 << 16, w, 1/w} and one 8-B {record start,
+// id} LDS entry (one ds_read_b128 + one ds_read_b64 per derived instance at the write-out, whose
+// owners are random across the lanes), instead of seven separate arrays (seven reads)
+#ifndef GSR_FE_AOS
+#define GSR_FE_AOS 1
+#endif
 struct FeRanks {
-    uint32_t start[FE_RANKS], x0[FE_RANKS], y0[FE_RANKS], w[FE_RANKS], g[FE_RANKS], rec[FE_RANKS];
+    uint32_t start[FE_RANKS];  // (also in geo: the owner search reads this array)
+#if GSR_FE_AOS
+    uint4 geo[FE_RANKS];
+    uint2 idr[FE_RANKS];
+#else
+    uint32_t x0[FE_RANKS], y0[FE_RANKS], w[FE_RANKS], g[FE_RANKS], rec[FE_RANKS];
     float rw[FE_RANKS];  // 1 / w
+#endif
 };
 
 // Stages chunk c's ranks; [wbeg, wend) is its instance range.  Ends with a barrier.
@@ -410,6 +422,10 @@ __device__ __forceinline__ void fe_stage(const FusedPassArgs& J, int c, FeRanks&
         }
     }
     s.start[tid] = start;
+#if GSR_FE_AOS
+    s.geo[tid] = make_uint4(start, x0 | (y0 << 16), wd, __float_as_uint(1.0f / (float)wd));
+    if (IDS) s.idr[tid] = make_uint2(rec, g);
+#else
     s.x0[tid] = x0;
     s.y0[tid] = y0;
     s.w[tid] = wd;
@@ -418,6 +434,7 @@ __device__ __forceinline__ void fe_stage(const FusedPassArgs& J, int c, FeRanks&
         s.g[tid] = g;
         s.rec[tid] = rec;
     }
+#endif
     wbeg = k0 == 0 ? 0u : J.offsets[k0 - 1];
     wend = J.offsets[min(k0 + FE_RANKS, J.P) - 1];
     __syncthreads();
@@ -436,15 +453,22 @@ __device__ __forceinline__ int fe_owner(const FeRanks& s, uint32_t sl)
 
 __device__ __forceinline__ uint32_t fe_tile(const FeRanks& s, int j, uint32_t sl, uint32_t gx, uint32_t& local)
 {
-    local = sl - s.start[j];
-    const uint32_t wj = s.w[j];
+#if GSR_FE_AOS
+    const uint4 q = s.geo[j];
+    const uint32_t st = q.x, x0 = q.y & 0xFFFFu, y0 = q.y >> 16, wj = q.z;
+    const float rw = __uint_as_float(q.w);
+#else
+    const uint32_t st = s.start[j], x0 = s.x0[j], y0 = s.y0[j], wj = s.w[j];
+    const float rw = s.rw[j];
+#endif
+    local = sl - st;
     // local / wj by a reciprocal estimate (off by at most one for local < 2^24) and one correction
     // each way, instead of the ~40-instruction integer division
-    uint32_t yy = (uint32_t)((float)local * s.rw[j]);
+    uint32_t yy = (uint32_t)((float)local * rw);
     yy -= yy * wj > local ? 1u : 0u;
     yy += (yy + 1u) * wj <= local ? 1u : 0u;
     const uint32_t xx = local - yy * wj;
-    return (s.y0[j] + yy) * gx + (s.x0[j] + xx);
+    return (y0 + yy) * gx + (x0 + xx);
 }
 
 __global__ void __launch_bounds__(RS_THREADS) fused_pass1_count_kernel(const ViewBatch<FusedPassArgs> B, uint32_t gx,
@@ -613,7 +637,12 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
                 const uint32_t k = fe_tile(s, j, r0 + li, gx, local);
                 const uint32_t d = k & mask;
                 const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
+#if GSR_FE_AOS
+                const uint2 ig = s.idr[j];
+                const uint2 v = make_uint2(ig.x + local, ig.y);
+#else
                 const uint2 v = make_uint2(s.rec[j] + local, s.g[j]);
+#endif
                 if (!last) {
                     J.keys_out[dst] = k;
                     J.vals_out[dst] = v;

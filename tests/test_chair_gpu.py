@@ -2,8 +2,8 @@
 VERDICT r03 item 9) -- the dataset's initial 100k-point cloud initialised as create_from_pcd does
 and three of its training cameras at 800 x 800 -- against the C oracle (needs an MI355X: -m gpu).
 
-Per case: the oracle re-run on the box reproduces the fixture's digests (so it is the run made in
-the build container); num_rendered, radii, the sorted tile|depth keys, their Gaussian ids and the
+Per case: the oracle re-run on the box reproduces the fixture's integer digests (so it is the run
+made in the build container); num_rendered, radii, the sorted tile|depth keys, their Gaussian ids and the
 tile ranges bit-exact; colour / invdepth / final_T / n_contrib through common.check_render; all
 eight backward outputs within 1e-4 of max|ref| outside the walks of flipped pixels, every outlier
 attributed (common.check_grad_attributed).  And the HIP distCUDA2 of the points equals the
@@ -45,9 +45,11 @@ def test_chair_case(chair, case):
     H, W, P = cam.image_height, cam.image_width, scene["means3D"].shape[0]
     o, og = make_chair.run_case(scene, cam, deg, aa, bg, seed, nthreads=min(16, os.cpu_count() or 1))
     d = make_chair.digests(o, og)
-    for k, v in d.items():  # the oracle run here is the fixture's
-        if k.startswith("sha") or k == "num_rendered":
-            assert str(v) == str(f[f"case{case}_{k}"]), k
+    # the oracle run here is the fixture's: its integer results bit for bit (the colour and n_contrib
+    # follow this host's libm expf, whose ifunc variant differs between CPUs: those are compared
+    # with the HIP path below, through check_render)
+    for k in ("num_rendered", "sha_keys", "sha_vals", "sha_ranges", "sha_radii"):
+        assert str(d[k]) == str(f[f"case{case}_{k}"]), k
     sc = {k: v.to(DEV).contiguous() for k, v in scene.items()}
     bg_t = torch.tensor(bg, dtype=torch.float32, device=DEV)
     e = torch.Tensor([])

@@ -2,7 +2,13 @@
 """Summarise rocprofv3 --pmc CSVs (tools/profile_pmc.sh) per kernel: mean counter value per
 dispatch.  Also derives per-launch memory-side traffic:
     traffic_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024
-FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B read requests as 64 B).
+FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B read requests as 64 B), and
+calibrated for this path's access shapes (profiles/r04_hbm_calib.json, tools/hbm_calib.hip): every
+read request of coalesced streams, random 48-B record gathers (into registers or LDS) and random 4-B
+gathers is a 128-B request (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ), so 2 x FETCH_SIZE is the bytes the
+memory side reads for all of them; WRITE_SIZE is exact for streams and runs and counts the 32/64-B
+sectors of scattered stores.  When a pass collected TCC_EA0_RDREQ_sum and TCC_EA0_RDREQ_128B_sum the
+read bytes come from the request sizes directly (128 / 64 / 32 B per request) instead.
 Writes <dir>/pmc_traffic.json (kernel -> bytes per launch) and <dir>/pmc_valu.json (kernel -> VALU
 wave-instructions per launch, SQ_INSTS_VALU) next to the printed summary."""
 import collections
@@ -83,8 +89,15 @@ def main(d, lib_sha256=None, workload=None, calls=None):
                 res[s] = tot[s] / n[s]
         return res
 
-    t_tot, t_n = totals(lambda e: (2 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
-                        if "FETCH_SIZE" in e and "WRITE_SIZE" in e else None)
+    def read_bytes(e):
+        if "TCC_EA0_RDREQ_sum" in e and "TCC_EA0_RDREQ_128B_sum" in e:  # request sizes, when collected
+            r32 = e.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+            r128 = e["TCC_EA0_RDREQ_128B_sum"]
+            return 128.0 * r128 + 32.0 * r32 + 64.0 * (e["TCC_EA0_RDREQ_sum"] - r128 - r32)
+        return 2 * e["FETCH_SIZE"] * 1024.0 if "FETCH_SIZE" in e else None
+
+    t_tot, t_n = totals(lambda e: read_bytes(e) + e["WRITE_SIZE"] * 1024.0
+                        if read_bytes(e) is not None and "WRITE_SIZE" in e else None)
     traffic = per_launch(t_tot, t_n)
     # stamped with the library AND the workload they were measured on: bench.py uses committed
     # figures only for that build and that workload
