@@ -234,6 +234,10 @@ constexpr int TILE_DIFF_MAX_CELLS = 8704;
 #ifndef GSR_TILE_DIFF
 #define GSR_TILE_DIFF 1
 #endif
+// the tile sort's second digit carried in the id word (radix.hip tile_sort_fused_batch)
+#ifndef GSR_TILE_PACK
+#define GSR_TILE_PACK 1
+#endif
 __host__ __device__ inline bool use_tile_diff(uint32_t grid_x, uint32_t grid_y)
 {
     return GSR_TILE_DIFF && rect_packable(grid_x, grid_y) && (grid_x + 1) * (grid_y + 1) <= (uint32_t)TILE_DIFF_MAX_CELLS &&

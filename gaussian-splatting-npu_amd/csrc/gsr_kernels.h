@@ -228,6 +228,9 @@ struct SortJob {  // radix_sort's arguments for one view
     // packed rects (rect_pack) in key order: carried as payload beside the id (v0 / v1 then hold
     // u32x2), the last pass unpacks them into sorted_rects -- no gather by id
     const uint32_t* rects4 = nullptr;
+    // > 0 (one pass, pairs given, keys_in null): the key is pairs[i].y >> key_hi_shift, and out_y
+    // gets pairs[i].y with those bits cleared
+    int key_hi_shift = 0;
 };
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };

@@ -49,6 +49,10 @@ struct CountJob {
     const uint32_t* keys;
     int n, nchunks;
     uint32_t* counts;
+    // keys == null: the key is pairs_hi[i].y >> hi_shift (the tile sort's second digit carried in
+    // the top bits of the id word, see TileSortJob)
+    const uint2* pairs_hi;
+    int hi_shift;
 };
 template <int ITEMS, typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
@@ -64,7 +68,13 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * (RS_THREADS * ITEMS);
     uint32_t k[ITEMS];
-    if (base + RS_THREADS * ITEMS <= (size_t)n && ((uintptr_t)keys & 15) == 0 && ITEMS % 4 == 0) {
+    if (!keys) {  // keys in the pairs' high bits (8-B loads; the slot word rides along unused)
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) k[i] = J.pairs_hi[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)].y >> J.hi_shift;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++)
+            if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+    } else if (base + RS_THREADS * ITEMS <= (size_t)n && ((uintptr_t)keys & 15) == 0 && ITEMS % 4 == 0) {
         // full chunk: 16-byte loads (a histogram does not care which thread counts which key)
         const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
@@ -211,6 +221,9 @@ struct SortPassArgs {
     // PAIR, first pass: the payload is (input index, rects4_in[index]) -- the packed rect carried
     // beside the id (the depth sort); the last pass then unpacks v.y into sorted_rects / sorted_counts
     const uint32_t* rects4_in;
+    // PAIR, > 0: there is no key array; the key is vals_in[i].y >> key_hi_shift and out_y receives
+    // v.y with those bits cleared (the tile sort's second pass, see TileSortJob)
+    int key_hi_shift;
 };
 
 // Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
@@ -262,9 +275,19 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     const uint64_t lt = (1ull << lane) - 1ull;
     // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
+    if (PAIR && a.key_hi_shift) {  // the key rides in the payload's high bits
 #pragma unroll
-    for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
-    if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
+        for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            if constexpr (PAIR) key[i] = val[i].y >> a.key_hi_shift;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
+    }
+    if (PAIR && a.key_hi_shift) {
+    } else if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             if constexpr (PAIR) val[i] = make_uint2((uint32_t)gidx(i), a.rects4_in[gidx(i)]);
@@ -335,7 +358,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
             } else {
                 if constexpr (PAIR) {
                     if (a.out_x) a.out_x[dst] = v.x;
-                    if (a.out_y) a.out_y[dst] = v.y;
+                    if (a.out_y) a.out_y[dst] = a.key_hi_shift ? v.y & ((1u << a.key_hi_shift) - 1u) : v.y;
                     if (a.sorted_rects) {  // the carried packed rect (no gather by id)
                         const uint2 rc = rect_unpack(v.y);
                         a.sorted_rects[dst] = rc;
@@ -384,6 +407,9 @@ struct FusedPassArgs {
     uint32_t* out_tiles;
     uint32_t* valid;
     uint2* ranges;
+    // > 0 (two passes, no tile ids wanted): no key array; the pass writes (slot, id | (tile >> w1)
+    // << pack_shift) and the second pass takes its key from those bits
+    int pack_shift, pack_w1;
 };
 
 // GSR_FE_AOS: a rank's fields as one 16-B {start, x0 | y0 << 16, w, 1/w} and one 8-B {record start,
@@ -527,7 +553,7 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     uint32_t wbeg, wend;
     fe_stage<true>(J, c, s, wbeg, wend);  // its barrier also publishes s_cnt = 0, s_base and s_own
     const uint64_t lt = (1ull << lane) - 1ull;
-    const bool last = J.keys_out == nullptr;
+    const bool last = J.keys_out == nullptr && !J.pack_shift;
     // this thread's staged rank: start and end of its instances
     const uint32_t my_start = s.start[tid];
     const uint32_t my_end = min(tid + 1 < FE_RANKS ? s.start[tid + 1] : wend, wend);
@@ -643,7 +669,9 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
 #else
                 const uint2 v = make_uint2(s.rec[j] + local, s.g[j]);
 #endif
-                if (!last) {
+                if (J.pack_shift) {
+                    J.vals_out[dst] = make_uint2(v.x, v.y | ((k >> J.pack_w1) << J.pack_shift));
+                } else if (!last) {
                     J.keys_out[dst] = k;
                     J.vals_out[dst] = v;
                 } else {
@@ -803,6 +831,8 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
         for (int v = 0; v < nv; v++) {
             kin[v] = jobs[v0 + v].keys_in;
             vin[v] = reinterpret_cast<const uint32_t*>(jobs[v0 + v].pairs);
+            // keys carried in the pairs' high bits: one pass only (the bits hold one digit)
+            if (jobs[v0 + v].key_hi_shift && (npass != 1 || !jobs[v0 + v].pairs)) return hipErrorInvalidValue;
         }
         int shift = shift0;
         for (int p = 0; p < npass; p++) {
@@ -815,7 +845,8 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             for (int v = 0; v < nv; v++) {
                 const SortJob& j = jobs[v0 + v];
                 const int nchunks = (int)rs_chunks(j.n);
-                cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j)};
+                cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j), j.key_hi_shift ? j.pairs : nullptr, j.key_hi_shift};
+                if (j.key_hi_shift) cb.v[v].keys = nullptr;
                 rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
                 SortPassArgs& a = sb.v[v];
                 a.n = j.n;
@@ -835,6 +866,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.sorted_counts = j.sorted_counts;
                 a.row_prefix = sort_counts(j);
                 a.totals = sort_totals(j);
+                a.key_hi_shift = j.key_hi_shift;
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
@@ -883,6 +915,7 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
         ViewBatch<FusedPassArgs> fb;
         ViewBatch<RowJob> rb;
         SortJob rest[VIEW_BATCH];
+        bool packed = false;
         fb.n = rb.n = nv;
         int maxc = 0;
         for (int v = 0; v < nv; v++) {
@@ -901,6 +934,15 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             // the fused pass writes (k1, v1), so that the later passes ping-pong k0 <- k1 <- k0 ...
             a.keys_out = npass > 1 ? j.k1 : nullptr;
             a.vals_out = npass > 1 ? reinterpret_cast<uint2*>(j.v1) : nullptr;
+            // two passes and no tile ids wanted (the ranges come from the rects' difference array):
+            // the second digit goes into the id word's free high bits, so the first pass writes 8
+            // bytes per instance instead of 12 and the second reads 8 instead of 12
+            a.pack_shift = 0;
+            a.pack_w1 = w1;
+            if (GSR_TILE_PACK && npass == 2 && !j.out_tiles && (uint64_t)j.P <= (1ull << (32 - (nbits - w1)))) {
+                a.pack_shift = 32 - (nbits - w1);
+                a.keys_out = nullptr;
+            }
             a.out_slot = j.out_slot;
             a.out_ids = j.out_ids;
             a.out_tiles = j.out_tiles;
@@ -908,8 +950,10 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             a.ranges = j.ranges;
             rb.v[v] = {a.counts, a.nchunks, a.totals};
             maxc = max(maxc, a.nchunks);
-            rest[v] = {j.L, j.k1, reinterpret_cast<const uint2*>(j.v1), j.k0, j.v0, j.k1, j.v1, j.out_slot, j.out_ids,
-                       j.out_tiles, j.scratch, nullptr, nullptr, nullptr};
+            rest[v] = {j.L, a.pack_shift ? nullptr : j.k1, reinterpret_cast<const uint2*>(j.v1), j.k0, j.v0, j.k1, j.v1,
+                       j.out_slot, j.out_ids, j.out_tiles, j.scratch, nullptr, nullptr, nullptr};
+            rest[v].key_hi_shift = a.pack_shift;
+            packed = a.pack_shift != 0;
         }
         if (maxc == 0) return hipSuccess;
         const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
@@ -931,7 +975,8 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
         hipError_t e = hipGetLastError();
         if (e != hipSuccess || npass == 1) return e;
         // the later passes: key bits [w1, nbits), ping-pong k1/v1 -> k0/v0 -> ...
-        return radix_sort_batch(rest, nv, nbits - w1, s, w1, SORT_TILE);
+        // (packed: the second digit, already shifted down, in the id word's high bits)
+        return radix_sort_batch(rest, nv, nbits - w1, s, packed ? 0 : w1, SORT_TILE);
     });
 }
 
