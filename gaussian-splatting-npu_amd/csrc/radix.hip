@@ -744,8 +744,7 @@ __global__ void __launch_bounds__(1024) tile_hist_kernel(const ViewBatch<TileHis
     const int tid = threadIdx.x;
     for (int c = tid; c < cells; c += 1024) s_h[c] = 0;
     __syncthreads();
-    for (int i = (int)blockIdx.x * 1024 + tid; i < J.P; i += TILE_HIST_WGS * 1024) {
-        const uint32_t r = J.rect4[i];
+    auto add = [&](uint32_t r) {
         const uint32_t x0 = r & 0xFFu, y0 = (r >> 8) & 0xFFu, x1 = (r >> 16) & 0xFFu, y1 = r >> 24;
         if (x1 > x0 && y1 > y0) {
             atomicAdd(&s_h[y0 * sx + x0], 1);
@@ -753,7 +752,25 @@ __global__ void __launch_bounds__(1024) tile_hist_kernel(const ViewBatch<TileHis
             atomicAdd(&s_h[y1 * sx + x0], -1);
             atomicAdd(&s_h[y1 * sx + x1], 1);
         }
+    };
+    // four rects per 16-B load, eight loads in flight per thread before the first LDS atomic (the
+    // loop is latency-bound otherwise: one dependent round trip per rect)
+    constexpr int U = 8, STRIDE = TILE_HIST_WGS * 1024;
+    const int n4 = J.P >> 2;
+    const uint4* r4 = reinterpret_cast<const uint4*>(J.rect4);
+    for (int i0 = (int)blockIdx.x * 1024 + tid; i0 < n4; i0 += U * STRIDE) {
+        uint4 q[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) q[u] = i0 + u * STRIDE < n4 ? r4[i0 + u * STRIDE] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            add(q[u].x);
+            add(q[u].y);
+            add(q[u].z);
+            add(q[u].w);
+        }
     }
+    if (blockIdx.x == 0 && tid < (J.P & 3)) add(J.rect4[4 * n4 + tid]);  // the last P mod 4 rects
     __syncthreads();
     for (int c = tid; c < cells; c += 1024) {
         const int v = s_h[c];

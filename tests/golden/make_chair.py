@@ -71,14 +71,20 @@ def main():
     dist2 = oracle.knn_dist2(xyz, nthreads=8)
     cams = ns.read_transforms(os.path.join(SCENE, "transforms_train.json"), frames=set(FRAMES))
     scene = ns.initial_gaussians(xyz, rgb, dist2)
+    # the cameras' matrices as computed here are part of the fixture: numpy's / torch's CPU linear
+    # algebra (inverse, bmm) may round differently on another host's CPU, and one ulp in a matrix
+    # can move a radius across a ceil (tests rebuild the cameras from these, not from R, T)
+    full = [ns.camera(c[0], c[1], c[2], c[3], c[4], c[5]) for c in cams]
     out = {"xyz": xyz, "rgb": rgb, "dist2": dist2,
            "R": np.stack([c[0] for c in cams]), "T": np.stack([c[1] for c in cams]),
            "fovx": np.array([c[2] for c in cams]), "fovy": np.array([c[3] for c in cams]),
            "width": np.int32(cams[0][4]), "height": np.int32(cams[0][5]),
-           "file_path": np.array([c[6] for c in cams])}
+           "file_path": np.array([c[6] for c in cams]),
+           "viewmatrix": np.stack([c.world_view_transform.numpy() for c in full]),
+           "projmatrix": np.stack([c.full_proj_transform.numpy() for c in full]),
+           "campos": np.stack([c.camera_center.numpy() for c in full])}
     for i, (frame, deg, aa, bg) in enumerate(CASES):
-        c = cams[frame]
-        cam = ns.camera(c[0], c[1], c[2], c[3], c[4], c[5])
+        cam = full[frame]
         o, g = run_case(scene, cam, deg, aa, bg, grad_seed=100 + i)
         for k, v in digests(o, g).items():
             out[f"case{i}_{k}"] = v

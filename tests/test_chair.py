@@ -11,6 +11,21 @@ import nerf_synthetic as ns
 FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "chair", "nerf_chair.npz")
 
 
+class FixtureCamera:
+    """A camera of the fixture: the matrices as computed where the fixture was made (another host's
+    CPU linear algebra may round them differently), the fields of view and the image size."""
+
+    def __init__(self, f, frame):
+        import math
+        import torch
+        self.world_view_transform = torch.from_numpy(f["viewmatrix"][frame].copy())
+        self.full_proj_transform = torch.from_numpy(f["projmatrix"][frame].copy())
+        self.camera_center = torch.from_numpy(f["campos"][frame].copy())
+        self.FoVx, self.FoVy = float(f["fovx"][frame]), float(f["fovy"][frame])
+        self.tanfovx, self.tanfovy = math.tan(self.FoVx * 0.5), math.tan(self.FoVy * 0.5)
+        self.image_width, self.image_height = int(f["width"]), int(f["height"])
+
+
 def load_chair():
     """(fixture dict, activated Gaussians, [cases: (camera, sh_degree, antialiasing, bg, grad_seed)])."""
     import make_chair
@@ -18,13 +33,12 @@ def load_chair():
     scene = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"])
     cases = []
     for i, (frame, deg, aa, bg) in enumerate(make_chair.CASES):
-        cam = ns.camera(f["R"][frame], f["T"][frame], float(f["fovx"][frame]), float(f["fovy"][frame]),
-                        int(f["width"]), int(f["height"]))
-        cases.append((cam, deg, aa, bg, 100 + i))
+        cases.append((FixtureCamera(f, frame), deg, aa, bg, 100 + i))
     return f, scene, cases
 
 
 def test_chair_inputs():
+    import make_chair
     f, scene, cases = load_chair()
     assert f["xyz"].shape == (100_000, 3) and f["rgb"].shape == (100_000, 3)
     assert np.all(np.abs(f["xyz"]) <= 1.3)  # the dataset's initial cloud: U(-1.3, 1.3)^3
@@ -33,7 +47,13 @@ def test_chair_inputs():
     assert np.all(scene["rotations"].numpy() == np.array([1, 0, 0, 0], np.float32))
     np.testing.assert_allclose(scene["opacities"].numpy(), 0.1, rtol=1e-6)
     np.testing.assert_allclose(scene["scales"][:, 0].numpy() ** 2, np.maximum(f["dist2"], 1e-7), rtol=1e-5)
-    for cam, *_ in cases:
+    for i, (cam, *_) in enumerate(cases):
+        # the stored matrices are those nerf_synthetic's restatement of the reference's readers builds
+        frame = make_chair.CASES[i][0]
+        ref = ns.camera(f["R"][frame], f["T"][frame], float(f["fovx"][frame]), float(f["fovy"][frame]),
+                        int(f["width"]), int(f["height"]))
+        np.testing.assert_allclose(cam.full_proj_transform.numpy(), ref.full_proj_transform.numpy(), atol=1e-6)
+        np.testing.assert_allclose(cam.world_view_transform.numpy(), ref.world_view_transform.numpy(), atol=1e-6)
         # a camera on the Blender sphere (radius ~4.03) looking at the origin: the origin projects
         # near the image centre, in front of the camera
         c = cam.camera_center.numpy()
