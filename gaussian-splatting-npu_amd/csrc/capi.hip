@@ -381,6 +381,7 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
         a.rect4 = at<uint32_t>(gb, g.off[GEOM_RECT]);
         a.rect = nullptr;
     }
+    a.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
     a.tile_diff = nullptr;
     a.tile_diff_words = 0;
     if (use_tile_diff(a.grid_x, a.grid_y)) {  // the tile ranges from the rects' difference array
@@ -979,6 +980,8 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     r.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
     r.hit = R > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
+    r.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+    r.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
     if (R > 0) {
         {
             ProfScope ps_(PK_TILE_ORDER, s);
@@ -1009,6 +1012,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     p.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
     p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
     p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
+    p.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
     p.has_invdepth = dL_invdepths != nullptr;
     p.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
     p.W = width; p.H = height;
@@ -1068,6 +1072,8 @@ static RenderBwdArgs render_bwd_args(int P, int R, const float* background, int 
     r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
     r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
     r.hit = at<uint8_t>(bb, b.off[BIN_HIT]);
+    r.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+    r.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
     return r;
 }
 
@@ -1153,7 +1159,7 @@ int gsr_backward_preprocess_views_range(int V, int P, int D, int M, const int* R
     p.view = nullptr; p.proj = nullptr; p.campos = nullptr;
     p.focal_x = p.focal_y = p.tan_fovx = p.tan_fovy = 0.f;
     p.antialiasing = antialiasing;
-    p.grad_inst = nullptr; p.valid = nullptr; p.emit_start = nullptr; p.tiles_touched = nullptr;
+    p.grad_inst = nullptr; p.valid = nullptr; p.emit_start = nullptr; p.tiles_touched = nullptr; p.rec_mask = nullptr;
     // a view rendered without an inverse-depth gradient has zero invdepth fields in its records:
     // subtracting their (zero) term leaves its gradients bit-identical
     p.has_invdepth = has_invdepth;
@@ -1189,6 +1195,7 @@ int gsr_backward_preprocess_views_range(int V, int P, int D, int M, const int* R
         bv.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
         bv.grad_inst = L > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
         bv.valid = L > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
+        bv.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
         bv.dL_dmean2D = dL_dmean2D[v];
     }
     // BACKWARD::preprocess (rasterizer_impl.cu:423-449) of the whole batch: one pass over the Gaussians

@@ -181,6 +181,8 @@ enum GeomArray {
     GEOM_RADIX_SCRATCH,   // count matrix + digit totals of the depth sort
     GEOM_SCAN_SCRATCH,    // 2 x u64[scan chunks + 1] look-back status words + chunk ticket of the two
                           // scans (depth order, index order; zeroed by preprocess)
+    GEOM_REC_MASK,        // u32[P] bit k: Gaussian i's record at slot emit_start[i] + k was written (render_bwd,
+                          // k < 32; zeroed by preprocess) -- its records without the valid-word round trip
     GEOM_COUNT
 };
 
@@ -234,6 +236,11 @@ constexpr int TILE_DIFF_MAX_CELLS = 8704;
 #ifndef GSR_TILE_DIFF
 #define GSR_TILE_DIFF 1
 #endif
+// records found through each Gaussian's record mask (GEOM_REC_MASK, set by render_bwd) instead of
+// the valid words
+#ifndef GSR_REC_MASK
+#define GSR_REC_MASK 1
+#endif
 // the tile sort's second digit carried in the id word (radix.hip tile_sort_fused_batch)
 #ifndef GSR_TILE_PACK
 #define GSR_TILE_PACK 1
@@ -258,7 +265,7 @@ inline GeomLayout geom_layout(int P)
                                 4 * p, 4 * p, 4 * p, 8 * p, 8 * p,
                                 // (after the depth sort, the fused tile-sort pass's count matrix)
                                 std::max(24 * p + 2048, fused_pass1_scratch_bytes(P)), radix_status_bytes(P, 4),
-                                16 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1)};
+                                16 * ((p + SCAN_ITEMS - 1) / SCAN_ITEMS + 1), 4 * p};
     GeomLayout l;
     size_t o = 0;
     for (int i = 0; i < GEOM_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -40,6 +40,7 @@ struct PreprocessArgs {
     uint32_t* rect4;  // the rect packed (rect_pack) instead, on grids of <= 255 x 255 tiles
     int* tile_diff;   // IMG_TILE_DIFF, zeroed here (tile_hist adds into it), or null
     int tile_diff_words;
+    uint32_t* rec_mask;  // GEOM_REC_MASK, zeroed here (render_bwd sets it)
 };
 
 struct RenderFwdArgs {
@@ -77,6 +78,8 @@ struct RenderBwdArgs {
     uint32_t* valid;            // bit (slot & 31) of valid[slot >> 5] set for every record written (cleared by emit)
     float* grad_inst;           // f32x12[L]: one gradient record per (tile, Gaussian) entry, at its record slot
     const uint8_t* hit;         // BIN_HIT (render_fwd): the quadrants each entry contributed to
+    const uint32_t* emit_start; // GEOM_EMIT_START: first record slot of each Gaussian
+    uint32_t* rec_mask;         // GEOM_REC_MASK: bit (slot - emit_start[id]) set for records at local index < 32
 };
 
 // Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  With u = G dL/dalpha
@@ -120,6 +123,7 @@ struct PreprocessBwdArgs {
     // exclusive scan of tiles_touched)
     const uint32_t* emit_start;     // first record slot of Gaussian i
     const uint32_t* tiles_touched;  // number of record slots of Gaussian i
+    const uint32_t* rec_mask;       // GEOM_REC_MASK: which of slots [emit_start, + 32) hold a record
     int has_invdepth;
     const float4* conic_opacity;    // GEOM_CONIC_OPACITY (the rendered, AA-scaled opacity in .w)
     int W, H;
@@ -154,6 +158,7 @@ struct BwdView {
     const uint32_t* tiles_touched;
     const float* grad_inst;
     const uint32_t* valid;
+    const uint32_t* rec_mask;
     float* dL_dmean2D;  // (P,3)
 };
 struct PreprocessBwdViewsArgs {

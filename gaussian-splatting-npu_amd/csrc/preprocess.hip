@@ -248,6 +248,8 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
     const int V = NV == 1 ? 1 : A.V;
     for (int v = 0; v < V; v++)
         if (idx < A.a[v].scan_status_words) A.a[v].scan_status[idx] = 0;  // the scans run after this kernel
+    if (idx < a.P)  // render_bwd ORs the records it writes into it
+        for (int v = 0; v < V; v++) A.a[v].rec_mask[idx] = 0u;
     for (int v = 0; v < V; v++)  // tile_hist adds into it after this kernel (grid-stride: P may be small)
         if (A.a[v].tile_diff)
             for (int c = idx; c < A.a[v].tile_diff_words; c += (int)gridDim.x * PF_TPB) A.a[v].tile_diff[c] = 0;

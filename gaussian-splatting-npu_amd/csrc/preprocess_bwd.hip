@@ -13,6 +13,7 @@ namespace gsr {
 
 __device__ __forceinline__ float sq(float x) { return x * x; }
 
+
 // One output element: written, or added to when the caller accumulates into it (AccBits).
 __device__ __forceinline__ void put(float* p, float v, bool acc) { *p = acc ? *p + v : v; }
 // the same with the old value already loaded (bwd_gather prefetches them)
@@ -83,13 +84,62 @@ __device__ __forceinline__ void gather_range(uint32_t e0, uint32_t e1, const uin
     }
 }
 
+// The records of a Gaussian with at most 32 slots from its own record mask (bit k: slot e0 + k holds
+// a record, render_bwd), loaded beside e0 and n: no dependent load of the valid words.  Same slot
+// order as gather_range: the same sums bit for bit.
+template <int B = REC_BATCH>
+__device__ __forceinline__ void gather_mask(uint32_t e0, uint32_t bits, const float* grad_inst, float (&g)[GF_NUM])
+{
+#pragma unroll
+    for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
+    while (bits) {
+        bool v[B];
+        uint32_t sl[B];
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            v[k] = bits != 0u;
+            sl[k] = e0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
+            bits &= bits - 1u;
+        }
+        float4 r[B][3];
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            if (v[k]) {
+                const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
+                r[k][0] = rec[0];
+                r[k][1] = rec[1];
+                r[k][2] = rec[2];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < B; k++) {
+            if (v[k]) {
+                g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
+                g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
+                g[8] += r[k][2].x; g[9] += r[k][2].y;
+            }
+        }
+    }
+}
+
+// One Gaussian's records of one view: by its record mask when it has at most 32 slots (almost all),
+// else through the valid words.
+template <int B = REC_BATCH>
+__device__ __forceinline__ void gather_any(uint32_t e0, uint32_t n, uint32_t mask, const uint32_t* valid,
+                                           const float* grad_inst, float (&g)[GF_NUM])
+{
+    if (GSR_REC_MASK && n <= 32u) gather_mask<B>(e0, mask, grad_inst, g);
+    else gather_range<B>(e0, e0 + n, valid, grad_inst, g);
+}
+
 template <int B = REC_BATCH>
 __device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
-                                               const uint32_t* valid, const float* grad_inst, int idx,
-                                               float (&g)[GF_NUM])
+                                               const uint32_t* rec_mask, const uint32_t* valid, const float* grad_inst,
+                                               int idx, float (&g)[GF_NUM])
 {
-    const uint32_t e0 = emit_start[idx];
-    gather_range<B>(e0, e0 + tiles_touched[idx], valid, grad_inst, g);  // 0 tiles for culled Gaussians
+    const uint32_t e0 = emit_start[idx], n = tiles_touched[idx];  // 0 tiles for culled Gaussians
+    const uint32_t mask = rec_mask[idx];
+    gather_any<B>(e0, n, mask, valid, grad_inst, g);
 }
 
 // The per-Gaussian parameters (and, accumulating, the outputs' old values); with `view` also the
@@ -126,7 +176,7 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
         const float* r = a.dL_drot + 4 * i;
         in.old_rot[0] = r[0]; in.old_rot[1] = r[1]; in.old_rot[2] = r[2]; in.old_rot[3] = r[3];
     }
-    if (view) gather_records(a.emit_start, a.tiles_touched, a.valid, a.grad_inst, idx, in.g);
+    if (view) gather_records(a.emit_start, a.tiles_touched, a.rec_mask, a.valid, a.grad_inst, idx, in.g);
 }
 
 // Per-Gaussian state carried from the non-SH part into the SH halves and the final dL/dmean3D.
@@ -614,6 +664,7 @@ struct ViewIn {
     float4 co;
     uint8_t cl;
     uint32_t e0, n;  // record slots [e0, e0 + n)
+    uint32_t mask;   // which of the first 32 hold a record
 };
 
 __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int idx, int v, ViewIn& vi)
@@ -623,6 +674,7 @@ __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int i
     vi.cl = bv.clamped[idx];
     vi.e0 = bv.emit_start[idx];
     vi.n = bv.tiles_touched[idx];
+    vi.mask = bv.rec_mask[idx];
 }
 
 // The batch's cameras in LDS (view 16, proj 16, campos 3, focal_x, focal_y, tan_fovx, tan_fovy),
@@ -674,7 +726,7 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 1e-3f * (float)(vi.e0 & 7u) + 1e-4f * q;
 #else
-        gather_range<VIEW_REC_BATCH>(vi.e0, vi.e0 + vi.n, bv.valid, bv.grad_inst, gs);
+        gather_any<VIEW_REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
 #endif
     } else {
 #pragma unroll

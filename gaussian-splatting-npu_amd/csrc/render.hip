@@ -762,9 +762,11 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         // only entries that contributed somewhere in the forward are read (43 % of the entries
         // below tmax contributed nowhere: their 48-B record gathers are skipped)
+        uint32_t es = 0;  // the Gaussian's first record slot (its record mask bit at the store)
         if (m != 0) {
             const float4* r = a.splat + 3 * (size_t)id;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
+            if (GSR_REC_MASK) es = a.emit_start[id];
             s_rec[0][lane] = r0;
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;
@@ -889,6 +891,10 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
             reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
             atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
+            // and in the Gaussian's own mask (its first 32 slots): preprocess_bwd then finds its records
+            // without a dependent load of the valid words
+            const uint32_t local = myslot - es;
+            if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
     }
