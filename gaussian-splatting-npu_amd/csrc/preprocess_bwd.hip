@@ -43,12 +43,14 @@ constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +
 // mask is 0) and are not read (most slots: records are sparse).  The mask has one bit per slot
 // (L/8 bytes: it stays in L2), so a Gaussian's flags are one or two words; its flagged records are
 // then read B at a time in slot order (bitwise reproducible sums).
-template <int B = REC_BATCH>
+template <int B = REC_BATCH, bool INIT = true>
 __device__ __forceinline__ void gather_range(uint32_t e0, uint32_t e1, const uint32_t* valid, const float* grad_inst,
                                              float (&g)[GF_NUM])
 {
+    if (INIT) {
 #pragma unroll
-    for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
+        for (int q = 0; q < GF_NUM; q++) g[q] = 0.f;
+    }
     for (uint32_t w0 = e0 & ~31u; w0 < e1; w0 += 32) {
         uint32_t bits = valid[w0 >> 5];
         if (w0 < e0) bits &= ~0u << (e0 - w0);
@@ -122,14 +124,19 @@ __device__ __forceinline__ void gather_mask(uint32_t e0, uint32_t bits, const fl
     }
 }
 
-// One Gaussian's records of one view: by its record mask when it has at most 32 slots (almost all),
-// else through the valid words.
+// One Gaussian's records of one view: its first 32 slots by its record mask, the rest (Gaussians
+// of more than 32 tiles only) through the valid words -- render_bwd flags each record in exactly one
+// of the two.  Slot order throughout: the sums are those of one walk over the valid words, bit for bit.
 template <int B = REC_BATCH>
 __device__ __forceinline__ void gather_any(uint32_t e0, uint32_t n, uint32_t mask, const uint32_t* valid,
                                            const float* grad_inst, float (&g)[GF_NUM])
 {
-    if (GSR_REC_MASK && n <= 32u) gather_mask<B>(e0, mask, grad_inst, g);
-    else gather_range<B>(e0, e0 + n, valid, grad_inst, g);
+    if (!GSR_REC_MASK) {
+        gather_range<B>(e0, e0 + n, valid, grad_inst, g);
+        return;
+    }
+    gather_mask<B>(e0, mask, grad_inst, g);
+    if (n > 32u) gather_range<B, false>(e0 + 32u, e0 + n, valid, grad_inst, g);
 }
 
 template <int B = REC_BATCH>

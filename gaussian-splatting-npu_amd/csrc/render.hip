@@ -890,11 +890,12 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
             reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
             reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
-            atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
-            // and in the Gaussian's own mask (its first 32 slots): preprocess_bwd then finds its records
-            // without a dependent load of the valid words
+            // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
+            // then finds the records without a dependent load of the valid words), else in the valid
+            // words: one atomic per record either way
             const uint32_t local = myslot - es;
             if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
+            else atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
     }

@@ -75,9 +75,11 @@ def read_points_ply(path):
     return xyz, rgb
 
 
-def initial_gaussians(xyz, rgb, dist2):
+def initial_gaussians(xyz, rgb, dist2, scale=None, opacity=None):
     """create_from_pcd + activations: {means3D, shs (P,16,3), scales, rotations, opacities}, float32.
-    dist2 = distCUDA2(xyz) (simple-knn's mean squared 3-NN distance)."""
+    dist2 = distCUDA2(xyz) (simple-knn's mean squared 3-NN distance).  scale (P,) / opacity: the
+    activated values when already known (a fixture's, computed on another host), instead of this
+    host's exp(log(sqrt(dist2))) and sigmoid(inverse_sigmoid(0.1))."""
     P = xyz.shape[0]
     colors = torch.tensor(rgb.astype(np.float64) / 255.0).float()
     fused = (colors - 0.5) / C0                                   # RGB2SH
@@ -88,7 +90,9 @@ def initial_gaussians(xyz, rgb, dist2):
     rots = torch.zeros((P, 4), dtype=torch.float32)
     rots[:, 0] = 1
     opac = torch.log(torch.tensor(0.1) / (1 - torch.tensor(0.1))) * torch.ones((P, 1))  # inverse_sigmoid(0.1)
+    scales = torch.exp(scaling) if scale is None else torch.as_tensor(scale, dtype=torch.float32)[:, None].repeat(1, 3)
+    opacities = torch.sigmoid(opac) if opacity is None else torch.full((P, 1), float(opacity), dtype=torch.float32)
     return {"means3D": torch.as_tensor(xyz).contiguous(), "shs": shs.contiguous(),
-            "scales": torch.exp(scaling).contiguous(),
+            "scales": scales.contiguous(),
             "rotations": torch.nn.functional.normalize(rots).contiguous(),
-            "opacities": torch.sigmoid(opac).contiguous()}
+            "opacities": opacities.contiguous()}

@@ -1,8 +1,12 @@
 """Shared helpers for the parity tests: build a case, run the oracle and the HIP path on it."""
+import os
+
 import numpy as np
 import torch
 
 import synthetic
+
+ROOT_OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
 
 # Tolerances (fp32).  Preprocess outputs and the sorted key/value arrays are compared
 # bit-exactly.  Render outputs differ from the oracle only through exp() (v_exp_f32 vs

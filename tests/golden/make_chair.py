@@ -82,7 +82,13 @@ def main():
            "file_path": np.array([c[6] for c in cams]),
            "viewmatrix": np.stack([c.world_view_transform.numpy() for c in full]),
            "projmatrix": np.stack([c.full_proj_transform.numpy() for c in full]),
-           "campos": np.stack([c.camera_center.numpy() for c in full])}
+           "campos": np.stack([c.camera_center.numpy() for c in full]),
+           # likewise the host math of the parameters (torch's vectorised exp / log / sigmoid and
+           # libm's tan may round differently on another CPU): the activated scale (isotropic) and
+           # opacity, and the tangents of the half fields of view, as computed here
+           "scale": scene["scales"][:, 0].numpy().copy(), "opacity": scene["opacities"][0, 0].numpy().copy(),
+           "tanfovx": np.array([c.tanfovx for c in full], np.float32),
+           "tanfovy": np.array([c.tanfovy for c in full], np.float32)}
     for i, (frame, deg, aa, bg) in enumerate(CASES):
         cam = full[frame]
         o, g = run_case(scene, cam, deg, aa, bg, grad_seed=100 + i)

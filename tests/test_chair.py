@@ -22,7 +22,7 @@ class FixtureCamera:
         self.full_proj_transform = torch.from_numpy(f["projmatrix"][frame].copy())
         self.camera_center = torch.from_numpy(f["campos"][frame].copy())
         self.FoVx, self.FoVy = float(f["fovx"][frame]), float(f["fovy"][frame])
-        self.tanfovx, self.tanfovy = math.tan(self.FoVx * 0.5), math.tan(self.FoVy * 0.5)
+        self.tanfovx, self.tanfovy = float(f["tanfovx"][frame]), float(f["tanfovy"][frame])
         self.image_width, self.image_height = int(f["width"]), int(f["height"])
 
 
@@ -30,7 +30,7 @@ def load_chair():
     """(fixture dict, activated Gaussians, [cases: (camera, sh_degree, antialiasing, bg, grad_seed)])."""
     import make_chair
     f = dict(np.load(FIX))
-    scene = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"])
+    scene = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"], scale=f["scale"], opacity=f["opacity"])
     cases = []
     for i, (frame, deg, aa, bg) in enumerate(make_chair.CASES):
         cases.append((FixtureCamera(f, frame), deg, aa, bg, 100 + i))
@@ -47,6 +47,10 @@ def test_chair_inputs():
     assert np.all(scene["rotations"].numpy() == np.array([1, 0, 0, 0], np.float32))
     np.testing.assert_allclose(scene["opacities"].numpy(), 0.1, rtol=1e-6)
     np.testing.assert_allclose(scene["scales"][:, 0].numpy() ** 2, np.maximum(f["dist2"], 1e-7), rtol=1e-5)
+    # the stored activations are this host's create_from_pcd (up to the last bit elsewhere)
+    here = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"])
+    np.testing.assert_allclose(here["scales"].numpy(), scene["scales"].numpy(), rtol=1e-6)
+    np.testing.assert_allclose(here["opacities"].numpy(), scene["opacities"].numpy(), rtol=1e-6)
     for i, (cam, *_) in enumerate(cases):
         # the stored matrices are those nerf_synthetic's restatement of the reference's readers builds
         frame = make_chair.CASES[i][0]
