@@ -62,36 +62,6 @@ int fail_hip(hipError_t e, int line)
 // prefiltered-violation flag and num_rendered straight into them (system-scope stores), so the
 // forward needs neither a device memset nor a D2H copy before its one stream synchronisation.
 constexpr int PINNED_SLOT_WORDS = 16;
-
-// DepthRange words of this host thread, per device and view slot: {epoch << 32 | ~min, epoch <<
-// 32 | max} of the visible depth keys (preprocess), read by the forward's depth sort.  A forward
-// takes the next epoch of its slot, so the words need no reset: an older epoch reads as "no key".
-// Zeroed once when allocated.  A slot's forwards follow one another (each reads its L back before
-// the next one starts), so one pair of words per slot suffices.
-#ifndef GSR_DEPTH_RANGE
-#define GSR_DEPTH_RANGE 1
-#endif
-thread_local unsigned long long* g_drange[64] = {};
-thread_local uint32_t g_depoch[64][MAX_VIEWS] = {};
-int depth_range(int slot, unsigned long long** words, uint32_t* epoch)
-{
-    *words = nullptr;
-    *epoch = 0;
-    if (!GSR_DEPTH_RANGE) return GSR_OK;
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess) return fail_hip(e, __LINE__);
-    if (dev < 0 || dev >= 64) return GSR_OK;
-    if (!g_drange[dev]) {
-        if ((e = hipMalloc((void**)&g_drange[dev], 16 * MAX_VIEWS)) != hipSuccess) return fail_hip(e, __LINE__);
-        if ((e = hipMemset(g_drange[dev], 0, 16 * MAX_VIEWS)) != hipSuccess) return fail_hip(e, __LINE__);
-    }
-    *words = g_drange[dev] + 2 * slot;
-    *epoch = ++g_depoch[dev][slot];
-    if (*epoch == 0) *epoch = ++g_depoch[dev][slot];  // (after 2^32 forwards: skip the zero epoch)
-    return GSR_OK;
-}
-
 int pinned(int slot, uint32_t** out)
 {
     if (!g_pinned) {
@@ -412,8 +382,6 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
         a.rect = nullptr;
     }
     a.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
-    rc = depth_range(slot, &a.drange, &a.depoch);
-    if (rc) return rc;
     a.tile_diff = nullptr;
     a.tile_diff_words = 0;
     if (use_tile_diff(a.grid_x, a.grid_y)) {  // the tile ranges from the rects' difference array
@@ -466,8 +434,6 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
         SortJob j = {P, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH],
                      a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                      a.rect4};
-        j.drange = a.drange;  // only the passes the visible keys' range needs
-        j.depoch = a.depoch;
         e = radix_sort_batch(&j, 1, DEPTH_BITS, s);
     }
     if (debug && e == hipSuccess) e = hipStreamSynchronize(s);
@@ -857,8 +823,6 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                     reinterpret_cast<uint32_t*>(tmp + 3 * q), reinterpret_cast<uint32_t*>(tmp + 4 * q),
                     at<uint32_t>(gb, g.off[GEOM_SORTED_IDS]), nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH], a.rect,
                     at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), a.rect4};
-        dsort[v].drange = a.drange;
-        dsort[v].depoch = a.depoch;
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
     }

@@ -41,10 +41,6 @@ struct PreprocessArgs {
     int* tile_diff;   // IMG_TILE_DIFF, zeroed here (tile_hist adds into it), or null
     int tile_diff_words;
     uint32_t* rec_mask;  // GEOM_REC_MASK, zeroed here (render_bwd sets it)
-    // DepthRange: {epoch << 32 | ~min, epoch << 32 | max} of the visible depth keys, by atomicMax
-    // (the epoch of this forward wins over any earlier one: no reset needed), or null
-    unsigned long long* drange;
-    uint32_t depoch;
 };
 
 struct RenderFwdArgs {
@@ -240,10 +236,6 @@ struct SortJob {  // radix_sort's arguments for one view
     // > 0 (one pass, pairs given, keys_in null): the key is pairs[i].y >> key_hi_shift, and out_y
     // gets pairs[i].y with those bits cleared
     int key_hi_shift = 0;
-    // the forward's depth sort: the visible keys' range as preprocess stamped it (DepthRange), so
-    // the sort runs only the passes the range needs (null: all of them)
-    const unsigned long long* drange = nullptr;
-    uint32_t depoch = 0;
 };
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };

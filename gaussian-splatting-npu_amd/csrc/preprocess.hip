@@ -238,47 +238,6 @@ struct PreprocessBatch {
     int V;
 };
 
-// The workgroup's share of each view's depth-key range (PreprocessArgs::drange): min and max of
-// the visible keys over the block, stamped with the forward's epoch and folded into the view's
-// two words by atomicMax -- only when they would raise them (a plain read first), so after the
-// first workgroups hardly any atomic is issued.
-template <int NV>
-__device__ __forceinline__ void depth_range_stamp(const PreprocessBatch<NV>& A, int V, int idx)
-{
-    __shared__ uint32_t s_mn[PF_TPB / 64], s_mx[PF_TPB / 64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int v = 0; v < V; v++) {
-        const PreprocessArgs& a = A.a[v];
-        if (!a.drange) continue;  // uniform
-        const uint32_t k = idx < a.P ? a.dkey[idx] : 0xFFFFFFFFu;  // this thread's own store
-        uint32_t mn = k, mx = k == 0xFFFFFFFFu ? 0u : k;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            mn = min(mn, (uint32_t)__shfl_xor((int)mn, d, 64));
-            mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
-        }
-        if (lane == 0) {
-            s_mn[w] = mn;
-            s_mx[w] = mx;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int q = 1; q < PF_TPB / 64; q++) {
-                mn = min(mn, s_mn[q]);
-                mx = max(mx, s_mx[q]);
-            }
-            if (mn != 0xFFFFFFFFu) {
-                const unsigned long long e = (unsigned long long)a.depoch << 32;
-                const unsigned long long lo = e | (uint32_t)~mn, hi = e | mx;
-                if (lo > __hip_atomic_load(a.drange, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(a.drange, lo);
-                if (hi > __hip_atomic_load(a.drange + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                    atomicMax(a.drange + 1, hi);
-            }
-        }
-        __syncthreads();  // s_mn / s_mx reused by the next view
-    }
-}
-
 template <bool STAGED, int NV>
 __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const PreprocessBatch<NV> A, int lds_stride)
 {
@@ -304,7 +263,6 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
     if (!STAGED) {
         const float* row = a.shs ? a.shs + (size_t)idx * a.M * 3 : nullptr;
         views(row, row);
-        depth_range_stamp(A, V, idx);
         return;
     }
     if (a.dc && a.M <= 16) {  // separate dc, verbatim: dc rows at 0, rest rows (stride 3(M-1)) after them
@@ -314,7 +272,6 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
         if (wr > 0) lds_copy_in(s_rest, a.shs + (size_t)base * wr, n * wr);
         __syncthreads();
         views(s_sh + 3 * threadIdx.x, s_rest + wr * threadIdx.x - 3);
-        depth_range_stamp(A, V, idx);
         return;
     }
     if (a.dc) {  // separate dc, wide rest rows: coefficient 0 into columns 0-2, the rest after it (16 used)
@@ -325,7 +282,6 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
         __syncthreads();
         const float* row = s_sh + threadIdx.x * lds_stride;
         views(row, row);
-        depth_range_stamp(A, V, idx);
         return;
     }
     const int W3 = a.M * 3;  // multiple of 4 on this path
@@ -351,7 +307,6 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
     __syncthreads();
     const float* row = s_sh + threadIdx.x * lds_stride;
     views(row, row);
-    depth_range_stamp(A, V, idx);
 }
 
 __global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* means3D, const float* view,

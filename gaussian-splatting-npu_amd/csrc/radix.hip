@@ -44,32 +44,6 @@ struct CellSort;
 
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
-// Adaptive depth sort (DepthRange, gsr_kernels.h): the forward's preprocess stamps the range of the
-// visible depth keys with the forward's epoch; the sort then orders key - min (culled keys,
-// 0xFFFFFFFF, map to max - min + 1: last) over just the 8-bit digits that range needs, and the
-// passes past them return at once.  Sorting key - min is sorting key (no wrap: every visible key
-// is >= min), so the order is the full 32-bit stable sort's.
-struct KeyMap {
-    uint32_t mn, cull;
-    int npass;
-};
-__device__ __forceinline__ KeyMap key_map(const unsigned long long* dr, uint32_t epoch)
-{
-    const unsigned long long w0 = __builtin_nontemporal_load(dr), w1 = __builtin_nontemporal_load(dr + 1);
-    KeyMap m;
-    if ((uint32_t)(w0 >> 32) == epoch) {  // some visible key this forward
-        m.mn = ~(uint32_t)w0;
-        m.cull = (uint32_t)w1 - m.mn + 1u;
-    } else {  // none: every key is culled
-        m.mn = 0u;
-        m.cull = 0u;
-    }
-    const int bits = m.cull ? 32 - __clz(m.cull) : 1;
-    m.npass = (bits + 7) >> 3;
-    return m;
-}
-__device__ __forceinline__ uint32_t mapped_key(uint32_t key, const KeyMap& m) { return key == 0xFFFFFFFFu ? m.cull : key - m.mn; }
-
 // (1) counts[d * nchunks + c] = number of elements of chunk c with digit d (view blockIdx.y).
 struct CountJob {
     const uint32_t* keys;
@@ -79,22 +53,12 @@ struct CountJob {
     // the top bits of the id word, see TileSortJob)
     const uint2* pairs_hi;
     int hi_shift;
-    // adaptive depth sort: the key range (DepthRange), this pass's index (0 maps the raw keys)
-    const unsigned long long* drange;
-    uint32_t depoch;
-    int pass;
 };
 template <int ITEMS, typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
     const CountJob& J = B.v[blockIdx.y];
     if ((int)blockIdx.x >= J.nchunks) return;  // past this view's chunks (uniform)
-    KeyMap km = {0u, 0u, 4};
-    if (J.drange) {
-        km = key_map(J.drange, J.depoch);
-        if (J.pass >= km.npass) return;  // a pass the keys' range does not need
-    }
-    const bool map0 = J.drange && J.pass == 0;  // the first pass maps the raw keys
     const uint32_t* keys = J.keys;
     const int n = J.n;
     __shared__ uint32_t h[4][RS_MAXBINS];
@@ -118,10 +82,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch
             const uint4 q = k4[j * RS_THREADS + tid];
             k[4 * j] = q.x; k[4 * j + 1] = q.y; k[4 * j + 2] = q.z; k[4 * j + 3] = q.w;
         }
-        if (map0) {
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) k[i] = mapped_key(k[i], km);
-        }
         // a wave whose 64 keys share one digit (the depth keys' top byte, mostly) adds once: 64
         // same-address LDS atomics would serialise
         const int lane = tid & 63;
@@ -138,10 +98,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch
     } else {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
-        if (map0) {
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) k[i] = mapped_key(k[i], km);
-        }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++)
             if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
@@ -157,9 +113,6 @@ struct RowJob {
     uint32_t* counts;
     int nchunks;
     uint32_t* totals;
-    const unsigned long long* drange;  // adaptive depth sort: passes past the range's return
-    uint32_t depoch;
-    int pass;
 };
 template <typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBatch<RowJob> B)
@@ -167,8 +120,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBat
     uint32_t* counts = B.v[blockIdx.y].counts;
     const int nchunks = B.v[blockIdx.y].nchunks;
     uint32_t* totals = B.v[blockIdx.y].totals;
-    if (B.v[blockIdx.y].drange && B.v[blockIdx.y].pass >= key_map(B.v[blockIdx.y].drange, B.v[blockIdx.y].depoch).npass)
-        return;  // a pass the keys' range does not need
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -207,9 +158,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const Vie
     uint32_t* counts = RB.v[blockIdx.y].counts;
     const int nchunks = RB.v[blockIdx.y].nchunks;
     uint32_t* totals = RB.v[blockIdx.y].totals;
-    if (RB.v[blockIdx.y].drange &&
-        RB.v[blockIdx.y].pass >= key_map(RB.v[blockIdx.y].drange, RB.v[blockIdx.y].depoch).npass)
-        return;  // a pass the keys' range does not need
     __shared__ uint32_t s_row[RS_ROW_LDS];
     __shared__ uint32_t s_wave[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -276,11 +224,6 @@ struct SortPassArgs {
     // PAIR, > 0: there is no key array; the key is vals_in[i].y >> key_hi_shift and out_y receives
     // v.y with those bits cleared (the tile sort's second pass, see TileSortJob)
     int key_hi_shift;
-    // adaptive depth sort (see key_map): the last pass is the range's, not the host's; the
-    // intermediate and final outputs are both given
-    const unsigned long long* drange;
-    uint32_t depoch;
-    int pass;
 };
 
 // Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
@@ -307,13 +250,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
 {
     const SortPassArgs& a = B.v[blockIdx.y];
     if ((int)blockIdx.x >= a.nchunks) return;  // past this view's chunks (uniform)
-    KeyMap km = {0u, 0u, 4};
-    if (a.drange) {
-        km = key_map(a.drange, a.depoch);
-        if (a.pass >= km.npass) return;  // a pass the keys' range does not need
-    }
-    // the final pass: the range's last (adaptive) or the host's (no intermediate outputs given)
-    const bool last = a.drange ? a.pass == km.npass - 1 : a.keys_out == nullptr;
     constexpr int TILE = RS_THREADS * ITEMS;
     using Val = typename std::conditional<PAIR, uint2, uint32_t>::type;
     __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
@@ -349,10 +285,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     } else {
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
-        if (a.drange && a.pass == 0) {  // the raw depth keys: mapped into the range
-#pragma unroll
-            for (int i = 0; i < ITEMS; i++) key[i] = mapped_key(key[i], km);
-        }
     }
     if (PAIR && a.key_hi_shift) {
     } else if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
@@ -420,7 +352,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
             const uint32_t d = digit_of(k, a.shift, mask);
             const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
             const Val v = s_vals[lpos];
-            if (!last) {
+            if (a.keys_out) {
                 a.keys_out[dst] = k;
                 reinterpret_cast<Val*>(a.vals_out)[dst] = v;
             } else {
@@ -930,10 +862,9 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             for (int v = 0; v < nv; v++) {
                 const SortJob& j = jobs[v0 + v];
                 const int nchunks = (int)rs_chunks(j.n);
-                cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j), j.key_hi_shift ? j.pairs : nullptr, j.key_hi_shift,
-                           j.drange, j.depoch, p};
+                cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j), j.key_hi_shift ? j.pairs : nullptr, j.key_hi_shift};
                 if (j.key_hi_shift) cb.v[v].keys = nullptr;
-                rb.v[v] = {sort_counts(j), nchunks, sort_totals(j), j.drange, j.depoch, p};
+                rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
                 SortPassArgs& a = sb.v[v];
                 a.n = j.n;
                 a.shift = shift;
@@ -941,23 +872,18 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.nchunks = nchunks;
                 a.keys_in = kin[v];
                 a.vals_in = vin[v];
-                // adaptive: any pass may be the range's last, so every pass gets both kinds of outputs
-                const bool fin = last || j.drange;
                 a.keys_out = last ? nullptr : ((p & 1) ? j.k1 : j.k0);
                 a.vals_out = last ? nullptr : ((p & 1) ? j.v1 : j.v0);
                 a.out_x = j.out_x;
                 a.out_y = j.out_y;
                 a.sorted_keys = j.sorted_keys;
-                a.rects = (fin && !pair) ? j.rects : nullptr;
+                a.rects = (last && !pair) ? j.rects : nullptr;
                 a.rects4_in = p == 0 ? j.rects4 : nullptr;
-                a.sorted_rects = (fin && (!pair || j.rects4)) ? j.sorted_rects : nullptr;
+                a.sorted_rects = (last && (!pair || j.rects4)) ? j.sorted_rects : nullptr;
                 a.sorted_counts = j.sorted_counts;
                 a.row_prefix = sort_counts(j);
                 a.totals = sort_totals(j);
                 a.key_hi_shift = j.key_hi_shift;
-                a.drange = j.drange;
-                a.depoch = j.depoch;
-                a.pass = p;
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
