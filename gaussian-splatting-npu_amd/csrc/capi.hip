@@ -601,7 +601,6 @@ static RenderFwdArgs render_fwd_args(char* gb, char* bb, char* ib, int P, int L,
     r.bg = background;
     r.final_T = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
-    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.out_color = out_color;
     r.invdepth = depth;
     r.hit = L > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
@@ -973,7 +972,6 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
-    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
@@ -1065,7 +1063,6 @@ static RenderBwdArgs render_bwd_args(int P, int R, const float* background, int 
     r.splat = at<float4>(gb, g.off[GEOM_SPLAT]);
     r.final_Ts = at<float>(ib, im.off[IMG_FINAL_T]);
     r.n_contrib = at<uint32_t>(ib, im.off[IMG_N_CONTRIB]);
-    r.accum = at<float4>(ib, im.off[IMG_ACCUM]);
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);

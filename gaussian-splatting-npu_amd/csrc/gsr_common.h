@@ -190,7 +190,6 @@ enum ImageArray {
     IMG_RANGES = 0,       // u32x2[T]
     IMG_FINAL_T,          // f32[N]
     IMG_N_CONTRIB,        // u32[N]
-    IMG_ACCUM,            // f32x4[N] blended colour before the background + blended inverse depth
     IMG_TILE_ORDER,       // u32[T] render launch order: tiles by decreasing work (longest first)
     IMG_TILE_WORK,        // u32[T] largest n_contrib of each tile (written by render_fwd, orders render_bwd)
     IMG_TILE_DIFF,        // i32[(grid_x + 1) (grid_y + 1)] 2-D difference array of the tile rects (tile_hist;
@@ -278,7 +277,7 @@ inline ImageLayout image_layout(int W, int H)
     size_t n = (size_t)W * H;
     const size_t gx = (size_t)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X), gy = (size_t)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y);
     size_t t = gx * gy;
-    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n, 16 * n, 4 * t, 4 * t, 4 * (gx + 1) * (gy + 1)};
+    size_t sizes[IMG_COUNT] = {8 * t, 4 * n, 4 * n, 4 * t, 4 * t, 4 * (gx + 1) * (gy + 1)};
     ImageLayout l;
     size_t o = 0;
     for (int i = 0; i < IMG_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

@@ -56,7 +56,6 @@ struct RenderFwdArgs {
     uint32_t* n_contrib;
     float* out_color;
     float* invdepth;
-    float4* accum;  // IMG_ACCUM: {C_r, C_g, C_b, invdepth} before the background
     uint8_t* hit;   // BIN_HIT: contributing quadrants of every processed list entry (out)
 };
 
@@ -71,7 +70,6 @@ struct RenderBwdArgs {
     const float4* splat;
     const float* final_Ts;
     const uint32_t* n_contrib;
-    const float4* accum;  // IMG_ACCUM written by the forward
     const float* dL_dpixels;
     const float* dL_invdepths;  // (1,H,W) or null
     const uint32_t* slot;       // gradient-record slot of each sorted position

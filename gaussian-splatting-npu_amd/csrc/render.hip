@@ -22,7 +22,7 @@
 //
 // Backward: one wave64 per tile, split into four 16-lane groups, one per quadrant, each lane
 // owning 4 pixels of its group's quadrant; each group walks only the entries that contributed
-// in its quadrant in the forward, front to back.  The ten per-(pixel, Gaussian) gradient terms
+// in its quadrant in the forward, back to front (as the reference).  The ten per-(pixel, Gaussian) gradient terms
 // are reduced on chip (in-lane over the 4 pixels, a transposed cross-lane reduction over the
 // group, the <= 4 quadrant partials added in LDS in a fixed order) and stored once per
 // (tile, Gaussian) entry -- no global atomics, bitwise-reproducible sums
@@ -451,30 +451,15 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
         a.out_color[1 * HW + pix_id] = C1 + T * a.bg[1];
         a.out_color[2 * HW + pix_id] = C2 + T * a.bg[2];
         if (a.invdepth) a.invdepth[pix_id] = ID;
-        a.accum[pix_id] = make_float4(C0, C1, C2, ID);
     }
 }
 
 // ---- transposed wave reduction (CDNA4 cross-lane ops, no LDS) ------------------------------
-// The swaps exchange the two registers in place (both operands are read and written).  Through
-// the builtin the compiler copies one operand to a scratch register before each swap (a v_mov per
-// exchanged pair); as inline asm on two "+v" operands it swaps the values where they live.  The
-// s_nop 1 is the gfx950 hazard a VALU write -> v_permlane*_swap read requires (two wait states),
-// which the compiler cannot see inside the asm.
-__device__ __forceinline__ void xswap32(float& a, float& b)
-{
-    asm("s_nop 1\n\tv_permlane32_swap_b32_e32 %0, %1" : "+v"(a), "+v"(b));
-}
-__device__ __forceinline__ void xswap16(float& a, float& b)
-{
-    asm("s_nop 1\n\tv_permlane16_swap_b32_e32 %0, %1" : "+v"(a), "+v"(b));
-}
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x)
-{
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
-}
-constexpr int DPP_ROW_MIRROR = 0x140, DPP_ROW_HALF_MIRROR = 0x141;
+// The swaps (GSR_SWAP8 below) exchange the two registers in place (both operands are read and
+// written).  Through the builtin the compiler copies one operand to a scratch register before each
+// swap (a v_mov per exchanged pair); as inline asm on "+v" operands it swaps the values where they
+// live.  The s_nop 1 is the gfx950 hazard a VALU write -> v_permlane*_swap read requires (two wait
+// states), which the compiler cannot see inside the asm.
 
 // Sums 32 per-lane values over each of four 16-lane groups and returns in r0 / r1 of lane l the
 // group totals of v[2 (l >> 2)] / v[2 (l >> 2) + 1].  Recursive halving: each exchange step hands
@@ -530,21 +515,24 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
     r1 = v[1];
 }
 
-// State of two pixels of the backward pass (backward.cu:498-528, restated front to back).
-// Pixels outside the image carry last_contributor = 0, so no list entry contributes to them.
+// State of two pixels of the backward pass (backward.cu:498-528).  Pixels outside the image carry
+// last_contributor = 0, so no list entry contributes to them.
 //
-// The reference replays each pixel's list back to front, rebuilding T by division and the
-// colour behind entry j (accum_rec) incrementally.  The same gradient in forward order:
-// with T_j the transmittance in front of j, cd_j = c_j . dL/dpixel (+ invdepth_j . dL/dinvdepth),
-// and B_j = R - sum_{k <= j} alpha_k T_k cd_k, R = out_color . dL/dpixel (+ invdepth .
-// dL/dinvdepth) (out_color includes the background term T_final * bg),
-//     dL/dalpha_j = T_j cd_j - B_j / (1 - alpha_j)                  (backward.cu:577-615)
-// because B_j = (colour behind j) . dL + T_final * (bg . dL).  T_j is then the forward's own
-// running product (bit-identical to forward.cu:372-383), no division by (1 - alpha) is needed to
-// rebuild it, and the per-pixel state shrinks to T, B and dL/dpixel.
+// Each pixel's list is replayed back to front, as the reference does: T is rebuilt from final_T
+// by the reciprocal of (1 - alpha) (backward.cu:581), and the colour behind entry j enters as ONE
+// normalised scalar, Bn_j = accum_rec_j . dL/dpixel (+ the inverse-depth channel), since dL/dpixel
+// is constant along the walk: Bn_{j-1} = Bn_j + alpha_j (cd_j - Bn_j), cd_j = c_j . dL/dpixel, a
+// convex recurrence (backward.cu:586-600), and
+//     dL/dalpha_j = T_j (cd_j - Bn_j) - T_final / (1 - alpha_j) (bg . dL/dpixel)   (:601-612).
+// Rounds 1-3 walked front to back with B_j = R - sum_{k <= j} alpha_k T_k cd_k (R = the forward's
+// out_color . dL): as cheap per entry, but B is a difference of O(1) terms that ends small, so its
+// absolute rounding error (~eps |R| per entry) grew to ~5x the reference's relative error on the
+// chair fixture (tools/dbg/bwd_accuracy.py: p99.9 record error 2-8e-3 vs 0.7-1.3e-3 for the
+// reference's order against float64; this walk: 0.4-1.2e-3).  The walk needs no accumulated
+// colour from the forward either (16 B per pixel neither written nor read).
 struct BwdPair {
-    v2f T, B, dp0, dp1, dp2, dinv;
-    uint32_t lc0, lc1;  // last_contributor
+    v2f T, Bn, K, dp0, dp1, dp2, dinv;  // K = T_final (bg . dL/dpixel)
+    uint32_t lc0, lc1;                  // last_contributor
 };
 
 // A lane's sums over its two pixel pairs for one Gaussian: the colour and invdepth terms per
@@ -575,14 +563,16 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, cons
     const v2f a = Gc * co.w;  // alpha before the 0.99 clamp (0 where the pixel is not reached)
     const v2f alpha = {fminf(0.99f, a.x), fminf(0.99f, a.y)};
     const v2f one_m = 1.f - alpha;
-    // v_rcp_f32 (1 ulp) in place of the IEEE division of backward.cu:615
+    // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:581,612 (exact for
+    // alpha = 0: T stays bitwise unchanged for entries that do not reach the pixel)
     const v2f r_om = {__builtin_amdgcn_rcpf(one_m.x), __builtin_amdgcn_rcpf(one_m.y)};
+    s.T = s.T * r_om;  // T in front of this entry
     v2f cd = fma2((v2f)(col.z), s.dp2, fma2((v2f)(col.y), s.dp1, (v2f)(col.x) * s.dp0));
     if constexpr (HAS_INV) cd = fma2((v2f)(col.w), s.dinv, cd);
+    const v2f diff = cd - s.Bn;  // (c - accum_rec) . dL/dpixel
     const v2f aT = alpha * s.T;  // dL/dcolour / dL/dpixel (backward.cu:586-590)
-    s.B = fma2(-aT, cd, s.B);
-    const v2f dL = fma2(s.T, cd, -s.B * r_om);
-    s.T = s.T * one_m;
+    const v2f dL = fma2(s.T, diff, -(r_om * s.K));
+    s.Bn = fma2(alpha, diff, s.Bn);  // the colour behind the entry in front
     const v2f u = Gc * dL;
     const v2f ux = u * dx;
     if constexpr (FIRST) {
@@ -632,10 +622,10 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // Backward: ONE wave per 16x16 tile, so there are no workgroup barriers in the main loop and no
 // cross-wave combine.  Lane group quad_group(lane) owns quadrant (g & 1, g >> 1); lane
 // l >> 2 of it the pixels (x, x + 4) and (x + 2, x + 6) of one quadrant row as two packed pairs.
-// The list is walked front to back in batches of 64 entries up to the tile's largest n_contrib:
+// The list below the tile's largest n_contrib is walked back to front in batches of 64 entries:
 // each lane stages the record of its entry if that entry contributed anywhere in the forward, and
 // each quadrant's contributing entries are listed in LDS (ballot + mbcnt, list order).  Iteration
-// i then evaluates the i-th entry of every quadrant at once (pixels of different quadrants share no
+// i then evaluates the i-th last entry of every quadrant at once (pixels of different quadrants share no
 // state; a group past its list evaluates a staged record at position "never", which adds zeros),
 // three iterations per transposed reduction; the groups add their partial totals into the
 // entries' LDS sums two groups at a time (two sets of sums), and at the end of the batch every contributing
@@ -683,7 +673,6 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     // Pixel state: every load issued before the first use (clamped addresses, masked after), so
     // the prologue costs one memory round trip instead of one per pixel.
     float Tf[4], dp0[4], dp1[4], dp2[4], dinv[4];
-    float4 acc[4];
     uint32_t lc[4];
     bool inside[4];
 #pragma unroll
@@ -692,7 +681,6 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         inside[p] = px < (uint32_t)a.W && qy < (uint32_t)a.H;
         const uint32_t pix_id = inside[p] ? (uint32_t)a.W * qy + px : 0u;
         Tf[p] = a.final_Ts[pix_id];
-        acc[p] = a.accum[pix_id];
         lc[p] = a.n_contrib[pix_id];
         dp0[p] = a.dL_dpixels[0 * HW + pix_id];
         dp1[p] = a.dL_dpixels[1 * HW + pix_id];
@@ -701,23 +689,22 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     }
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
-    float R[4];  // out_color . dL/dpixel (+ invdepth . dL/dinvdepth): B before the first entry
+    float K[4];  // T_final (bg . dL/dpixel): the background's share of dL/dalpha (backward.cu:610-612)
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         if (!inside[p]) {
             Tf[p] = 0.f;
-            acc[p] = make_float4(0.f, 0.f, 0.f, 0.f);
             lc[p] = 0u;
             dp0[p] = dp1[p] = dp2[p] = dinv[p] = 0.f;
         }
-        R[p] = (acc[p].x + Tf[p] * bg0) * dp0[p] + (acc[p].y + Tf[p] * bg1) * dp1[p] +
-               (acc[p].z + Tf[p] * bg2) * dp2[p] + acc[p].w * dinv[p];
+        K[p] = Tf[p] * (bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p]);
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         BwdPair& s = st[h];
-        s.T = (v2f)(1.f);
-        s.B = {R[2 * h], R[2 * h + 1]};
+        s.T = {Tf[2 * h], Tf[2 * h + 1]};
+        s.Bn = (v2f)(0.f);
+        s.K = {K[2 * h], K[2 * h + 1]};
         s.dp0 = {dp0[2 * h], dp0[2 * h + 1]};
         s.dp1 = {dp1[2 * h], dp1[2 * h + 1]};
         s.dp2 = {dp2[2 * h], dp2[2 * h + 1]};
@@ -744,21 +731,24 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     // pixel) are evaluated; entries that contributed nowhere (and list positions >= tmax) get no
     // record: valid[slot] stays 0 and preprocess_bwd skips them.
 
-    // list ids, slots and contribution bits are fetched one batch ahead; the records of the
+    // The list is walked back to front in batches of 64 (the last batch first); list ids, slots
+    // and contribution bits are fetched one batch ahead (the batch in front); the records of the
     // batch's contributing entries are all in flight before the first is used
     const int last = (int)tmax - 1;
+    const int pfirst = tmax > 0 ? (last & ~63) : -64;
     uint32_t next_id = 0, next_slot = 0, next_hit = 0;
     if (tmax > 0) {
-        next_id = a.point_list[range.x + min(lane, last)];
-        next_slot = a.slot[range.x + min(lane, last)];
-        next_hit = a.hit[range.x + min(lane, last)];
+        next_id = a.point_list[range.x + min(pfirst + lane, last)];
+        next_slot = a.slot[range.x + min(pfirst + lane, last)];
+        next_hit = a.hit[range.x + min(pfirst + lane, last)];
     }
-    for (int p0 = 0; p0 < (int)tmax; p0 += 64) {
+    for (int p0 = pfirst; p0 >= 0; p0 -= 64) {
         const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
         const uint32_t id = next_id, myslot = next_slot, hit = next_hit;
-        next_id = a.point_list[range.x + min(pos_l + 64, last)];
-        next_slot = a.slot[range.x + min(pos_l + 64, last)];
-        next_hit = a.hit[range.x + min(pos_l + 64, last)];
+        const int pn = max(p0 - 64, 0) + lane;  // (the first batch re-reads itself: never used)
+        next_id = a.point_list[range.x + pn];
+        next_slot = a.slot[range.x + pn];
+        next_hit = a.hit[range.x + pn];
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         // only entries that contributed somewhere in the forward are read (43 % of the entries
         // below tmax contributed nowhere: their 48-B record gathers are skipped)
@@ -788,7 +778,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // Each quadrant group walks its own entries in list order (pixels of different quadrants
+        // Each quadrant group walks its own entries back to front (pixels of different quadrants
         // share no state), iteration i of all four groups at once; a group past its count
         // evaluates a staged record at position "never" (alpha = 0: state unchanged, zero terms).
         const int fv = (int)__builtin_ctzll(any);
@@ -800,7 +790,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
                 act[jj] = i0 + jj < mycnt;
-                ej[jj] = act[jj] ? (int)s_lq[grp][i0 + jj] : fv;
+                ej[jj] = act[jj] ? (int)s_lq[grp][mycnt - 1 - (i0 + jj)] : fv;
             }
             float v[32];
             // GSR_BWD_PREFETCH: entry jj + 1's staged record is read from LDS while entry jj computes

@@ -258,7 +258,13 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
  * any view), dL_dmean2D: each view's (P,3) screen-space gradient); R, tan_fovx and tan_fovy are
  * host arrays.  dL_dcolor (may be NULL) and the parameter gradients are the sums over the views;
  * `accumulate` as in gsr_backward_dc_acc.  Results equal the sum of V gsr_backward_dc calls up to
- * fp32 summation order. */
+ * fp32 summation order.
+ * radii: accepted for the reference's argument list but NOT read -- the batched preprocess
+ * backward (and gsr_backward_preprocess_views / _range below) takes a Gaussian's visibility in a
+ * view from that view's forward state (its tiles_touched, i.e. radius > 0 as the forward computed
+ * it), where the reference gates on the radii passed in (backward.cu:163,420).  The two agree for
+ * radii produced by the forward; a caller that edits radii between forward and backward has that
+ * edit ignored here (the single-view gsr_backward* entry points do read radii). */
 int gsr_backward_views(int V, int P, int D, int M, const int* R, const float* background, int width, int height,
                        const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                        const float* opacities, const float* scales, float scale_modifier, const float* rotations,

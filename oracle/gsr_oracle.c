@@ -675,6 +675,99 @@ static void render_bwd_tile(const oracle_state* st, uint32_t tx, uint32_t ty, co
         }
 }
 
+/* The same per-pixel walk with the gradient arithmetic in float64 -- the accuracy yardstick of the
+ * parity tests (tests/common.py check_rel_truth), not a restatement: the contribution DECISIONS
+ * (power > 0, alpha < 1/255, the last contributor) are the float32 ones above, so both walks sum
+ * the same terms; G, alpha, the transmittances (a front-to-back float64 product, not the
+ * reference's division chain), the colour behind each entry and every accumulation are float64. */
+static inline void atomic_addd(double* p, double v)
+{
+#pragma omp atomic
+    *p += v;
+}
+static void render_bwd_tile_f64(const oracle_state* st, uint32_t tx, uint32_t ty, const float* bg, const float* colors,
+                                const float* dL_dpixels, const float* dL_invdepths, double* g_mean2D, double* g_conic,
+                                double* g_opacity, double* g_colors, double* g_invdepths, double* scratch)
+{
+    const int W = st->W, H = st->H;
+    const uint32_t* range = st->ranges + 2 * (ty * st->gx + tx);
+    const double ddelx_dx = 0.5 * W, ddely_dy = 0.5 * H;
+    /* scratch: per contributing entry (k, G, alpha, T in front) of one pixel */
+    for (uint32_t ly = 0; ly < BLOCK_Y; ly++)
+        for (uint32_t lx = 0; lx < BLOCK_X; lx++) {
+            uint32_t pxi = tx * BLOCK_X + lx, pyi = ty * BLOCK_Y + ly;
+            if (!(pxi < (uint32_t)W && pyi < (uint32_t)H)) continue;
+            uint32_t pix_id = (uint32_t)W * pyi + pxi;
+            const float pfx = (float)pxi, pfy = (float)pyi;
+            const uint32_t last_contributor = st->n_contrib[pix_id];
+            double dpx[3];
+            for (int i = 0; i < 3; i++) dpx[i] = dL_dpixels[i * H * W + pix_id];
+            const double dinv = dL_invdepths ? dL_invdepths[pix_id] : 0.0;
+            /* front to back: the contributing entries, float32 decisions, float64 values */
+            int n = 0;
+            double T = 1.0;
+            for (uint32_t j = 0; j < last_contributor && range[0] + j < range[1]; j++) {
+                uint32_t gid = st->vals[range[0] + j];
+                const float* co = st->conic_opacity + 4 * (size_t)gid;
+                const float dxf = st->means2D[2 * gid] - pfx, dyf = st->means2D[2 * gid + 1] - pfy;
+                const float power = -0.5f * (co[0] * dxf * dxf + co[2] * dyf * dyf) - co[1] * dxf * dyf;
+                if (power > 0.0f) continue;
+                const float alpha_f = fminf_(0.99f, co[3] * expf(power));
+                if (alpha_f < 1.0f / 255.0f) continue;
+                const double dx = dxf, dy = dyf;
+                const double pw = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                const double G = exp(pw);
+                const double alpha = fmin(0.99, co[3] * G);
+                double* e = scratch + 4 * (size_t)n++;
+                e[0] = (double)gid;
+                e[1] = G;
+                e[2] = alpha;
+                e[3] = T;
+                T *= 1.0 - alpha;
+            }
+            const double T_final = T;
+            double bg_dot = 0.0;
+            for (int i = 0; i < 3; i++) bg_dot += (double)bg[i] * dpx[i];
+            /* back to front: behind = colour (and inverse depth) . dL behind the entry, absolute */
+            double behind = T_final * bg_dot;
+            for (int q = n - 1; q >= 0; q--) {
+                const double* e = scratch + 4 * (size_t)q;
+                const uint32_t gid = (uint32_t)e[0];
+                const double G = e[1], alpha = e[2], Tj = e[3];
+                const float* co = st->conic_opacity + 4 * (size_t)gid;
+                const double dx = (double)(st->means2D[2 * gid] - pfx), dy = (double)(st->means2D[2 * gid + 1] - pfy);
+                double cd = 0.0;
+                for (int ch = 0; ch < 3; ch++) {
+                    cd += (double)colors[gid * 3 + ch] * dpx[ch];
+                    atomic_addd(&g_colors[gid * 3 + ch], alpha * Tj * dpx[ch]);
+                }
+                if (dL_invdepths) {
+                    const double invd = 1.0 / (double)st->depths[gid];
+                    cd += invd * dinv;
+                    atomic_addd(&g_invdepths[gid], alpha * Tj * dinv);
+                }
+                /* dL/dalpha = T_j (c_j . dL) - (light behind j) / (1 - alpha_j) */
+                const double dL_dalpha = Tj * cd - behind / (1.0 - alpha);
+                behind += alpha * Tj * cd;
+                const double dL_dG = co[3] * dL_dalpha;
+                const double gdx = G * dx, gdy = G * dy;
+                const double dG_ddelx = -gdx * co[0] - gdy * co[1];
+                const double dG_ddely = -gdy * co[2] - gdx * co[1];
+                atomic_addd(&g_mean2D[3 * gid + 0], dL_dG * dG_ddelx * ddelx_dx);
+                atomic_addd(&g_mean2D[3 * gid + 1], dL_dG * dG_ddely * ddely_dy);
+                atomic_addd(&g_conic[4 * gid + 0], -0.5 * gdx * dx * dL_dG);
+                atomic_addd(&g_conic[4 * gid + 1], -0.5 * gdx * dy * dL_dG);
+                atomic_addd(&g_conic[4 * gid + 3], -0.5 * gdy * dy * dL_dG);
+                atomic_addd(&g_opacity[gid], G * dL_dalpha);
+            }
+        }
+}
+
+static int g_bwd_f64 = 0;
+/* 1: gsr_oracle_backward runs the render backward in float64 (render_bwd_tile_f64) and rounds its
+ * per-Gaussian sums to float32 once, before the (float32) preprocess backward. */
+void gsr_oracle_set_bwd_f64(int on) { g_bwd_f64 = on; }
+
 static inline float sq(float x) { return x * x; }
 
 /* backward.cu:147-326 (computeCov2DCUDA) for one Gaussian */
@@ -943,10 +1036,44 @@ int gsr_oracle_backward(void* p, const float* bg, const float* means3D, const fl
     const float focal_x = W / (2.0f * tan_fovx);
     const float* color_ptr = colors_precomp ? colors_precomp : st->rgb;
     size_t T = (size_t)st->gx * st->gy;
+    if (g_bwd_f64) {
+        double* acc = (double*)calloc(Pn * 12, sizeof(double));  /* mean2D 3 | conic 4 | opacity 1 | colour 3 | invdepth 1 */
+        uint32_t maxlen = 0;
+        for (size_t t = 0; t < T; t++) maxlen = maxlen > st->ranges[2 * t + 1] - st->ranges[2 * t] ? maxlen : st->ranges[2 * t + 1] - st->ranges[2 * t];
+        if (!acc) return -1;
+        int fail = 0;
+#pragma omp parallel
+        {
+            double* scratch = (double*)malloc(((size_t)maxlen + 1) * 4 * sizeof(double));
+            if (!scratch) {
+#pragma omp atomic write
+                fail = 1;
+            } else {
+#pragma omp for schedule(dynamic, 4)
+                for (int t = 0; t < (int)T; t++)
+                    render_bwd_tile_f64(st, (uint32_t)t % st->gx, (uint32_t)t / st->gx, bg, color_ptr, dL_dpix,
+                                        dL_dinvdepth_pix, acc, acc + 3 * Pn, acc + 7 * Pn, acc + 8 * Pn, acc + 11 * Pn,
+                                        scratch);
+                free(scratch);
+            }
+        }
+        if (fail) {
+            free(acc);
+            return -1;
+        }
+        for (size_t i = 0; i < 3 * Pn; i++) dL_dmean2D[i] = (float)acc[i];
+        for (size_t i = 0; i < 4 * Pn; i++) dL_dconic[i] = (float)acc[3 * Pn + i];
+        for (size_t i = 0; i < Pn; i++) dL_dopacity[i] = (float)acc[7 * Pn + i];
+        for (size_t i = 0; i < 3 * Pn; i++) dL_dcolor[i] = (float)acc[8 * Pn + i];
+        if (dL_dinvdepths)
+            for (size_t i = 0; i < Pn; i++) dL_dinvdepths[i] = (float)acc[11 * Pn + i];
+        free(acc);
+    } else {
 #pragma omp parallel for schedule(dynamic, 4)
-    for (int t = 0; t < (int)T; t++)
-        render_bwd_tile(st, (uint32_t)t % st->gx, (uint32_t)t / st->gx, bg, color_ptr, dL_dpix, dL_dinvdepth_pix,
-                        dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepths);
+        for (int t = 0; t < (int)T; t++)
+            render_bwd_tile(st, (uint32_t)t % st->gx, (uint32_t)t / st->gx, bg, color_ptr, dL_dpix, dL_dinvdepth_pix,
+                            dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepths);
+    }
 
     const float* cov3D_ptr = cov3D_precomp ? cov3D_precomp : st->cov3D;
 #pragma omp parallel for schedule(static)

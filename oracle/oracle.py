@@ -101,7 +101,9 @@ class OracleRaster:
                                  out.ctypes.data_as(ctypes.c_void_p))
         return out
 
-    def backward(self, dL_dcolor, dL_dinvdepth=None):
+    def backward(self, dL_dcolor, dL_dinvdepth=None, f64=False):
+        """f64: the render backward's arithmetic in float64 (gsr_oracle_set_bwd_f64) -- the
+        accuracy yardstick of tests/common.check_rel_truth, not the reference's float32 order."""
         a = self.args
         P, M = self.P, self.M
         g = dict(dL_dmean2D=np.zeros((P, 3), np.float32), dL_dconic=np.zeros((P, 2, 2), np.float32),
@@ -111,6 +113,7 @@ class OracleRaster:
                  dL_drotations=np.zeros((P, 4), np.float32))
         dc = _np(dL_dcolor)
         di = _np(dL_dinvdepth)
+        lib().gsr_oracle_set_bwd_f64(ctypes.c_int(int(bool(f64))))
         rc = lib().gsr_oracle_backward(
             ctypes.c_void_p(self.h), _p(a["bg"]), _p(a["means3D"]), _p(a["shs"]), _p(a["colors"]),
             _p(a["opacities"]), _p(a["scales"]), ctypes.c_float(self.scale_modifier), _p(a["rots"]),
@@ -119,6 +122,7 @@ class OracleRaster:
             _p(g["dL_dopacity"]), _p(g["dL_dcolors"]), _p(g["dL_dmeans3D"]), _p(g["dL_dcov3D"]),
             _p(g["dL_dsh"]) if M else None, _p(g["dL_dscales"]), _p(g["dL_drotations"]),
             ctypes.c_int(self.nthreads))
+        lib().gsr_oracle_set_bwd_f64(ctypes.c_int(0))
         if rc != 0:
             raise RuntimeError("oracle backward failed")
         return g

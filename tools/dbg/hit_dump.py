@@ -27,7 +27,7 @@ il = _C.image_layout(W, H)
 T = 120 * 68
 hit = binning[bl[-2]:bl[-2] + L].cpu().numpy()  # BIN_HIT
 ranges = img[il[0]:il[0] + 8 * T].view(torch.int32).cpu().numpy().reshape(-1, 2)
-work = img[il[5]:il[5] + 4 * T].view(torch.int32).cpu().numpy()  # IMG_TILE_WORK
+work = img[il[4]:il[4] + 4 * T].view(torch.int32).cpu().numpy()  # IMG_TILE_WORK
 os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
 np.savez_compressed(os.path.join(root, "gpurun_out", "hit_dump.npz"), hit=hit, ranges=ranges, work=work, L=L)
 print("dumped", L, "entries")

@@ -22,7 +22,7 @@ il = _C.image_layout(W, H)
 T = 120 * 68
 hit = binning[bl[-2]:bl[-2] + L].cpu().numpy()  # BIN_HIT: the last array
 ranges = img[il[0]:il[0] + 8 * T].view(torch.int32).cpu().numpy().reshape(-1, 2)
-work = img[il[5]:il[5] + 4 * T].view(torch.int32).cpu().numpy()  # IMG_TILE_WORK
+work = img[il[4]:il[4] + 4 * T].view(torch.int32).cpu().numpy()  # IMG_TILE_WORK
 sel = np.concatenate([hit[a:a + w] for (a, b), w in zip(ranges, work)])
 print("L", L, "entries below tmax", sel.size, "fraction of L", sel.size / L)
 nz = sel[sel != 0]
