@@ -6,7 +6,9 @@ Per case: the oracle re-run on the box reproduces the fixture's integer digests 
 made in the build container); num_rendered, radii, the sorted tile|depth keys, their Gaussian ids and the
 tile ranges bit-exact; colour / invdepth / final_T / n_contrib through common.check_render; all
 eight backward outputs within 1e-4 of max|ref| outside the walks of flipped pixels, every outlier
-attributed (common.check_grad_attributed).  And the HIP distCUDA2 of the points equals the
+attributed (common.check_grad_attributed); per element no further from the float64 gradient (the
+oracle's render backward in float64 on the same decisions) than 1.5x the reference's own float32
+order is (common.check_rel_truth), and within REL_P999 of the oracle (common.check_rel).  And the HIP distCUDA2 of the points equals the
 fixture's brute-force dist2 bit for bit (the scales create_from_pcd derives from it).
 """
 import os
@@ -81,7 +83,9 @@ def test_chair_case(chair, case):
         bg_t, sc["means3D"], radii, e, sc["opacities"], sc["scales"], sc["rotations"], 1.0, e, vm, pm, cam.tanfovx,
         cam.tanfovy, gc, gi, sc["shs"], deg, cp, geom, L, binning, img, aa, False)
     torch.cuda.synchronize()
+    g64 = o.backward(gc.cpu(), gi.cpu(), f64=True)  # the accuracy yardstick (check_rel_truth)
     for n, t in zip(make_chair.GRAD_NAMES, out):
         hip, ref = t.cpu().numpy(), og[n].reshape(t.shape)
         common.check_grad_attributed(f"{tag} {n}", hip, ref, affected)
+        common.check_rel_truth(f"{tag} {n}", hip, ref, g64[n].reshape(t.shape))
         common.check_rel(f"{tag} {n}", hip, ref)

@@ -86,6 +86,29 @@ def test_oracle_backward_matches_autograd(mode, antialiasing):
         assert ok, f"{mode} aa={antialiasing}: oracle d{k} vs autograd rel err {rel:.3e}"
 
 
+@pytest.mark.parametrize("antialiasing", [False, True])
+def test_oracle_f64_backward_is_the_float64_gradient(antialiasing):
+    """The oracle's float64 render-backward mode (the yardstick of common.check_rel_truth) against
+    torch.autograd of the dense float64 restatement: an order of magnitude closer than the float32
+    reference order is (only the float32 preprocess backward and the float32 inputs remain)."""
+    case = _small_case()
+    o, og = common.run_oracle(case, "sh_scales", antialiasing=antialiasing)
+    g64 = o.backward(case["grad_color"], case["grad_invdepth"], f64=True)
+    inp = _dense_inputs(case, "sh_scales")
+    out = dense_ref.dense_render(inp, dense_ref.ring_cam(case["cam"]), case["H"], case["W"], 3,
+                                 case["bg"].to(torch.float64), antialiasing=antialiasing)
+    _decisions_agree(o, out)
+    dense_ref.loss_of(out, case["grad_color"].to(torch.float64), case["grad_invdepth"].to(torch.float64)).backward()
+    for k, t in inp.items():
+        ref = t.grad.numpy()
+        _, rel32 = common.allclose_rel(og[PAIRS[k]].reshape(t.shape), ref)
+        ok, rel64 = common.allclose_rel(g64[PAIRS[k]].reshape(t.shape), ref, rtol=2e-5, atol=1e-9)
+        assert ok, f"f64 d{k} vs autograd rel err {rel64:.3e} (float32 order: {rel32:.3e})"
+    # the flag is reset: a following backward is the float32 one again
+    again = o.backward(case["grad_color"], case["grad_invdepth"])
+    np.testing.assert_array_equal(again["dL_dmean2D"], og["dL_dmean2D"])
+
+
 def _fd_case(seed=5):
     """<= 16 Gaussians in front of view 0 of the ring, overlapping on a 48x40 image: every one
     visible, alpha < 0.99 everywhere (no clamp kink), SH colours > 0 (no clamp kink)."""

@@ -25,6 +25,7 @@ import synthetic  # noqa: E402
 from test_chair import load_chair  # noqa: E402
 
 f32 = np.float32
+RNG = np.random.default_rng(1)
 LOG2E = f32(1.4426950408889634)
 
 
@@ -49,7 +50,7 @@ def run(case=2, ntiles=200, seed=0):
     rng = np.random.default_rng(seed)
     nonempty = np.nonzero(ranges[:, 1] > ranges[:, 0])[0]
     tiles = rng.choice(nonempty, size=min(ntiles, nonempty.size), replace=False)
-    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f")}
+    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1")}
     for t in tiles:
         tx, ty = t % gx, t // gx
         xs, ys = tile_pixels(tx, ty, W, H)
@@ -105,12 +106,12 @@ def run(case=2, ntiles=200, seed=0):
             aT_r[j] = np.where(c, alr[j] * Tr, 0)
         out["ref"].append(records(Gr, dLda_r, aT_r, dxf, dyf, dp, contrib))
         # ---- hip: forward-order B ----
-        for var in ("hip", "hip_split", "hip_chan", "hip_b2f"):
+        for var in ("hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1"):
             out[var].append(hip_records(var, contrib, Gr, alr, col, dp, dxf, dyf, fT[pid], bgv))
     f64 = np.concatenate(out["f64"])
     sel = np.abs(f64) > 1e-3 * np.abs(f64).max(axis=0, keepdims=True)
     names = ["opacity", "mean_x", "mean_y", "conic_a", "conic_b", "conic_c", "col_r", "col_g", "col_b"]
-    for k in ("ref", "hip", "hip_split", "hip_chan", "hip_b2f"):
+    for k in ("ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1"):
         x = np.concatenate(out[k]).astype(np.float64)
         rel = np.abs(x - f64) / np.where(sel, np.abs(f64), 1)
         line = " ".join(f"{nm}={np.quantile(rel[:, i][sel[:, i]], 0.999):.1e}" for i, nm in enumerate(names))
@@ -127,7 +128,32 @@ def records(G, dLda, aT, dx, dy, dp, contrib):
 
 def hip_records(var, contrib, G, al, col, dp, dx, dy, fT, bgv):
     n, npx = G.shape
-    if var == "hip_b2f":  # back to front: T rebuilt by the reciprocal, normalised colour behind
+    def rcp(x, noisy):
+        r = (f32(1) / x).astype(f32)
+        if noisy:  # v_rcp_f32: up to 1 ulp; model it as a random +-1 ulp error
+            r = np.where(RNG.random(r.shape) < 0.5, np.nextafter(r, f32(np.inf)), np.nextafter(r, f32(0))).astype(f32)
+        return r
+    if var.startswith("hip_b2fq"):  # back to front: T_j = T_final / prod_{k >= j} (1 - alpha_k)
+        noisy = var.endswith("rcp1")
+        Tf = fT.astype(f32)
+        bgd = (bgv[:, None] * dp).sum(0, dtype=f32)
+        Q = np.ones(npx, f32)
+        Bn = np.zeros(npx, f32)
+        dLda = np.zeros((n, npx), f32)
+        aT = np.zeros((n, npx), f32)
+        for j in range(n - 1, -1, -1):
+            a = np.where(contrib[j], al[j], f32(0))
+            Qn = (Q * (f32(1) - a)).astype(f32)
+            T = (Tf * rcp(Qn, noisy)).astype(f32)
+            cd = (col[j, 0] * dp[0] + col[j, 1] * dp[1] + col[j, 2] * dp[2]).astype(f32)
+            diff = (cd - Bn).astype(f32)
+            dLda[j] = np.where(contrib[j], T * (diff - Q * bgd), 0)
+            Bn = (Bn + a * diff).astype(f32)
+            aT[j] = a * T
+            Q = Qn
+        return records(G, dLda, aT, dx, dy, dp, contrib)
+    if var.startswith("hip_b2f"):  # back to front: T rebuilt by the reciprocal, normalised colour behind
+        noisy = var.endswith("rcp1")
         T = fT.astype(f32).copy()
         K = (fT.astype(f32) * (bgv[:, None] * dp).sum(0, dtype=f32)).astype(f32)
         Bn = np.zeros(npx, f32)
@@ -135,7 +161,7 @@ def hip_records(var, contrib, G, al, col, dp, dx, dy, fT, bgv):
         aT = np.zeros((n, npx), f32)
         for j in range(n - 1, -1, -1):
             a = np.where(contrib[j], al[j], f32(0))
-            r = (f32(1) / (f32(1) - a)).astype(f32)
+            r = np.where(a > 0, rcp(f32(1) - a, noisy), f32(1))
             T = (T * r).astype(f32)
             cd = (col[j, 0] * dp[0] + col[j, 1] * dp[1] + col[j, 2] * dp[2]).astype(f32)
             diff = (cd - Bn).astype(f32)
