@@ -518,16 +518,12 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
 // State of two pixels of the backward pass (backward.cu:498-528).  Pixels outside the image carry
 // last_contributor = 0, so no list entry contributes to them.
 //
-// Each pixel's list is replayed back to front, as the reference does.  T in front of entry j is
-// T_final / Q_j with Q_j = prod_{k >= j} (1 - alpha_k) the product of the walk so far (the
-// reference divides T by (1 - alpha) entry by entry, backward.cu:581: through v_rcp_f32's 1 ulp
-// that chain accumulates one ulp per entry, 4x the reference's error on the chair's colour
-// gradients; the product accumulates half an ulp per entry as the forward's T does, and the one
-// reciprocal per entry does not accumulate).  The colour behind entry j enters as ONE normalised
-// scalar, Bn_j = accum_rec_j . dL/dpixel (+ the inverse-depth channel), since dL/dpixel is constant
-// along the walk: Bn_{j-1} = Bn_j + alpha_j (cd_j - Bn_j), cd_j = c_j . dL/dpixel, a convex
-// recurrence (backward.cu:586-600), and, with T_final / (1 - alpha_j) = T_j Q_{j+1},
-//     dL/dalpha_j = T_j (cd_j - Bn_j - Q_{j+1} (bg . dL/dpixel))              (:601-612).
+// Each pixel's list is replayed back to front, as the reference does: T is rebuilt from final_T
+// by the reciprocal of (1 - alpha) (backward.cu:581), and the colour behind entry j enters as ONE
+// normalised scalar, Bn_j = accum_rec_j . dL/dpixel (+ the inverse-depth channel), since dL/dpixel
+// is constant along the walk: Bn_{j-1} = Bn_j + alpha_j (cd_j - Bn_j), cd_j = c_j . dL/dpixel, a
+// convex recurrence (backward.cu:586-600), and
+//     dL/dalpha_j = T_j (cd_j - Bn_j) - T_final / (1 - alpha_j) (bg . dL/dpixel)   (:601-612).
 // Rounds 1-3 walked front to back with B_j = R - sum_{k <= j} alpha_k T_k cd_k (R = the forward's
 // out_color . dL): as cheap per entry, but B is a difference of O(1) terms that ends small, so its
 // absolute rounding error (~eps |R| per entry) grew to ~5x the reference's relative error on the
@@ -535,8 +531,8 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
 // reference's order against float64; this walk: 0.4-1.2e-3).  The walk needs no accumulated
 // colour from the forward either (16 B per pixel neither written nor read).
 struct BwdPair {
-    v2f Q, Tf, Bn, bgd, dp0, dp1, dp2, dinv;  // bgd = bg . dL/dpixel
-    uint32_t lc0, lc1;                        // last_contributor
+    v2f T, Bn, K, dp0, dp1, dp2, dinv;  // K = T_final (bg . dL/dpixel)
+    uint32_t lc0, lc1;                  // last_contributor
 };
 
 // A lane's sums over its two pixel pairs for one Gaussian: the colour and invdepth terms per
@@ -566,16 +562,17 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, cons
     const v2f Gc = {c0 ? G.x : 0.f, c1 ? G.y : 0.f};
     const v2f a = Gc * co.w;  // alpha before the 0.99 clamp (0 where the pixel is not reached)
     const v2f alpha = {fminf(0.99f, a.x), fminf(0.99f, a.y)};
-    const v2f Qn = s.Q * (1.f - alpha);  // Q_j (alpha = 0 leaves it bitwise unchanged)
-    // T_j = T_final / Q_j: v_rcp_f32 (1 ulp) in place of the IEEE division
-    const v2f T = s.Tf * (v2f){__builtin_amdgcn_rcpf(Qn.x), __builtin_amdgcn_rcpf(Qn.y)};
+    const v2f one_m = 1.f - alpha;
+    // v_rcp_f32 (1 ulp) in place of the IEEE divisions of backward.cu:581,612 (exact for
+    // alpha = 0: T stays bitwise unchanged for entries that do not reach the pixel)
+    const v2f r_om = {__builtin_amdgcn_rcpf(one_m.x), __builtin_amdgcn_rcpf(one_m.y)};
+    s.T = s.T * r_om;  // T in front of this entry
     v2f cd = fma2((v2f)(col.z), s.dp2, fma2((v2f)(col.y), s.dp1, (v2f)(col.x) * s.dp0));
     if constexpr (HAS_INV) cd = fma2((v2f)(col.w), s.dinv, cd);
     const v2f diff = cd - s.Bn;  // (c - accum_rec) . dL/dpixel
-    const v2f aT = alpha * T;    // dL/dcolour / dL/dpixel (backward.cu:586-590)
-    const v2f dL = T * fma2(-s.Q, s.bgd, diff);
+    const v2f aT = alpha * s.T;  // dL/dcolour / dL/dpixel (backward.cu:586-590)
+    const v2f dL = fma2(s.T, diff, -(r_om * s.K));
     s.Bn = fma2(alpha, diff, s.Bn);  // the colour behind the entry in front
-    s.Q = Qn;
     const v2f u = Gc * dL;
     const v2f ux = u * dx;
     if constexpr (FIRST) {
@@ -692,7 +689,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     }
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
-    float bgd[4];  // bg . dL/dpixel: the background's share of dL/dalpha (backward.cu:610-612)
+    float K[4];  // T_final (bg . dL/dpixel): the background's share of dL/dalpha (backward.cu:610-612)
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         if (!inside[p]) {
@@ -700,15 +697,14 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             lc[p] = 0u;
             dp0[p] = dp1[p] = dp2[p] = dinv[p] = 0.f;
         }
-        bgd[p] = bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p];
+        K[p] = Tf[p] * (bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p]);
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         BwdPair& s = st[h];
-        s.Q = (v2f)(1.f);
-        s.Tf = {Tf[2 * h], Tf[2 * h + 1]};
+        s.T = {Tf[2 * h], Tf[2 * h + 1]};
         s.Bn = (v2f)(0.f);
-        s.bgd = {bgd[2 * h], bgd[2 * h + 1]};
+        s.K = {K[2 * h], K[2 * h + 1]};
         s.dp0 = {dp0[2 * h], dp0[2 * h + 1]};
         s.dp1 = {dp1[2 * h], dp1[2 * h + 1]};
         s.dp2 = {dp2[2 * h], dp2[2 * h + 1]};

@@ -138,15 +138,24 @@ def check_rel(name, hip, ref):
 # TRUTH_FACTOR times as far from it (99.9th percentile of the per-element relative error, over
 # the elements above REL_FLOOR of the max) as the reference's own float32 order is, plus
 # TRUTH_SLACK.  This pins the ACCURACY of the HIP formulation to the reference's, where the
-# HIP-vs-oracle comparison alone cannot tell whose rounding an element's difference is.
+# HIP-vs-oracle comparison alone cannot tell whose rounding an element's difference is.  The
+# Gaussians in the walks of flipped pixels (`affected`, flip_gaussians) are left out: there the
+# HIP path made a different float32 decision than the oracle (an alpha within an ulp of 1/255),
+# which the float64 yardstick, built on the oracle's decisions, does not share -- one term of
+# ~1/255 of a pixel's dL in a colour-gradient sum over ~100 pixels is ~1e-4 of it
+# (check_grad_attributed bounds those rows).
 TRUTH_FACTOR = 1.5
 TRUTH_SLACK = 5e-5
 
 
-def check_rel_truth(name, hip, ref, truth):
-    """Logs hip-vs-truth and oracle-vs-truth relative-error statistics; asserts the bound above."""
-    sh, so = rel_stats(hip, truth), rel_stats(ref, truth)
-    PARITY_LOG.append({"name": name + " vs float64", "hip": sh, "oracle_f32": so})
+def check_rel_truth(name, hip, ref, truth, affected=None):
+    """Logs hip-vs-truth and oracle-vs-truth relative-error statistics over the rows (Gaussians)
+    outside `affected`; asserts the bound above."""
+    hip, ref, truth = (np.asarray(x, np.float64).reshape(len(x), -1) for x in (hip, ref, truth))
+    keep = np.ones(len(truth), bool) if affected is None else ~np.asarray(affected, bool)
+    sh, so = rel_stats(hip[keep], truth[keep]), rel_stats(ref[keep], truth[keep])
+    PARITY_LOG.append({"name": name + " vs float64", "rows_left_out": int((~keep).sum()), "hip": sh,
+                       "oracle_f32": so})
     assert sh["p999"] <= TRUTH_FACTOR * so["p999"] + TRUTH_SLACK, \
         f"{name}: p99.9 error vs float64 {sh['p999']:.3e}, the reference order's {so['p999']:.3e}"
     return sh, so

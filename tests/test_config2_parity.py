@@ -49,11 +49,14 @@ def _settings(case, antialiasing):
 # whose gradients gain or lose that pixel's term: within common.GRAD_RTOL_ATTRIBUTED there, and the
 # test asserts that EVERY element beyond the tolerance belongs to such a Gaussian
 # (common.check_grad_attributed).  The bulk is bounded per element by
-# common.check_rel.
+# common.check_rel, and its accuracy against the float64 render backward (the oracle's decisions)
+# by common.check_rel_truth: no worse than 1.5x the reference's own float32 order.
 
 
-def _grad_check(name, hip, ref, affected):
+def _grad_check(name, hip, ref, affected, truth=None):
     common.check_grad_attributed(name, hip, ref, affected)
+    if truth is not None:
+        common.check_rel_truth(name, hip, ref, truth, affected)
     common.check_rel(name, hip, ref)  # per element, not only relative to the max
 
 
@@ -95,9 +98,11 @@ def test_config2_full_size(case, antialiasing):
     names = ["dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
              "dL_drotations"]
     torch.cuda.synchronize()
+    g64 = o.backward(case["grad_color"], case["grad_invdepth"], f64=True)
     for n, t in zip(names, out):
-        _grad_check(f"config2 aa={antialiasing} {n}", t.cpu().numpy(), og[n].reshape(t.shape), affected)
-    del out
+        _grad_check(f"config2 aa={antialiasing} {n}", t.cpu().numpy(), og[n].reshape(t.shape), affected,
+                    g64[n].reshape(t.shape))
+    del out, g64
 
     # the separate-DC form on the same view: dL/ddc and dL/drest against the oracle's dL/dsh split
     dc, rest = sc["shs"][:, :1].contiguous(), sc["shs"][:, 1:].contiguous()

@@ -50,7 +50,7 @@ def run(case=2, ntiles=200, seed=0):
     rng = np.random.default_rng(seed)
     nonempty = np.nonzero(ranges[:, 1] > ranges[:, 0])[0]
     tiles = rng.choice(nonempty, size=min(ntiles, nonempty.size), replace=False)
-    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1")}
+    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1", "hip_g")}
     for t in tiles:
         tx, ty = t % gx, t // gx
         xs, ys = tile_pixels(tx, ty, W, H)
@@ -108,10 +108,21 @@ def run(case=2, ntiles=200, seed=0):
         # ---- hip: forward-order B ----
         for var in ("hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1"):
             out[var].append(hip_records(var, contrib, Gr, alr, col, dp, dxf, dyf, fT[pid], bgv))
+        # the render kernels' falloff: conic pre-scaled into log2 units (preprocess.hip), p2 by two
+        # fused multiply-adds, exp2 (render.hip bwd_pair)
+        ka, kb, kc = f32(-0.5 * 1.4426950408889634) * a_, f32(-1.4426950408889634) * b_, f32(-0.5 * 1.4426950408889634) * c_
+        d64 = lambda x: x.astype(np.float64)
+        bq = (kb * dyf).astype(f32)
+        cq = ((kc * dyf).astype(f32) * dyf).astype(f32)
+        inner = (d64(ka) * d64(dxf) + d64(bq)).astype(f32)
+        p2 = (d64(inner) * d64(dxf) + d64(cq)).astype(f32)
+        Gh = np.where(contrib, np.exp2(p2).astype(f32), f32(0))
+        alh = np.where(contrib, np.minimum(f32(0.99), Gh * op), f32(0)).astype(f32)
+        out["hip_g"].append(hip_records("hip_b2fq", contrib, Gh, alh, col, dp, dxf, dyf, fT[pid], bgv))
     f64 = np.concatenate(out["f64"])
     sel = np.abs(f64) > 1e-3 * np.abs(f64).max(axis=0, keepdims=True)
     names = ["opacity", "mean_x", "mean_y", "conic_a", "conic_b", "conic_c", "col_r", "col_g", "col_b"]
-    for k in ("ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1"):
+    for k in ("ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1", "hip_g"):
         x = np.concatenate(out[k]).astype(np.float64)
         rel = np.abs(x - f64) / np.where(sel, np.abs(f64), 1)
         line = " ".join(f"{nm}={np.quantile(rel[:, i][sel[:, i]], 0.999):.1e}" for i, nm in enumerate(names))
