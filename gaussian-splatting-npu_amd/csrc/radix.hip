@@ -244,14 +244,10 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
     return pre;
 }
 
-// (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.  HI (PAIR, every
-// view's key_hi_shift > 0: the tile sort's second pass): the key rides in the payload, so no key is
-// staged in LDS or kept in registers -- 22.5 instead of 30.7 KB of LDS per workgroup and 76
-// instead of 84 VGPRs: 6 resident waves per SIMD instead of 5.
-template <int ITEMS, bool PAIR, typename KIND, int NBITS, bool HI = false>
+// (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
+template <int ITEMS, bool PAIR, typename KIND, int NBITS>
 __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
-    static_assert(!HI || PAIR, "keys in the payload need a pair payload");
     const SortPassArgs& a = B.v[blockIdx.y];
     if ((int)blockIdx.x >= a.nchunks) return;  // past this view's chunks (uniform)
     constexpr int TILE = RS_THREADS * ITEMS;
@@ -259,7 +255,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
     __shared__ uint32_t s_blk[RS_MAXBINS];     // block-local start of each digit
     __shared__ uint32_t s_base[RS_MAXBINS];    // global start of each digit for this chunk
-    __shared__ uint32_t s_keys[HI ? 1 : TILE];
+    __shared__ uint32_t s_keys[TILE];
     __shared__ Val s_vals[TILE];
     __shared__ uint32_t s_w0[4], s_w1[4];      // wave totals of the two block scans
 
@@ -279,7 +275,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     const uint64_t lt = (1ull << lane) - 1ull;
     // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
-    if (HI || (PAIR && a.key_hi_shift)) {  // the key rides in the payload's high bits
+    if (PAIR && a.key_hi_shift) {  // the key rides in the payload's high bits
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
 #pragma unroll
@@ -290,7 +286,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
     }
-    if (HI || (PAIR && a.key_hi_shift)) {
+    if (PAIR && a.key_hi_shift) {
     } else if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
@@ -342,7 +338,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
         if (rank[i] != 0xFFFFFFFFu) {
             const uint32_t d = digit_of(key[i], a.shift, mask);
             const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
-            if (!HI) s_keys[lpos] = key[i];
+            s_keys[lpos] = key[i];
             s_vals[lpos] = val[i];
         }
     }
@@ -352,12 +348,10 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     for (int i = 0; i < ITEMS; i++) {
         const int lpos = i * RS_THREADS + tid;
         if (lpos < nvalid) {
-            const Val v = s_vals[lpos];
-            uint32_t k;
-            if constexpr (HI) k = v.y >> a.key_hi_shift;
-            else k = s_keys[lpos];
+            const uint32_t k = s_keys[lpos];
             const uint32_t d = digit_of(k, a.shift, mask);
             const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
+            const Val v = s_vals[lpos];
             if (a.keys_out) {
                 a.keys_out[dst] = k;
                 reinterpret_cast<Val*>(a.vals_out)[dst] = v;
@@ -834,11 +828,6 @@ static inline uint32_t* sort_totals(const SortJob& j)
     return reinterpret_cast<uint32_t*>(j.scratch + align_up(rs_chunks(j.n) * RS_MAXBINS * 4 + 256, 256));
 }
 
-// GSR_SCATTER_HI=0: the tile sort's second pass stages its keys like every other pass (A/B switch)
-#ifndef GSR_SCATTER_HI
-#define GSR_SCATTER_HI 1
-#endif
-
 template <typename KIND>
 static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
 {
@@ -854,8 +843,6 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
         for (int v = 0; v < nv; v++)  // one payload width per launch
             if ((jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr) != pair) return hipErrorInvalidValue;
         if (maxc == 0) return hipSuccess;
-        bool hi = pair && GSR_SCATTER_HI;  // every view's key in its payload: the HI scatter
-        for (int v = 0; v < nv; v++) hi = hi && jobs[v0 + v].key_hi_shift > 0;
         const uint32_t* kin[VIEW_BATCH];
         const uint32_t* vin[VIEW_BATCH];
         for (int v = 0; v < nv; v++) {
@@ -906,20 +893,6 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 hipLaunchKernelGGL(radix_rowscan_lds_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
             else
                 hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
-            if constexpr (std::is_same<KIND, TileSort>::value) {
-                if (hi) {
-                    switch (w) {
-#define GSR_SCATTER_HI_W(W_) \
-    case W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, W_, true>), g, b, 0, s, sb); break;
-                        GSR_SCATTER_HI_W(1) GSR_SCATTER_HI_W(2) GSR_SCATTER_HI_W(3) GSR_SCATTER_HI_W(4)
-                        GSR_SCATTER_HI_W(5) GSR_SCATTER_HI_W(6) GSR_SCATTER_HI_W(7) GSR_SCATTER_HI_W(8)
-#undef GSR_SCATTER_HI_W
-                    default: return hipErrorInvalidValue;
-                    }
-                    shift += w;
-                    continue;
-                }
-            }
             switch (w * 2 + (pair ? 1 : 0)) {
 #define GSR_SCATTER_W(W_)                                                                                   \
     case 2 * W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, W_>), g, b, 0, s, sb); break; \
