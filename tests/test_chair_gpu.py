@@ -88,5 +88,13 @@ def test_chair_case(chair, case):
     for n, t in zip(make_chair.GRAD_NAMES, out):
         hip, ref = t.cpu().numpy(), og[n].reshape(t.shape)
         common.check_grad_attributed(f"{tag} {n}", hip, ref, affected)
-        common.check_rel_truth(f"{tag} {n}", hip, ref, g64[n].reshape(t.shape), affected)
+        try:
+            common.check_rel_truth(f"{tag} {n}", hip, ref, g64[n].reshape(t.shape), affected)
+        except AssertionError:  # what the diagnosis needs (tools/dbg), then the failure
+            os.makedirs(os.path.join(common.ROOT_OUT, "chair"), exist_ok=True)
+            np.savez_compressed(os.path.join(common.ROOT_OUT, "chair", f"truth_case{case}_{n}.npz"), hip=hip,
+                                oracle=ref, f64=g64[n].reshape(t.shape), affected=affected,
+                                color_hip=color.cpu().numpy(), color_oracle=o.color, nc_hip=nc,
+                                nc_oracle=o.get("n_contrib"))
+            raise
         common.check_rel(f"{tag} {n}", hip, ref)

@@ -22,6 +22,15 @@ for st in "$@"; do
   case "$st" in
     test) run pytest 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread
           cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null ;;
+    testall)  # every GPU test (no -x); plain test failures (pytest exit 1) do not end the session,
+              # anything else (a fault, an abort, a time limit) does
+          echo "=== pytest_all ($(date +%T))"
+          timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > "$OUT/pytest_all.log" 2>&1
+          rc=$?
+          echo "=== pytest_all rc=$rc"
+          grep -E "^(FAILED|ERROR)|passed|failed" "$OUT/pytest_all.log" | tail -n 12 | cut -c1-300
+          cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null
+          [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     testsel:*) run pytest_sel 600 python -u -m pytest ${st#testsel:} -m gpu -x -v --timeout 300 --timeout-method thread
           cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null ;;
     bench) run bench 600 python -u bench.py
