@@ -432,6 +432,52 @@ static void render_tile(const oracle_state* st, uint32_t tx, uint32_t ty, const 
         }
 }
 
+/* Pixels whose blend takes a decision within `rel` of its threshold (test infrastructure, not a
+ * restatement): power within rel of 0 (forward.cu:355), alpha within rel * (1/255) of 1/255
+ * (:364) or test_T within rel * 1e-4 of 1e-4 (:369), over the entries the pixel's walk
+ * evaluates.  A float32 evaluation in another order (v_exp_f32 of a log2-scaled falloff on the
+ * GPU) may take such a decision the other way without moving the pixel's colour past the
+ * parity tests' IMG_ATOL; tests/common.check_rel_truth leaves the Gaussians of these pixels' walks
+ * out with those of the flipped pixels.  out[N]: 1 = near a threshold. */
+int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out)
+{
+    const oracle_state* st = (const oracle_state*)p;
+    const int W = st->W, H = st->H;
+    memset(out, 0, (size_t)W * H);
+    const int T = (int)(st->gx * st->gy);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int t = 0; t < T; t++) {
+        const uint32_t tx = (uint32_t)t % st->gx, ty = (uint32_t)t / st->gx;
+        const uint32_t* range = st->ranges + 2 * (size_t)t;
+        for (uint32_t ly = 0; ly < BLOCK_Y; ly++)
+            for (uint32_t lx = 0; lx < BLOCK_X; lx++) {
+                uint32_t pxi = tx * BLOCK_X + lx, pyi = ty * BLOCK_Y + ly;
+                if (!(pxi < (uint32_t)W && pyi < (uint32_t)H)) continue;
+                const uint32_t pix_id = (uint32_t)W * pyi + pxi;
+                const float pfx = (float)pxi, pfy = (float)pyi;
+                float Tr = 1.0f;
+                int near = 0;
+                for (uint32_t k = range[0]; k < range[1] && !near; k++) {
+                    const uint32_t id = st->vals[k];
+                    const float dx = st->means2D[2 * id] - pfx, dy = st->means2D[2 * id + 1] - pfy;
+                    const float* co = st->conic_opacity + 4 * (size_t)id;
+                    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    if (fabsf(power) <= rel) near = 1;
+                    if (power > 0.0f) continue;
+                    const float alpha = fminf_(0.99f, co[3] * expf(power));
+                    if (fabsf(alpha - 1.0f / 255.0f) <= rel * (1.0f / 255.0f)) near = 1;
+                    if (alpha < 1.0f / 255.0f) continue;
+                    const float test_T = Tr * (1 - alpha);
+                    if (fabsf(test_T - 0.0001f) <= rel * 0.0001f) near = 1;
+                    if (test_T < 0.0001f) break;
+                    Tr = test_T;
+                }
+                out[pix_id] = (uint8_t)near;
+            }
+    }
+    return 0;
+}
+
 void gsr_oracle_free(void* p)
 {
     oracle_state* st = (oracle_state*)p;

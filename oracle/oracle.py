@@ -127,6 +127,16 @@ class OracleRaster:
             raise RuntimeError("oracle backward failed")
         return g
 
+    def near_threshold(self, rel=1e-5):
+        """bool (H, W): pixels whose walk takes a blend decision within `rel` of its threshold
+        (gsr_oracle_near_threshold) -- candidates for a decision the GPU's float32 order takes the
+        other way below the image tolerance; test infrastructure."""
+        out = np.zeros((self.H, self.W), np.uint8)
+        if out.size:
+            lib().gsr_oracle_near_threshold(ctypes.c_void_p(self.h), ctypes.c_float(rel),
+                                            out.ctypes.data_as(ctypes.c_void_p))
+        return out.astype(bool)
+
     def __del__(self):
         try:
             if getattr(self, "h", None) and _lib is not None:
