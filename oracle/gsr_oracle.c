@@ -433,7 +433,8 @@ static void render_tile(const oracle_state* st, uint32_t tx, uint32_t ty, const 
 }
 
 /* Pixels whose blend takes a decision within `rel` of its threshold (test infrastructure, not a
- * restatement): power within rel of 0 (forward.cu:355), alpha within rel * (1/255) of 1/255
+ * restatement): power within rel of its terms' magnitude of 0 (forward.cu:355), alpha within
+ * rel * (1/255) of 1/255
  * (:364) or test_T within rel * 1e-4 of 1e-4 (:369), over the entries the pixel's walk
  * evaluates.  A float32 evaluation in another order (v_exp_f32 of a log2-scaled falloff on the
  * GPU) may take such a decision the other way without moving the pixel's colour past the
@@ -462,7 +463,9 @@ int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out)
                     const float dx = st->means2D[2 * id] - pfx, dy = st->means2D[2 * id + 1] - pfy;
                     const float* co = st->conic_opacity + 4 * (size_t)id;
                     const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                    if (fabsf(power) <= rel) near = 1;
+                    /* power's sign can flip by rounding only where its terms nearly cancel */
+                    const float terms = 0.5f * (fabsf(co[0]) * dx * dx + fabsf(co[2]) * dy * dy) + fabsf(co[1] * dx * dy);
+                    if (fabsf(power) <= rel * terms) near = 1;
                     if (power > 0.0f) continue;
                     const float alpha = fminf_(0.99f, co[3] * expf(power));
                     if (fabsf(alpha - 1.0f / 255.0f) <= rel * (1.0f / 255.0f)) near = 1;
