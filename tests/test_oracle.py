@@ -109,6 +109,32 @@ def test_oracle_f64_backward_is_the_float64_gradient(antialiasing):
     np.testing.assert_array_equal(again["dL_dmean2D"], og["dL_dmean2D"])
 
 
+def test_oracle_near_threshold_flags():
+    """gsr_oracle_near_threshold (test infrastructure for the float64 accuracy check): a (H, W)
+    mask, monotone in the margin, empty at margin 0 on a case without exact ties, and every
+    flagged pixel's walk really holds an alpha within the margin of 1/255 (or a power / test_T
+    near its threshold) -- re-derived here in numpy for the alpha criterion."""
+    case = _small_case()
+    o, _ = common.run_oracle(case, backward=False)
+    H, W = case["H"], case["W"]
+    m0, m1, m2 = (o.near_threshold(r) for r in (0.0, 1e-4, 1e-2))
+    assert m1.shape == (H, W) and not m0.any()
+    assert (m1 <= m2).all() and m2.sum() > m1.sum()
+    vals, ranges, m2d, co = o.get("vals"), o.get("ranges"), o.get("means2D"), o.get("conic_opacity")
+    gx = (W + 15) // 16
+    ys, xs = np.nonzero(m2)
+    hits = 0
+    for y, x in zip(ys[:200], xs[:200]):
+        t = (y // 16) * gx + (x // 16)
+        ids = vals[ranges[t, 0]:ranges[t, 1]]
+        dx = m2d[ids, 0] - np.float32(x)
+        dy = m2d[ids, 1] - np.float32(y)
+        pw = np.float32(-0.5) * (co[ids, 0] * dx * dx + co[ids, 2] * dy * dy) - co[ids, 1] * dx * dy
+        al = np.minimum(np.float32(0.99), co[ids, 3] * np.exp(pw))
+        hits += bool((np.abs(al - 1 / 255) <= 1e-2 / 255 * 1.001).any())
+    assert hits >= 0.5 * min(200, len(ys))  # the rest: power or test_T criteria
+
+
 def _fd_case(seed=5):
     """<= 16 Gaussians in front of view 0 of the ring, overlapping on a 48x40 image: every one
     visible, alpha < 0.99 everywhere (no clamp kink), SH colours > 0 (no clamp kink)."""
