@@ -439,12 +439,14 @@ static void render_tile(const oracle_state* st, uint32_t tx, uint32_t ty, const 
  * evaluates.  A float32 evaluation in another order (v_exp_f32 of a log2-scaled falloff on the
  * GPU) may take such a decision the other way without moving the pixel's colour past the
  * parity tests' IMG_ATOL; tests/common.check_rel_truth leaves the Gaussians of these pixels' walks
- * out with those of the flipped pixels.  out[N]: 1 = near a threshold. */
-int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out)
+ * out with those of the flipped pixels.  out[N]: 1 = near a threshold; out_gauss[P] (may be NULL):
+ * 1 = the Gaussian whose decision it is (the one whose term appears or vanishes). */
+int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out, uint8_t* out_gauss)
 {
     const oracle_state* st = (const oracle_state*)p;
     const int W = st->W, H = st->H;
     memset(out, 0, (size_t)W * H);
+    if (out_gauss) memset(out_gauss, 0, (size_t)st->P);
     const int T = (int)(st->gx * st->gy);
 #pragma omp parallel for schedule(dynamic, 4)
     for (int t = 0; t < T; t++) {
@@ -466,14 +468,17 @@ int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out)
                     /* power's sign can flip by rounding only where its terms nearly cancel */
                     const float terms = 0.5f * (fabsf(co[0]) * dx * dx + fabsf(co[2]) * dy * dy) + fabsf(co[1] * dx * dy);
                     if (fabsf(power) <= rel * terms) near = 1;
-                    if (power > 0.0f) continue;
-                    const float alpha = fminf_(0.99f, co[3] * expf(power));
-                    if (fabsf(alpha - 1.0f / 255.0f) <= rel * (1.0f / 255.0f)) near = 1;
-                    if (alpha < 1.0f / 255.0f) continue;
-                    const float test_T = Tr * (1 - alpha);
-                    if (fabsf(test_T - 0.0001f) <= rel * 0.0001f) near = 1;
-                    if (test_T < 0.0001f) break;
-                    Tr = test_T;
+                    if (power <= 0.0f) {
+                        const float alpha = fminf_(0.99f, co[3] * expf(power));
+                        if (fabsf(alpha - 1.0f / 255.0f) <= rel * (1.0f / 255.0f)) near = 1;
+                        if (alpha >= 1.0f / 255.0f) {
+                            const float test_T = Tr * (1 - alpha);
+                            if (fabsf(test_T - 0.0001f) <= rel * 0.0001f) near = 1;
+                            if (test_T < 0.0001f && !near) break;
+                            Tr = test_T;
+                        }
+                    }
+                    if (near && out_gauss) out_gauss[id] = 1;  /* (benign race: every writer stores 1) */
                 }
                 out[pix_id] = (uint8_t)near;
             }

@@ -127,15 +127,17 @@ class OracleRaster:
             raise RuntimeError("oracle backward failed")
         return g
 
-    def near_threshold(self, rel=1e-5):
+    def near_threshold(self, rel=1e-5, gaussians=False):
         """bool (H, W): pixels whose walk takes a blend decision within `rel` of its threshold
         (gsr_oracle_near_threshold) -- candidates for a decision the GPU's float32 order takes the
-        other way below the image tolerance; test infrastructure."""
+        other way below the image tolerance; with gaussians=True also bool (P,): the Gaussians
+        whose decisions those are.  Test infrastructure."""
         out = np.zeros((self.H, self.W), np.uint8)
+        g = np.zeros((max(self.P, 1),), np.uint8)
         if out.size:
             lib().gsr_oracle_near_threshold(ctypes.c_void_p(self.h), ctypes.c_float(rel),
-                                            out.ctypes.data_as(ctypes.c_void_p))
-        return out.astype(bool)
+                                            out.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p))
+        return (out.astype(bool), g[:self.P].astype(bool)) if gaussians else out.astype(bool)
 
     def __del__(self):
         try:

@@ -67,6 +67,12 @@ def test_chair_case(chair, case):
     tag = f"chair case {case} (deg {deg}, aa {aa})"
     assert L == o.num_rendered, f"{tag}: num_rendered {L} vs {o.num_rendered}"
     np.testing.assert_array_equal(radii.cpu().numpy(), o.radii)
+    # the preprocess outputs the blend reads, bit for bit (visible Gaussians)
+    vis = o.radii > 0
+    lay, gb = dgr._C.geometry_layout(P), geom.cpu().numpy()
+    for i, name, w in ((0, "depths", 1), (3, "means2D", 2), (4, "conic_opacity", 4), (5, "rgb", 3)):
+        hip_a = gb[lay[i]:lay[i] + 4 * w * P].view(np.uint32).reshape(P, w) if w > 1 else gb[lay[i]:lay[i] + 4 * P].view(np.uint32)
+        np.testing.assert_array_equal(hip_a[vis], o.get(name).view(np.uint32).reshape(hip_a.shape)[vis], err_msg=f"{tag} {name}")
     keys, vals, ranges = dgr._C.sorted_keys(geom, binning, img, P, L, W, H)
     np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
     np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))

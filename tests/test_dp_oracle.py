@@ -227,7 +227,9 @@ def _worker(rank, port, raw0, targets, choices, q):
             if d is not None:
                 did[it] = d
         torch.cuda.synchronize()
-        q.put((rank, {k: p.detach().cpu() for k, p in trainer.params.items()}, did))
+        # numpy copies: a torch CPU tensor crosses the queue as a shared-memory fd that dies with this
+        # process (the parent then reads EOF)
+        q.put((rank, {k: p.detach().cpu().numpy().copy() for k, p in trainer.params.items()}, did))
     finally:
         dist.destroy_process_group()
 
@@ -268,6 +270,8 @@ def test_dp_trainer_matches_oracle_loop():
     p_reset = _psnrs(snap, ring, targets)  # after the densifications and the opacity reset
     p_cpu = _psnrs(raw_cpu, ring, targets)
     (r0, params0, did0), (r1, params1, did1) = res
+    params0 = {k: torch.from_numpy(v) for k, v in params0.items()}
+    params1 = {k: torch.from_numpy(v) for k, v in params1.items()}
     for k in params0:
         assert torch.equal(params0[k], params1[k]), f"ranks differ in {k}"
     p_gpu = _psnrs(params0, ring, targets)
