@@ -27,18 +27,28 @@ GRAD_ATOL = 1e-6
 # 2.05e-3 (a flip at T ~ 1, final_T off by 1/255); every other case none.
 FLIP_FRACTION = 1e-4
 FLIP_MAX_ABS = 5e-3
+# A decision taken the other way can also move a pixel by less than IMG_ATOL: an alpha at 1/255
+# blended at T ~ 1e-3 changes the colour by ~4e-6.  Such a pixel is not "flipped" (the image is
+# within tolerance) but the Gaussians of its walk gain or lose one pixel's term, ~1e-4 of their
+# gradient (chair fixture, case 1, pixel (600, 29): 7.5e-6, every walk Gaussian's record for that
+# tile off by ~1e-4 -- tools/dbg/chair_records_cmp.py).  Pixels off by more than DECISION_ATOL
+# (the remaining differences are the rounding of the colour sums: ~1e-7, a handful of pixels per
+# million up to ~1e-6) are "decision suspects": the per-element relative checks (check_rel,
+# check_rel_truth) leave their walks' Gaussians out, which check_grad_attributed bounds instead.
+DECISION_ATOL = 1e-6
 # every check_render call appends its statistics here; conftest writes them to
 # gpurun_out/parity_stats.json at the end of a session that has any
 PARITY_LOG = []
 
 
-def check_render(name, hip, ora, flips=None):
+def check_render(name, hip, ora, flips=None, suspects=None):
     """hip / ora: dicts with 'color' (3,H,W), 'invdepth' (1,H,W) and optionally 'final_T' (N)
     and 'n_contrib' (N).  Flipped pixels: n_contrib differs (when both have it) or some
     colour / invdepth / final_T value is off by more than IMG_ATOL.  Asserts: flipped fraction
     <= FLIP_FRACTION, every value of a flipped pixel within FLIP_MAX_ABS (final_T within
     1/255 + IMG_ATOL), all others within IMG_ATOL with the same n_contrib.  `flips`: a list that
-    receives the flipped pixels' mask (bool (N,)), for flip_gaussians."""
+    receives the flipped pixels' mask (bool (N,)), for flip_gaussians; `suspects` the mask of the
+    flipped pixels and those off by more than DECISION_ATOL."""
     c = np.abs(np.asarray(hip["color"], np.float64) - np.asarray(ora["color"], np.float64))
     N = c.shape[-1] * c.shape[-2]
     err = c.reshape(c.shape[0], N).max(0)
@@ -59,10 +69,16 @@ def check_render(name, hip, ora, flips=None):
     n_flip = int(flip.sum())
     if flips is not None:
         flips.append(flip)
+    suspect = flip | (err > DECISION_ATOL)
+    if terr is not None:
+        suspect |= terr > DECISION_ATOL
+    if suspects is not None:
+        suspects.append(suspect)
     stats = {"name": name, "pixels": N, "flipped": n_flip, "frac": n_flip / max(N, 1), "n_contrib_diff": nc_diff,
              "max_err_flipped": float(err[flip].max()) if n_flip else 0.0,
              "max_err_other": float(err[~flip].max()) if n_flip < N else 0.0,
-             "max_T_err_flipped": float(terr[flip].max()) if (n_flip and terr is not None) else 0.0}
+             "max_T_err_flipped": float(terr[flip].max()) if (n_flip and terr is not None) else 0.0,
+             "decision_suspects": int(suspect.sum())}
     PARITY_LOG.append(stats)
     assert stats["frac"] <= FLIP_FRACTION, f"{name}: {n_flip} of {N} pixels flipped ({stats})"
     assert stats["max_err_flipped"] <= FLIP_MAX_ABS, f"{name}: flipped pixel off by {stats['max_err_flipped']:.3e}"
@@ -124,10 +140,16 @@ def rel_stats(hip, ref, floor=REL_FLOOR):
             "max": float(r.max()), "n_over_1e-3": int((r > 1e-3).sum()), "n_over_REL_OUT": int((r > REL_OUT).sum())}
 
 
-def check_rel(name, hip, ref):
-    """Asserts the per-element relative-error bounds above; returns (and logs) the statistics."""
+def check_rel(name, hip, ref, affected=None):
+    """Asserts the per-element relative-error bounds above over the rows (Gaussians) outside
+    `affected` (the walks of decision-suspect pixels: their rows are bounded by
+    check_grad_attributed); returns (and logs) the statistics."""
+    if affected is not None:
+        keep = ~np.asarray(affected, bool)
+        hip = np.asarray(hip).reshape(len(keep), -1)[keep]
+        ref = np.asarray(ref).reshape(len(keep), -1)[keep]
     st = rel_stats(hip, ref)
-    PARITY_LOG.append({"name": name + " rel", **st})
+    PARITY_LOG.append({"name": name + " rel", "rows_left_out": 0 if affected is None else int((~keep).sum()), **st})
     assert st["p999"] <= REL_P999, f"{name}: 99.9th percentile relative error {st['p999']:.3e} ({st})"
     assert st["n_over_REL_OUT"] <= max(2, REL_OUT_FRAC * st["considered"]), f"{name}: {st}"
     return st
@@ -139,11 +161,10 @@ def check_rel(name, hip, ref):
 # the elements above REL_FLOOR of the max) as the reference's own float32 order is, plus
 # TRUTH_SLACK.  This pins the ACCURACY of the HIP formulation to the reference's, where the
 # HIP-vs-oracle comparison alone cannot tell whose rounding an element's difference is.  The
-# Gaussians in the walks of flipped pixels (`affected`, flip_gaussians) are left out: there the
-# HIP path made a different float32 decision than the oracle (an alpha within an ulp of 1/255),
-# which the float64 yardstick, built on the oracle's decisions, does not share -- one term of
-# ~1/255 of a pixel's dL in a colour-gradient sum over ~100 pixels is ~1e-4 of it
-# (check_grad_attributed bounds those rows).
+# Gaussians in the walks of decision-suspect pixels (`affected`: flip_gaussians of check_render's
+# `suspects`) are left out: there the HIP path may have taken a float32 blend decision the other
+# way (an alpha within an ulp of 1/255), which the float64 yardstick, built on the oracle's
+# decisions, does not share (check_grad_attributed bounds those rows).
 TRUTH_FACTOR = 1.5
 TRUTH_SLACK = 5e-5
 

@@ -38,9 +38,9 @@ def scene():
     return synthetic.make_scene(P, seed=0)
 
 
-def _grad_check(name, hip, ref, affected):
+def _grad_check(name, hip, ref, affected, suspect_rows):
     common.check_grad_attributed(name, hip, ref, affected)
-    common.check_rel(name, hip, ref)
+    common.check_rel(name, hip, ref, suspect_rows)
 
 
 @pytest.mark.parametrize("antialiasing", [False, True])
@@ -71,7 +71,8 @@ def test_bench_step_8_views(scene, antialiasing):
     torch.cuda.synchronize()
 
     from test_gpu_parity import _img_state
-    ref_sum, affected = None, None  # affected: Gaussians in some view's flipped-pixel walk
+    # affected: Gaussians in some view's flipped-pixel walk; suspect_rows: in a decision suspect's
+    ref_sum, affected, suspect_rows = None, None, None
     for v in range(V):
         o = oracle.OracleRaster(scene["means3D"], scene["opacities"], bg, cams[v].world_view_transform,
                                 cams[v].full_proj_transform, cams[v].camera_center, cams[v].tanfovx,
@@ -87,18 +88,21 @@ def test_bench_step_8_views(scene, antialiasing):
                                       err_msg=f"{tag}: ranges")
         del keys, vals, ranges
         fT, nc = _img_state(imgs[v], W, H)
-        flips = []
+        flips, sus = [], []
         common.check_render(tag, {"color": color[v].detach().cpu().numpy(), "invdepth": inv[v].detach().cpu().numpy(),
                                   "final_T": fT, "n_contrib": nc},
                             {"color": o.color, "invdepth": o.invdepth, "final_T": o.get("final_T"),
-                             "n_contrib": o.get("n_contrib")}, flips=flips)
+                             "n_contrib": o.get("n_contrib")}, flips=flips, suspects=sus)
         aff = common.flip_gaussians(flips[0], nc, o.get("n_contrib"), o.get("vals"), o.get("ranges"), W, H, P)
+        saff = common.flip_gaussians(sus[0], nc, o.get("n_contrib"), o.get("vals"), o.get("ranges"), W, H, P)
         affected = aff if affected is None else affected | aff
+        suspect_rows = saff if suspect_rows is None else suspect_rows | saff
         og = o.backward(grads[v][0], grads[v][1])
         del o
-        _grad_check(f"{tag} dL_dmean2D", means2D.grad[v].cpu().numpy(), og["dL_dmean2D"], aff)
+        _grad_check(f"{tag} dL_dmean2D", means2D.grad[v].cpu().numpy(), og["dL_dmean2D"], aff, saff)
         og = {k: og[k].astype(np.float64) for k in PARAM_KEYS.values()}
         ref_sum = og if ref_sum is None else {k: ref_sum[k] + og[k] for k in ref_sum}
     for k, ok_ in PARAM_KEYS.items():
         a = params[k].grad.cpu().numpy()
-        _grad_check(f"bench step aa={antialiasing} sum of 8 views {ok_}", a, ref_sum[ok_].reshape(a.shape), affected)
+        _grad_check(f"bench step aa={antialiasing} sum of 8 views {ok_}", a, ref_sum[ok_].reshape(a.shape), affected,
+                    suspect_rows)

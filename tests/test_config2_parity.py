@@ -53,11 +53,12 @@ def _settings(case, antialiasing):
 # by common.check_rel_truth: no worse than 1.5x the reference's own float32 order.
 
 
-def _grad_check(name, hip, ref, affected, truth=None):
+def _grad_check(name, hip, ref, affected, suspect_rows, truth=None):
     common.check_grad_attributed(name, hip, ref, affected)
     if truth is not None:
-        common.check_rel_truth(name, hip, ref, truth, affected)
-    common.check_rel(name, hip, ref)  # per element, not only relative to the max
+        common.check_rel_truth(name, hip, ref, truth, suspect_rows)
+    # per element, not only relative to the max
+    common.check_rel(name, hip, ref, suspect_rows)
 
 
 @pytest.mark.parametrize("antialiasing", [False, True])
@@ -83,12 +84,13 @@ def test_config2_full_size(case, antialiasing):
     np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
     del keys, vals
     fT, nc = _img_state(img, W, H)
-    flips = []
+    flips, sus = [], []
     common.check_render(f"config2 aa={antialiasing}",
                         {"color": color.cpu().numpy(), "invdepth": inv.cpu().numpy(), "final_T": fT, "n_contrib": nc},
                         {"color": o.color, "invdepth": o.invdepth, "final_T": o.get("final_T"),
-                         "n_contrib": o.get("n_contrib")}, flips=flips)
+                         "n_contrib": o.get("n_contrib")}, flips=flips, suspects=sus)
     affected = common.flip_gaussians(flips[0], nc, o.get("n_contrib"), o.get("vals"), o.get("ranges"), W, H, P)
+    suspect_rows = common.flip_gaussians(sus[0], nc, o.get("n_contrib"), o.get("vals"), o.get("ranges"), W, H, P)
 
     gc, gi = case["grad_color"].to(DEV), case["grad_invdepth"].to(DEV)
     out = dgr._C.rasterize_gaussians_backward(
@@ -101,7 +103,7 @@ def test_config2_full_size(case, antialiasing):
     g64 = o.backward(case["grad_color"], case["grad_invdepth"], f64=True)
     for n, t in zip(names, out):
         _grad_check(f"config2 aa={antialiasing} {n}", t.cpu().numpy(), og[n].reshape(t.shape), affected,
-                    g64[n].reshape(t.shape))
+                    suspect_rows, g64[n].reshape(t.shape))
     del out, g64
 
     # the separate-DC form on the same view: dL/ddc and dL/drest against the oracle's dL/dsh split
@@ -116,9 +118,10 @@ def test_config2_full_size(case, antialiasing):
         False, dc=dc)
     torch.cuda.synchronize()
     sh_ref = og["dL_dsh"].reshape(P, 16, 3)
-    _grad_check(f"config2 aa={antialiasing} dc dL_ddc", out[5].cpu().numpy(), sh_ref[:, :1], affected)
-    _grad_check(f"config2 aa={antialiasing} dc dL_drest", out[6].cpu().numpy(), sh_ref[:, 1:], affected)
-    _grad_check(f"config2 aa={antialiasing} dc dL_dmeans3D", out[3].cpu().numpy(), og["dL_dmeans3D"], affected)
+    _grad_check(f"config2 aa={antialiasing} dc dL_ddc", out[5].cpu().numpy(), sh_ref[:, :1], affected, suspect_rows)
+    _grad_check(f"config2 aa={antialiasing} dc dL_drest", out[6].cpu().numpy(), sh_ref[:, 1:], affected, suspect_rows)
+    _grad_check(f"config2 aa={antialiasing} dc dL_dmeans3D", out[3].cpu().numpy(), og["dL_dmeans3D"], affected,
+                suspect_rows)
 
 
 def test_config2_batched_views_match_single_views(case):
