@@ -140,17 +140,23 @@ def rel_stats(hip, ref, floor=REL_FLOOR):
             "max": float(r.max()), "n_over_1e-3": int((r > 1e-3).sum()), "n_over_REL_OUT": int((r > REL_OUT).sum())}
 
 
-def check_rel(name, hip, ref, affected=None):
+def check_rel(name, hip, ref, affected=None, truth_stats=None):
     """Asserts the per-element relative-error bounds above over the rows (Gaussians) outside
     `affected` (the walks of decision-suspect pixels: their rows are bounded by
-    check_grad_attributed); returns (and logs) the statistics."""
+    check_grad_attributed); returns (and logs) the statistics.  truth_stats: the oracle's own
+    statistics against the float64 yardstick (check_rel_truth) -- the HIP-vs-oracle difference is
+    at most the sum of the two errors, so the bound on it becomes max(REL_P999, (1 + TRUTH_FACTOR)
+    x the oracle's p99.9 + TRUTH_SLACK): where the reference's float32 order is itself 9e-4 from
+    float64 (the chair on white), a 1e-3 bound between two float32 results tests the oracle."""
     if affected is not None:
         keep = ~np.asarray(affected, bool)
         hip = np.asarray(hip).reshape(len(keep), -1)[keep]
         ref = np.asarray(ref).reshape(len(keep), -1)[keep]
     st = rel_stats(hip, ref)
-    PARITY_LOG.append({"name": name + " rel", "rows_left_out": 0 if affected is None else int((~keep).sum()), **st})
-    assert st["p999"] <= REL_P999, f"{name}: 99.9th percentile relative error {st['p999']:.3e} ({st})"
+    bound = REL_P999 if truth_stats is None else max(REL_P999, (1 + TRUTH_FACTOR) * truth_stats["p999"] + TRUTH_SLACK)
+    PARITY_LOG.append({"name": name + " rel", "rows_left_out": 0 if affected is None else int((~keep).sum()),
+                       "p999_bound": bound, **st})
+    assert st["p999"] <= bound, f"{name}: 99.9th percentile relative error {st['p999']:.3e} > {bound:.3e} ({st})"
     assert st["n_over_REL_OUT"] <= max(2, REL_OUT_FRAC * st["considered"]), f"{name}: {st}"
     return st
 

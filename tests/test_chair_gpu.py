@@ -96,7 +96,7 @@ def test_chair_case(chair, case):
         hip, ref = t.cpu().numpy(), og[n].reshape(t.shape)
         common.check_grad_attributed(f"{tag} {n}", hip, ref, affected)
         try:
-            common.check_rel_truth(f"{tag} {n}", hip, ref, g64[n].reshape(t.shape), suspect_rows)
+            _, so = common.check_rel_truth(f"{tag} {n}", hip, ref, g64[n].reshape(t.shape), suspect_rows)
         except AssertionError:  # what the diagnosis needs (tools/dbg), then the failure
             os.makedirs(os.path.join(common.ROOT_OUT, "chair"), exist_ok=True)
             np.savez_compressed(os.path.join(common.ROOT_OUT, "chair", f"truth_case{case}_{n}.npz"), hip=hip,
@@ -104,4 +104,4 @@ def test_chair_case(chair, case):
                                 color_hip=color.cpu().numpy(), color_oracle=o.color, nc_hip=nc,
                                 nc_oracle=o.get("n_contrib"))
             raise
-        common.check_rel(f"{tag} {n}", hip, ref, suspect_rows)
+        common.check_rel(f"{tag} {n}", hip, ref, suspect_rows, so)
