@@ -729,12 +729,7 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     const bool vis = has_view && vi.n > 0;
     float gs[GF_NUM];
     if (vis) {
-#if GSR_PBWD_NOGATHER  // timing experiment only (wrong gradients): no valid-word / record loads
-#pragma unroll
-        for (int q = 0; q < GF_NUM; q++) gs[q] = 1e-3f * (float)(vi.e0 & 7u) + 1e-4f * q;
-#else
         gather_any<VIEW_REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
-#endif
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;

@@ -639,14 +639,8 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
 // 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
 constexpr int BWD_TPW = 4;
-// GSR_BWD_STRAIGHT=1 (one basic block for a reduction group's three entries) measured 2 % slower
-// (render_bwd 1,957-1,970 vs 1,916-1,924 us per 8-view launch, same box, 3 rounds)
-#ifndef GSR_BWD_STRAIGHT
-#define GSR_BWD_STRAIGHT 0
-#endif
-#ifndef GSR_BWD_PREFETCH
-#define GSR_BWD_PREFETCH 0
-#endif
+// (Measured and dropped, DESIGN §10: a reduction group's three entries as ONE basic block, 2 %
+// slower; entry jj + 1's staged record read from LDS while entry jj computes, 2 % slower.)
 
 template <bool HAS_INV>
 __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_eu(4))) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
@@ -793,35 +787,12 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                 ej[jj] = act[jj] ? (int)s_lq[grp][mycnt - 1 - (i0 + jj)] : fv;
             }
             float v[32];
-            // GSR_BWD_PREFETCH: entry jj + 1's staged record is read from LDS while entry jj computes
-            float4 nxy, nco, ncol;
-            if (GSR_BWD_PREFETCH) {
-                nxy = s_rec[0][ej[0]];
-                nco = s_rec[1][ej[0]];
-                ncol = s_rec[2][ej[0]];
-            }
 #pragma unroll
             for (int jj = 0; jj < G; jj++) {
-                // GSR_BWD_STRAIGHT: the G entries as ONE basic block (an entry past niter evaluates
-                // the staged record at position "never": zero terms), so the scheduler overlaps the
-                // independent falloff / exp / alpha work of the later entries with the T / B chain of
-                // the earlier ones; otherwise a wave-uniform branch per entry (a block per entry)
-                if (GSR_BWD_STRAIGHT || i0 + jj < niter) {
-                    float4 xy, co, col;
-                    if (GSR_BWD_PREFETCH) {
-                        xy = nxy;
-                        co = nco;
-                        col = ncol;
-                        if (jj + 1 < G) {
-                            nxy = s_rec[0][ej[jj + 1]];
-                            nco = s_rec[1][ej[jj + 1]];
-                            ncol = s_rec[2][ej[jj + 1]];
-                        }
-                    } else {
-                        xy = s_rec[0][ej[jj]];
-                        co = s_rec[1][ej[jj]];
-                        col = s_rec[2][ej[jj]];
-                    }
+                // a wave-uniform branch per entry (a block per entry): the iterations past niter
+                // evaluate nothing
+                if (i0 + jj < niter) {
+                    const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
                     const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
                     const Falloff f = falloff(co);
                     // the falloff's dy terms, shared by the lane's two pairs (one row)
