@@ -524,6 +524,10 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
 // is constant along the walk: Bn_{j-1} = Bn_j + alpha_j (cd_j - Bn_j), cd_j = c_j . dL/dpixel, a
 // convex recurrence (backward.cu:586-600), and
 //     dL/dalpha_j = T_j (cd_j - Bn_j) - T_final / (1 - alpha_j) (bg . dL/dpixel)   (:601-612).
+// The background term folds into Bn: with Bn' = Bn + T_final (bg . dL) / T_{j+1} (the background
+// as the colour behind the last entry, normalised the same way), Bn' obeys the same recurrence
+// from Bn' = bg . dL/dpixel behind the last entry, and dL/dalpha_j = T_j (cd_j - Bn'_j) --
+// since T_j / T_{j+1} = 1 / (1 - alpha_j) -- one multiply and one register less per pixel.
 // Rounds 1-3 walked front to back with B_j = R - sum_{k <= j} alpha_k T_k cd_k (R = the forward's
 // out_color . dL): as cheap per entry, but B is a difference of O(1) terms that ends small, so its
 // absolute rounding error (~eps |R| per entry) grew to ~5x the reference's relative error on the
@@ -531,8 +535,8 @@ __device__ __forceinline__ void group_transpose_reduce32(float (&v)[32], int lan
 // reference's order against float64; this walk: 0.4-1.2e-3).  The walk needs no accumulated
 // colour from the forward either (16 B per pixel neither written nor read).
 struct BwdPair {
-    v2f T, Bn, K, dp0, dp1, dp2, dinv;  // K = T_final (bg . dL/dpixel)
-    uint32_t lc0, lc1;                  // last_contributor
+    v2f T, Bn, dp0, dp1, dp2, dinv;  // Bn: the colour behind, the background's included
+    uint32_t lc0, lc1;               // last_contributor
 };
 
 // A lane's sums over its two pixel pairs for one Gaussian: the colour and invdepth terms per
@@ -571,7 +575,7 @@ __device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, cons
     if constexpr (HAS_INV) cd = fma2((v2f)(col.w), s.dinv, cd);
     const v2f diff = cd - s.Bn;  // (c - accum_rec) . dL/dpixel
     const v2f aT = alpha * s.T;  // dL/dcolour / dL/dpixel (backward.cu:586-590)
-    const v2f dL = fma2(s.T, diff, -(r_om * s.K));
+    const v2f dL = s.T * diff;
     s.Bn = fma2(alpha, diff, s.Bn);  // the colour behind the entry in front
     const v2f u = Gc * dL;
     const v2f ux = u * dx;
@@ -683,7 +687,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     }
     const float bg0 = a.bg[0], bg1 = a.bg[1], bg2 = a.bg[2];
     BwdPair st[2];
-    float K[4];  // T_final (bg . dL/dpixel): the background's share of dL/dalpha (backward.cu:610-612)
+    float bgd[4];  // bg . dL/dpixel: the colour behind the last entry (the background, backward.cu:610-612)
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         if (!inside[p]) {
@@ -691,14 +695,13 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             lc[p] = 0u;
             dp0[p] = dp1[p] = dp2[p] = dinv[p] = 0.f;
         }
-        K[p] = Tf[p] * (bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p]);
+        bgd[p] = bg0 * dp0[p] + bg1 * dp1[p] + bg2 * dp2[p];
     }
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         BwdPair& s = st[h];
         s.T = {Tf[2 * h], Tf[2 * h + 1]};
-        s.Bn = (v2f)(0.f);
-        s.K = {K[2 * h], K[2 * h + 1]};
+        s.Bn = {bgd[2 * h], bgd[2 * h + 1]};
         s.dp0 = {dp0[2 * h], dp0[2 * h + 1]};
         s.dp1 = {dp1[2 * h], dp1[2 * h + 1]};
         s.dp2 = {dp2[2 * h], dp2[2 * h + 1]};

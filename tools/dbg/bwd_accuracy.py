@@ -50,7 +50,7 @@ def run(case=2, ntiles=200, seed=0):
     rng = np.random.default_rng(seed)
     nonempty = np.nonzero(ranges[:, 1] > ranges[:, 0])[0]
     tiles = rng.choice(nonempty, size=min(ntiles, nonempty.size), replace=False)
-    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1", "hip_g")}
+    out = {k: [] for k in ("f64", "ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1", "hip_g", "hip_fold")}
     for t in tiles:
         tx, ty = t % gx, t // gx
         xs, ys = tile_pixels(tx, ty, W, H)
@@ -106,7 +106,7 @@ def run(case=2, ntiles=200, seed=0):
             aT_r[j] = np.where(c, alr[j] * Tr, 0)
         out["ref"].append(records(Gr, dLda_r, aT_r, dxf, dyf, dp, contrib))
         # ---- hip: forward-order B ----
-        for var in ("hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1"):
+        for var in ("hip_b2f_rcp1", "hip_fold"):
             out[var].append(hip_records(var, contrib, Gr, alr, col, dp, dxf, dyf, fT[pid], bgv))
         # the render kernels' falloff: conic pre-scaled into log2 units (preprocess.hip), p2 by two
         # fused multiply-adds, exp2 (render.hip bwd_pair)
@@ -118,11 +118,12 @@ def run(case=2, ntiles=200, seed=0):
         p2 = (d64(inner) * d64(dxf) + d64(cq)).astype(f32)
         Gh = np.where(contrib, np.exp2(p2).astype(f32), f32(0))
         alh = np.where(contrib, np.minimum(f32(0.99), Gh * op), f32(0)).astype(f32)
+        out["hip_g"] = out.get("hip_g", [])
         out["hip_g"].append(hip_records("hip_b2fq", contrib, Gh, alh, col, dp, dxf, dyf, fT[pid], bgv))
     f64 = np.concatenate(out["f64"])
     sel = np.abs(f64) > 1e-3 * np.abs(f64).max(axis=0, keepdims=True)
     names = ["opacity", "mean_x", "mean_y", "conic_a", "conic_b", "conic_c", "col_r", "col_g", "col_b"]
-    for k in ("ref", "hip", "hip_split", "hip_chan", "hip_b2f", "hip_b2f_rcp1", "hip_b2fq", "hip_b2fq_rcp1", "hip_g"):
+    for k in ("ref", "hip_b2f_rcp1", "hip_fold"):
         x = np.concatenate(out[k]).astype(np.float64)
         rel = np.abs(x - f64) / np.where(sel, np.abs(f64), 1)
         line = " ".join(f"{nm}={np.quantile(rel[:, i][sel[:, i]], 0.999):.1e}" for i, nm in enumerate(names))
@@ -162,6 +163,21 @@ def hip_records(var, contrib, G, al, col, dp, dx, dy, fT, bgv):
             Bn = (Bn + a * diff).astype(f32)
             aT[j] = a * T
             Q = Qn
+        return records(G, dLda, aT, dx, dy, dp, contrib)
+    if var == "hip_fold":  # back to front, the background folded into the colour behind (render.hip)
+        T = fT.astype(f32).copy()
+        Bn = (bgv[:, None] * dp).sum(0, dtype=f32).astype(f32)
+        dLda = np.zeros((n, npx), f32)
+        aT = np.zeros((n, npx), f32)
+        for j in range(n - 1, -1, -1):
+            a = np.where(contrib[j], al[j], f32(0))
+            r = np.where(a > 0, rcp(f32(1) - a, True), f32(1))
+            T = (T * r).astype(f32)
+            cd = (col[j, 0] * dp[0] + col[j, 1] * dp[1] + col[j, 2] * dp[2]).astype(f32)
+            diff = (cd - Bn).astype(f32)
+            dLda[j] = np.where(contrib[j], T * diff, 0)
+            Bn = (Bn + a * diff).astype(f32)
+            aT[j] = a * T
         return records(G, dLda, aT, dx, dy, dp, contrib)
     if var.startswith("hip_b2f"):  # back to front: T rebuilt by the reciprocal, normalised colour behind
         noisy = var.endswith("rcp1")
