@@ -255,10 +255,13 @@ def test_8k_view_three_pass_tile_sort():
 def test_packed_rect_boundary_keys_bit_exact(H, W):
     """The depth sort carries the tile rect packed into one word (a byte per bound) on grids of at
     most 255 x 255 tiles and gathers the u16x4 rect by id above that: 255 and 256 tiles along
-    either axis (rect bounds up to 255 / 256) give keys, ids and ranges bit-identical to the oracle."""
+    either axis (rect bounds up to 255 / 256) give keys, ids and ranges bit-identical to the oracle.
+    The backward too: render_bwd locates a record's mask bit from the packed rect in the render
+    record up to 255 tiles and from the Gaussian's first record slot above -- every gradient
+    against the oracle on both sides of the boundary."""
     dgr = _dgr()
     case = common.make_case(P=3000, H=H, W=W)
-    o, _ = common.run_oracle(case, nthreads=8, backward=False)
+    o, og = common.run_oracle(case, nthreads=8, backward=True)
     s = _settings(case)
     sc = {k: v.to(DEV) for k, v in case["scene"].items()}
     L, color, radii, geom, binning, img, inv = dgr._C.rasterize_gaussians(
@@ -273,6 +276,22 @@ def test_packed_rect_boundary_keys_bit_exact(H, W):
     np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
     np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
     np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+    del keys, vals, ranges
+    fT, nc = _img_state(img, W, H)
+    flips = []
+    common.check_render(f"rect boundary {W}x{H}", {"color": color.cpu().numpy(), "invdepth": inv.cpu().numpy(),
+                                                  "final_T": fT, "n_contrib": nc}, _ora_render(o), flips=flips)
+    affected = common.flip_gaussians(flips[0], nc, o.get("n_contrib"), o.get("vals"), o.get("ranges"), W, H, P)
+    gc, gi = case["grad_color"].to(DEV), case["grad_invdepth"].to(DEV)
+    out = dgr._C.rasterize_gaussians_backward(
+        s.bg, sc["means3D"], radii, torch.Tensor([]), sc["opacities"], sc["scales"], sc["rotations"], 1.0,
+        torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, gc, gi, sc["shs"], s.sh_degree, s.campos,
+        geom, L, binning, img, False, False)
+    torch.cuda.synchronize()
+    names = ["dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for n, t in zip(names, out):
+        common.check_grad_attributed(f"rect boundary {W}x{H} {n}", t.cpu().numpy(), og[n].reshape(t.shape), affected)
 
 
 def test_mark_visible():
