@@ -166,7 +166,7 @@ enum GeomArray {
     GEOM_RGB,             // f32[3P]
     GEOM_TILES_TOUCHED,   // u32[P]
     GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched in depth order
-    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, rect} {ka, kb, kc, opacity} {r, g, b, 1/depth}
+    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {ka, kb, kc, opacity} {r, g, b, 1/depth}
                           // (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic; cullK scaled by log2(e)/2
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order

@@ -216,10 +216,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     constexpr float LOG2E = 1.4426950408889634f;
     if (cullK >= 0.f && cullK < 1.0e37f) cullK = cullK * (0.5f * LOG2E);
     float4* sp = a.splat + 3 * (size_t)idx;
-    // the free word: the packed tile rect (render_bwd locates a record's mask bit from it), or
-    // all ones on grids too large to pack
-    const uint32_t rpk = a.rect4 ? rect_pack(rminx, rminy, rmaxx, rmaxy) : 0xFFFFFFFFu;
-    sp[0] = make_float4(pix_x, pix_y, cullK, __uint_as_float(rpk));
+    sp[0] = make_float4(pix_x, pix_y, cullK, 0.0f);
     sp[1] = make_float4((-0.5f * LOG2E) * conic_x, (-LOG2E) * conic_y, (-0.5f * LOG2E) * conic_z, opacity);
     sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
 }

@@ -749,22 +749,11 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         // only entries that contributed somewhere in the forward are read (43 % of the entries
         // below tmax contributed nowhere: their 48-B record gathers are skipped)
-        // the record's index among its Gaussian's slots (its record-mask bit at the store): from
-        // the Gaussian's packed tile rect in the record's free word (slots enumerate the rect
-        // row-major, fe_tile) -- or, on grids too large to pack, from its first slot
-        uint32_t loc = 0;
+        uint32_t es = 0;  // the Gaussian's first record slot (its record mask bit at the store)
         if (m != 0) {
             const float4* r = a.splat + 3 * (size_t)id;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            if (GSR_REC_MASK) {
-                const uint32_t rpk = __float_as_uint(r0.w);
-                if (rpk != 0xFFFFFFFFu) {
-                    const uint32_t x0 = rpk & 0xFFu, y0 = (rpk >> 8) & 0xFFu, x1 = (rpk >> 16) & 0xFFu;
-                    loc = (ty - y0) * max(x1 - x0, 1u) + (tx - x0);
-                } else {
-                    loc = myslot - a.emit_start[id];
-                }
-            }
+            if (GSR_REC_MASK) es = a.emit_start[id];
             s_rec[0][lane] = r0;
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;
@@ -868,7 +857,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
             // then finds the records without a dependent load of the valid words), else in the valid
             // words: one atomic per record either way
-            if (GSR_REC_MASK && loc < 32u) atomicOr(&a.rec_mask[id], 1u << loc);
+            const uint32_t local = myslot - es;
+            if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
             else atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
