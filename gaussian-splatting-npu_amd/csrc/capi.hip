@@ -393,9 +393,24 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
     return GSR_OK;
 }
 
+// The forward tile order of a view whose tile ranges come from the rects' difference array
+// (tile_hist): it needs nothing from the tile sort, so it runs on the auxiliary stream right after
+// tile_hist, beside the depth and tile sorts, instead of between the tile sort and render_fwd.
+static OrderJob diff_order_job(char* ib, int width, int height, uint32_t gx, uint32_t gy)
+{
+    const ImageLayout im = image_layout(width, height);
+    OrderJob oj = {};
+    oj.order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    oj.diff = at<int>(ib, im.off[IMG_TILE_DIFF]);
+    oj.ranges_out = at<uint2>(ib, im.off[IMG_RANGES]);
+    oj.grid_x = gx;
+    oj.grid_y = gy;
+    return oj;
+}
+
 // After preprocess: the record-slot scan, the depth sort and the tile-count scan of one view.
-static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint32_t* h_dev, hipStream_t s,
-                                 bool debug, bool use_aux = true)
+static int forward_geometry_sort(const PreprocessArgs& a, char* gb, char* ib, int width, int height, int P,
+                                 uint32_t* h_dev, hipStream_t s, bool debug, bool use_aux = true)
 {
     const GeomLayout g = geom_layout(P);
     // 1b. each Gaussian's first gradient-record slot: index-order exclusive scan of the tile counts
@@ -416,6 +431,11 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, int P, uint3
         ProfScope ps_(PK_RANGES, aux);
         const TileHistJob hj = {a.rect4, P, a.tile_diff};
         e = launch_tile_hist_batch(&hj, 1, a.grid_x, a.grid_y, aux);
+    }
+    if (e == hipSuccess && a.tile_diff) {  // ... and from it the tile ranges and the forward's tile order
+        ProfScope ps_(PK_TILE_ORDER, aux);
+        const OrderJob oj = diff_order_job(ib, width, height, a.grid_x, a.grid_y);
+        e = launch_tile_order_batch(&oj, 1, (int)(a.grid_x * a.grid_y), aux);
     }
 
     // 2. stable depth sort of the Gaussians (first half of the reference's tile|depth key sort)
@@ -478,7 +498,7 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
         HIP_TRY(launch_preprocess(a, s));
     }
     DEBUG_SYNC(s);
-    return forward_geometry_sort(a, geometry_buffer, P, h_dev, s, debug, use_aux);
+    return forward_geometry_sort(a, geometry_buffer, image_buffer, width, height, P, h_dev, s, debug, use_aux);
 }
 
 static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rendered)
@@ -639,15 +659,9 @@ static int forward_render_impl(char* geometry_buffer, char* binning_buffer, char
     DEBUG_SYNC(s);
     uint2* ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     uint32_t* tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
-    if (use_tile_diff(gx, gy)) {  // ranges and order from the rects' difference array (tile_hist)
-        ProfScope ps_(PK_TILE_ORDER, s);
-        OrderJob oj = {};
-        oj.order = tile_order;
-        oj.diff = at<int>(ib, im.off[IMG_TILE_DIFF]);
-        oj.ranges_out = ranges;
-        oj.grid_x = gx;
-        oj.grid_y = gy;
-        HIP_TRY(launch_tile_order_batch(&oj, 1, T, s));
+    if (use_tile_diff(gx, gy)) {
+        // ranges and order: written from the rects' difference array by the geometry half (the
+        // auxiliary stream, joined before the tile-count scan)
     } else {
         {
             ProfScope ps_(PK_RANGES, s);
@@ -837,8 +851,16 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         if (e == hipSuccess && use_tile_diff(gx, gy)) {  // the rects' difference arrays, beside the depth sorts
             TileHistJob hj[MAX_VIEWS];
             for (int v = 0; v < V; v++) hj[v] = {pa[v].rect4, P, pa[v].tile_diff};
-            ProfScope ps_(PK_RANGES, aux);
-            e = launch_tile_hist_batch(hj, V, gx, gy, aux);
+            {
+                ProfScope ps_(PK_RANGES, aux);
+                e = launch_tile_hist_batch(hj, V, gx, gy, aux);
+            }
+            if (e == hipSuccess) {  // the views' tile ranges and forward tile orders, beside the sorts
+                OrderJob dj[MAX_VIEWS];
+                for (int v = 0; v < V; v++) dj[v] = diff_order_job(image_buffers[v], width, height, gx, gy);
+                ProfScope ps_(PK_TILE_ORDER, aux);
+                e = launch_tile_order_batch(dj, V, T, aux);
+            }
         }
         if (e == hipSuccess) {
             ProfScope ps_(PK_DEPTH_SORT, ps);
@@ -889,21 +911,14 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         if (L[v] > 0) tsort[ns++] = fused_tile_sort_job(gb, bb, ib, P, L[v], width, height);
         rj[nf] = {L[v], L[v] > 0 ? at<uint32_t>(bb, b.off[BIN_SORTED_TILES]) : nullptr, at<uint2>(ib, im.off[IMG_RANGES])};
         oj[nf] = {at<uint2>(ib, im.off[IMG_RANGES]), nullptr, at<uint32_t>(ib, im.off[IMG_TILE_ORDER])};
-        if (use_tile_diff(gx, gy)) {  // the order kernel writes the ranges from the difference array
-            oj[nf].ranges = nullptr;
-            oj[nf].diff = at<int>(ib, im.off[IMG_TILE_DIFF]);
-            oj[nf].ranges_out = at<uint2>(ib, im.off[IMG_RANGES]);
-            oj[nf].grid_x = gx;
-            oj[nf].grid_y = gy;
-        }
         fit[nf++] = v;
     }
     if (ns) {
         ProfScope ps_(PK_TILE_SORT, ps, true);
         HIP_TRY(tile_sort_fused_batch(tsort, ns, gx, T, ps, FUSED_SCATTER));
     }
-    if (nf) {
-        if (!use_tile_diff(gx, gy)) {
+    if (nf && !use_tile_diff(gx, gy)) {  // (with the difference array: ranges and orders are done)
+        {
             ProfScope ps_(PK_RANGES, ps);
             HIP_TRY(launch_tile_ranges_batch(rj, nf, T, ps));
         }
