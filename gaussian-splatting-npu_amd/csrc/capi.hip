@@ -1008,35 +1008,42 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
         DEBUG_SYNC(s);
     }
 
-    // BACKWARD::preprocess (rasterizer_impl.cu:423-449), with the per-Gaussian gather of the records
-    PreprocessBwdArgs p;
+    // BACKWARD::preprocess (rasterizer_impl.cu:423-449), with the per-Gaussian gather of the records:
+    // the batched kernel at one lane per Gaussian (launch_preprocess_bwd_single)
+    PreprocessBwdViewsArgs A;
+    PreprocessBwdArgs& p = A.a;
     p.P = P; p.D = D; p.M = dc ? M + 1 : M;
     p.means3D = means3D; p.radii = rad; p.shs = shs; p.dc = dc; p.dL_ddc = dc ? dL_ddc : nullptr;
-    p.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
     p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
     p.cov3D_precomp = cov3D_precomp;
-    p.view = viewmatrix; p.proj = projmatrix;
-    p.focal_y = height / (2.0f * tan_fovy);
-    p.focal_x = width / (2.0f * tan_fovx);
-    p.tan_fovx = tan_fovx; p.tan_fovy = tan_fovy;
-    p.campos = campos;
     p.antialiasing = antialiasing;
-    p.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
-    p.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
-    p.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
-    p.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
-    p.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
     p.has_invdepth = dL_invdepths != nullptr;
-    p.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
     p.W = width; p.H = height;
-    p.dL_dmean2D = dL_dmean2D; p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
+    p.dL_dconic = dL_dconic; p.dL_dinvdepth = dL_dinvdepth;
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
     p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;
     p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;
     p.acc = accumulate;
+    A.V = 1;
+    A.g_begin = 0;
+    A.g_end = P;
+    BwdView& bv = A.v[0];
+    bv.view = viewmatrix; bv.proj = projmatrix; bv.campos = campos;
+    bv.focal_y = height / (2.0f * tan_fovy);
+    bv.focal_x = width / (2.0f * tan_fovx);
+    bv.tan_fovx = tan_fovx; bv.tan_fovy = tan_fovy;
+    bv.radii = rad;
+    bv.conic_opacity = at<float4>(gb, g.off[GEOM_CONIC_OPACITY]);
+    bv.clamped = at<uint8_t>(gb, g.off[GEOM_CLAMPED]);
+    bv.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
+    bv.tiles_touched = at<uint32_t>(gb, g.off[GEOM_TILES_TOUCHED]);
+    bv.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
+    bv.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
+    bv.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
+    bv.dL_dmean2D = dL_dmean2D;
     {
         ProfScope ps_(PK_PREPROCESS_BWD, s);
-        HIP_TRY(launch_preprocess_bwd(p, s));
+        HIP_TRY(launch_preprocess_bwd_single(A, s));
     }
     DEBUG_SYNC(s);
     return GSR_OK;
@@ -1165,19 +1172,14 @@ int gsr_backward_preprocess_views_range(int V, int P, int D, int M, const int* R
     PreprocessBwdArgs& p = A.a;
     p.P = P; p.D = D; p.M = dc ? M + 1 : M;
     p.means3D = means3D; p.radii = nullptr; p.shs = shs; p.dc = dc; p.dL_ddc = dc ? dL_ddc : nullptr;
-    p.clamped = nullptr;
     p.opacities = opacities; p.scales = scales; p.rotations = rotations; p.scale_modifier = scale_modifier;
     p.cov3D_precomp = cov3D_precomp;
-    p.view = nullptr; p.proj = nullptr; p.campos = nullptr;
-    p.focal_x = p.focal_y = p.tan_fovx = p.tan_fovy = 0.f;
     p.antialiasing = antialiasing;
-    p.grad_inst = nullptr; p.valid = nullptr; p.emit_start = nullptr; p.tiles_touched = nullptr; p.rec_mask = nullptr;
     // a view rendered without an inverse-depth gradient has zero invdepth fields in its records:
     // subtracting their (zero) term leaves its gradients bit-identical
     p.has_invdepth = has_invdepth;
-    p.conic_opacity = nullptr;
     p.W = width; p.H = height;
-    p.dL_dmean2D = nullptr; p.dL_dconic = nullptr; p.dL_dinvdepth = nullptr;
+    p.dL_dconic = nullptr; p.dL_dinvdepth = nullptr;
     p.dL_dopacity = dL_dopacity; p.dL_dcolor = dL_dcolor;
     p.dL_dmean3D = dL_dmean3D; p.dL_dcov3D = dL_dcov3D; p.dL_dsh = (shs && M > 0) ? dL_dsh : nullptr;
     p.dL_dscale = dL_dscale; p.dL_drot = dL_drot;

@@ -100,33 +100,18 @@ enum AccBits : uint32_t {
 struct PreprocessBwdArgs {
     int P, D, M;
     const float* means3D;
-    const int* radii;
+    const int* radii;  // the single-view launch: visibility radius > 0 (backward.cu:420); null for batches
     const float* shs;  // as PreprocessArgs: with dc, the rest coefficients and M counts dc
     const float* dc;
-    const uint8_t* clamped;
     const float* opacities;
     const float* scales;
     const float* rotations;
     float scale_modifier;
     const float* cov3D_precomp;  // null: cov3D is recomputed from scales/rotations
-    const float* view;
-    const float* proj;
-    float focal_x, focal_y, tan_fovx, tan_fovy;
-    const float* campos;
     int antialiasing;
-    // per-instance gradient records and the gather map
-    const float* grad_inst;         // f32x12[L], at the record slots (Gaussian order)
-    const uint32_t* valid;          // one bit per slot: records not flagged were never written (no contribution)
-    // (Gaussian i's records are slots [emit_start[i], +tiles_touched[i]), emit_start the index-order
-    // exclusive scan of tiles_touched)
-    const uint32_t* emit_start;     // first record slot of Gaussian i
-    const uint32_t* tiles_touched;  // number of record slots of Gaussian i
-    const uint32_t* rec_mask;       // GEOM_REC_MASK: which of slots [emit_start, + 32) hold a record
     int has_invdepth;
-    const float4* conic_opacity;    // GEOM_CONIC_OPACITY (the rendered, AA-scaled opacity in .w)
     int W, H;
-    // reduced per-Gaussian render gradients (fully written; outputs of the reference glue)
-    float* dL_dmean2D;   // (P,3)
+    // the single-view launch's other render-pass gradients (outputs of the reference glue; null for batches)
     float* dL_dconic;    // (P,4)
     float* dL_dinvdepth; // (P) or null
     float* dL_dopacity;  // (P)
@@ -319,8 +304,9 @@ hipError_t launch_render_bwd(const RenderBwdArgs& a, int T, hipStream_t s);
 // view with dL_invdepths, or none
 hipError_t launch_render_fwd_batch(const RenderFwdArgs* a, int V, int T, hipStream_t s);
 hipError_t launch_render_bwd_batch(const RenderBwdArgs* a, int V, int T, hipStream_t s);
-hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& a, hipStream_t s);
+// one view through the batched kernel at one lane per Gaussian (a.radii set: the view's visibility)
+hipError_t launch_preprocess_bwd_single(const PreprocessBwdViewsArgs& a, hipStream_t s);
 
 // fused SSIM (ssim.hip); dA/dB/dC null: map only
 hipError_t launch_ssim_fwd(int planes, int H, int W, float C1, float C2, const float* img1, const float* img2,

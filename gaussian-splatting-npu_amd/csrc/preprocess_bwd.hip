@@ -1,8 +1,9 @@
 // preprocess_bwd.hip -- BACKWARD::preprocess (backward.cu:640-712): the
 // reference's two per-Gaussian kernels computeCov2DCUDA (backward.cu:147-326)
 // and preprocessCUDA (backward.cu:398-449, with computeColorFromSH :23-142 and
-// computeCov3D :330-393) fused into one gfx950 kernel, one thread per
-// Gaussian.  Every output row is written (zeros for culled Gaussians), so the
+// computeCov3D :330-393) fused into one gfx950 kernel for one view or a batch
+// of views: LPG lanes per Gaussian, one per view (one lane for a single view,
+// gsr_backward).  Every output row is written (zeros for culled Gaussians), so the
 // caller does not have to pre-zero dL_dmean3D / dL_dcov3D / dL_dsh /
 // dL_dscale / dL_drot.  HBM-bound: reads ~236 B/G of parameters + the 44 B/G
 // gradient record, writes ~232 B/G.
@@ -23,20 +24,20 @@ __device__ __forceinline__ void put(float* p, float v, bool acc, float old) { *p
 // overlap it (and each other): every load is issued unconditionally (clamped indices, values
 // masked after), so no branch sits between a load and the next one.
 struct BwdIn {
-    bool visible;
-    float g[GF_NUM];  // sums of this Gaussian's per-tile gradient records
-    float4 co;        // conic + (rendered) opacity
     float cov[6];
     f3 mean;
     float4 rot;
     f3 scale;
     float opacity;
-    uint8_t clamped;
     // accumulating (AccBits): the outputs' current values, loaded here with everything else
     float old_mean[3], old_opacity, old_scale[3], old_rot[4];
 };
 
-constexpr int REC_BATCH = 8;  // record flags / records in flight per step (4: +3 us, 2: +10 us)
+// records in flight per lane (the V lanes of a Gaussian already gather side by side)
+#ifndef GSR_VIEW_REC_BATCH
+#define GSR_VIEW_REC_BATCH 4
+#endif
+constexpr int REC_BATCH = GSR_VIEW_REC_BATCH;
 
 // Sum of one Gaussian's per-tile gradient records of one view.  Its records are contiguous
 // (slots [emit_start, + tiles_touched)); entries that contributed to no pixel were never written (their bit in the valid
@@ -139,26 +140,10 @@ __device__ __forceinline__ void gather_any(uint32_t e0, uint32_t n, uint32_t mas
     if (n > 32u) gather_range<B, false>(e0 + 32u, e0 + n, valid, grad_inst, g);
 }
 
-template <int B = REC_BATCH>
-__device__ __forceinline__ void gather_records(const uint32_t* emit_start, const uint32_t* tiles_touched,
-                                               const uint32_t* rec_mask, const uint32_t* valid, const float* grad_inst,
-                                               int idx, float (&g)[GF_NUM])
-{
-    const uint32_t e0 = emit_start[idx], n = tiles_touched[idx];  // 0 tiles for culled Gaussians
-    const uint32_t mask = rec_mask[idx];
-    gather_any<B>(e0, n, mask, valid, grad_inst, g);
-}
-
-// The per-Gaussian parameters (and, accumulating, the outputs' old values); with `view` also the
-// launch's own view: visibility, conic, clamp flags and records.
-__device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in, bool view = true)
+// The per-Gaussian parameters (and, accumulating, the outputs' old values).
+__device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, BwdIn& in)
 {
     const size_t i = (size_t)idx;
-    if (view) {
-        in.visible = a.radii[idx] > 0;
-        in.co = a.conic_opacity[idx];
-        in.clamped = a.clamped[idx];
-    }
     if (a.cov3D_precomp) {  // uniform over the launch
 #pragma unroll
         for (int k = 0; k < 6; k++) in.cov[k] = a.cov3D_precomp[6 * i + k];
@@ -183,20 +168,7 @@ __device__ __forceinline__ void bwd_gather(const PreprocessBwdArgs& a, int idx, 
         const float* r = a.dL_drot + 4 * i;
         in.old_rot[0] = r[0]; in.old_rot[1] = r[1]; in.old_rot[2] = r[2]; in.old_rot[3] = r[3];
     }
-    if (view) gather_records(a.emit_start, a.tiles_touched, a.rec_mask, a.valid, a.grad_inst, idx, in.g);
 }
-
-// Per-Gaussian state carried from the non-SH part into the SH halves and the final dL/dmean3D.
-struct BwdState {
-    bool visible;
-    int ncoef;            // SH coefficients in use: (D + 1)^2, at most M (0: colors_precomp / culled)
-    f3 dir_orig;          // mean - campos (backward.cu:31)
-    float x, y, z;        // its normalisation
-    float dRGB[3];        // dL/dcolor, zeroed for clamped channels (backward.cu:41-44)
-    float dmx, dmy, dmz;  // dL/dmean3D without the view-direction term
-    float ddir[3];        // dL/d(normalised direction), summed over the SH coefficients
-    float old_mean[3];    // accumulating: dL/dmean3D's current value
-};
 
 // Coefficient k's factor dRGB/dsh_k (backward.cu:51-100, same expressions: dL/dsh is
 // bit-identical) and its derivatives along the normalised view direction (the per-coefficient
@@ -238,52 +210,6 @@ __device__ __forceinline__ void sh_term(int k, float x, float y, float z, float&
     }
 }
 
-// SH backward over coefficients [K0, K1) (computeColorFromSH backward, backward.cu:23-142):
-// dL/dsh_k = b_k * dRGB, and the view-direction gradient accumulated into st.ddir.  `sh` / `dsh`
-// point at coefficient K0 of this Gaussian (global memory or its LDS staging row; they may be
-// the same row: every coefficient is read before it is overwritten).
-// Coefficients at or beyond `kw` (the row width in coefficients) are not written.
-template <int K0, int K1>
-__device__ __forceinline__ void sh_bwd_range(BwdState& st, const float* sh, float* dsh, int kw = K1, bool acc = false)
-{
-#pragma unroll
-    for (int k = K0; k < K1; k++) {
-        if (k < st.ncoef) {
-            float b, gx, gy, gz;
-            sh_term(k, st.x, st.y, st.z, b, gx, gy, gz);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                const float v = sh[(k - K0) * 3 + c];
-                const float t = v * st.dRGB[c];
-                put(&dsh[(k - K0) * 3 + c], b * st.dRGB[c], acc);
-                st.ddir[0] += t * gx;
-                st.ddir[1] += t * gy;
-                st.ddir[2] += t * gz;
-            }
-        } else if (k < kw && !acc) {
-#pragma unroll
-            for (int c = 0; c < 3; c++) dsh[(k - K0) * 3 + c] = 0.f;
-        }
-    }
-}
-
-// dL/dmean3D with the view-direction term (backward.cu:130-141, 423-440), written.
-__device__ __forceinline__ void bwd_finish(const PreprocessBwdArgs& a, int idx, const BwdState& st)
-{
-    float* dmean = a.dL_dmean3D + 3 * (size_t)idx;
-    float dmx = st.dmx, dmy = st.dmy, dmz = st.dmz;
-    if (st.visible && st.ncoef > 1) {  // degree 0 has no direction dependence
-        const f3 dn = dnormvdv(st.dir_orig, {st.ddir[0], st.ddir[1], st.ddir[2]});
-        dmx += dn.x;
-        dmy += dn.y;
-        dmz += dn.z;
-    }
-    const bool acc = a.acc & ACC_MEANS3D;
-    put(dmean, dmx, acc, st.old_mean[0]);
-    put(dmean + 1, dmy, acc, st.old_mean[1]);
-    put(dmean + 2, dmz, acc, st.old_mean[2]);
-}
-
 // One camera of the backward: the launch's own (single view) or an entry of the multi-view table.
 struct ViewCam {
     const float* view;
@@ -291,11 +217,6 @@ struct ViewCam {
     const float* campos;
     float focal_x, focal_y, tan_fovx, tan_fovy;
 };
-
-__device__ __forceinline__ ViewCam cam_of(const PreprocessBwdArgs& a)
-{
-    return {a.view, a.proj, a.campos, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy};
-}
 
 // One view's contribution to one visible Gaussian's gradients (no memory access).
 struct ViewGrad {
@@ -554,75 +475,6 @@ __device__ __forceinline__ void put_scale_rot(const PreprocessBwdArgs& a, int id
     }
 }
 
-// Everything of one Gaussian except the SH coefficients, for the launch's own view: the reduced
-// render gradients, view_grad, computeCov3D backward; sets up the SH state.
-__device__ __forceinline__ void bwd_core(const PreprocessBwdArgs& a, int idx, const BwdIn& in, BwdState& st)
-{
-    const size_t i = (size_t)idx;
-    st.visible = in.visible;
-    st.ncoef = 0;
-    st.dmx = st.dmy = st.dmz = 0.f;
-    st.ddir[0] = st.ddir[1] = st.ddir[2] = 0.f;
-    st.old_mean[0] = in.old_mean[0]; st.old_mean[1] = in.old_mean[1]; st.old_mean[2] = in.old_mean[2];
-    float* dcov_out = a.dL_dcov3D + 6 * i;
-
-    if (!in.visible) {
-        a.dL_dmean2D[3 * i] = 0.f; a.dL_dmean2D[3 * i + 1] = 0.f; a.dL_dmean2D[3 * i + 2] = 0.f;
-        a.dL_dconic[4 * i] = 0.f; a.dL_dconic[4 * i + 1] = 0.f; a.dL_dconic[4 * i + 2] = 0.f;
-        a.dL_dconic[4 * i + 3] = 0.f;
-        // accumulated outputs gain nothing from a culled Gaussian: left as they are
-        if (!(a.acc & ACC_OPACITY)) a.dL_dopacity[i] = 0.f;
-        if (!(a.acc & ACC_COLORS)) {
-            a.dL_dcolor[3 * i] = 0.f; a.dL_dcolor[3 * i + 1] = 0.f; a.dL_dcolor[3 * i + 2] = 0.f;
-        }
-        if (a.dL_dinvdepth) a.dL_dinvdepth[i] = 0.f;
-        if (!(a.acc & ACC_COV3D)) {
-#pragma unroll
-            for (int k = 0; k < 6; k++) dcov_out[k] = 0.f;
-        }
-        if (a.dL_dscale && !(a.acc & ACC_SCALES)) {
-            a.dL_dscale[3 * i] = 0.f; a.dL_dscale[3 * i + 1] = 0.f; a.dL_dscale[3 * i + 2] = 0.f;
-        }
-        if (a.dL_drot && !(a.acc & ACC_ROTATIONS)) {
-            float* dr = a.dL_drot + 4 * i; dr[0] = 0.f; dr[1] = 0.f; dr[2] = 0.f; dr[3] = 0.f;
-        }
-        return;
-    }
-
-    float cov3D[6];
-    cov3d_of(a, in, cov3D);
-    ViewGrad o;
-    view_grad(a, cam_of(a), in.g, in.co, in.clamped, in.mean, in.opacity, cov3D, o);
-    const float* g = o.g;
-    // render-pass gradients of the reference glue (rasterize_points.cu:164-172), fully written
-    a.dL_dmean2D[3 * i] = g[GF_MEAN2D_X]; a.dL_dmean2D[3 * i + 1] = g[GF_MEAN2D_Y]; a.dL_dmean2D[3 * i + 2] = 0.f;
-    a.dL_dconic[4 * i] = g[GF_CONIC_A]; a.dL_dconic[4 * i + 1] = g[GF_CONIC_B]; a.dL_dconic[4 * i + 2] = 0.f;
-    a.dL_dconic[4 * i + 3] = g[GF_CONIC_C];
-    {
-        const bool acc = a.acc & ACC_COLORS;
-        put(a.dL_dcolor + 3 * i, g[GF_COLOR_R], acc);
-        put(a.dL_dcolor + 3 * i + 1, g[GF_COLOR_G], acc);
-        put(a.dL_dcolor + 3 * i + 2, g[GF_COLOR_B], acc);
-    }
-    if (a.dL_dinvdepth) a.dL_dinvdepth[i] = g[GF_INVDEPTH];
-    put(a.dL_dopacity + idx, o.dopacity, a.acc & ACC_OPACITY, in.old_opacity);
-#pragma unroll
-    for (int k = 0; k < 6; k++) put(dcov_out + k, o.dcov[k], a.acc & ACC_COV3D);
-    st.dmx = o.dmx;
-    st.dmy = o.dmy;
-    st.dmz = o.dmz;
-    if (a.shs || a.dc) {
-        st.ncoef = sh_ncoef(a);
-        st.dir_orig = o.dir_orig;
-        st.x = o.x;
-        st.y = o.y;
-        st.z = o.z;
-#pragma unroll
-        for (int c = 0; c < 3; c++) st.dRGB[c] = o.dRGB[c];
-    }
-    put_scale_rot(a, idx, in, o.dcov);
-}
-
 // SH coefficients (48 floats per Gaussian at degree 3) are the bulk of this kernel's traffic.
 // STAGED (M = 16): the workgroup's 256 rows are read with coalesced 16-byte loads into LDS rows
 // padded to 49 dwords (an odd stride: the 64 lanes walking their own rows hit 64 different
@@ -659,12 +511,6 @@ __device__ __forceinline__ float group_sum(float x)
     return x;
 }
 
-// records in flight per lane: the V lanes of a Gaussian already gather side by side
-#ifndef GSR_VIEW_REC_BATCH
-#define GSR_VIEW_REC_BATCH 4
-#endif
-constexpr int VIEW_REC_BATCH = GSR_VIEW_REC_BATCH;
-
 // A lane's view inputs, loaded in the kernel's prologue (unconditionally, clamped), so that their
 // round trip overlaps the SH staging and the record gather is the only dependent one after it.
 struct ViewIn {
@@ -672,6 +518,7 @@ struct ViewIn {
     uint8_t cl;
     uint32_t e0, n;  // record slots [e0, e0 + n)
     uint32_t mask;   // which of the first 32 hold a record
+    bool drawn;      // the single-view launch (a.radii set): radius > 0 (backward.cu:420)
 };
 
 __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int idx, int v, ViewIn& vi)
@@ -682,6 +529,7 @@ __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int i
     vi.e0 = bv.emit_start[idx];
     vi.n = bv.tiles_touched[idx];
     vi.mask = bv.rec_mask[idx];
+    vi.drawn = A.a.radii ? A.a.radii[idx] > 0 : true;
 }
 
 // The batch's cameras in LDS (view 16, proj 16, campos 3, focal_x, focal_y, tan_fovx, tan_fovy),
@@ -726,10 +574,11 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     const BwdView& bv = A.v[v < A.V ? v : 0];
     // visible <=> radius > 0 (backward.cu:163,420) <=> a tile count > 0: preprocess culls a Gaussian whose
     // rect is empty and writes radius 0 and no tiles for every culled one (4 B per view less to read)
-    const bool vis = has_view && vi.n > 0;
+    // (the single-view launch keeps the reference's test on the caller's radii)
+    const bool vis = has_view && (a.radii ? vi.drawn : vi.n > 0);
     float gs[GF_NUM];
     if (vis) {
-        gather_any<VIEW_REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
+        gather_any<REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
@@ -753,6 +602,11 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     if (has_view) {
         float* m2 = bv.dL_dmean2D + 3 * i;
         m2[0] = o.g[GF_MEAN2D_X]; m2[1] = o.g[GF_MEAN2D_Y]; m2[2] = 0.f;
+        if (a.dL_dconic) {  // the single-view launch's other render-pass gradients (rasterize_points.cu:164-172)
+            float* dc4 = a.dL_dconic + 4 * i;
+            dc4[0] = o.g[GF_CONIC_A]; dc4[1] = o.g[GF_CONIC_B]; dc4[2] = 0.f; dc4[3] = o.g[GF_CONIC_C];
+        }
+        if (a.dL_dinvdepth) a.dL_dinvdepth[i] = o.g[GF_INVDEPTH];
     }
     const bool writer = live && v == 0;
     {
@@ -890,43 +744,6 @@ __device__ __forceinline__ void staged_sh(const PreprocessBwdArgs& a, float* s_s
 // Shared-memory bytes of staged_sh for ROWS rows (either layout).
 constexpr int staged_lds_bytes(int rows) { return rows * SH_STRIDE * 4; }
 
-// STAGED: the SH rows of the workgroup's 256 Gaussians go through LDS (staged_sh), one thread per
-// Gaussian.
-template <bool STAGED>
-__global__ void __launch_bounds__(256) preprocess_bwd_kernel(const PreprocessBwdArgs a)
-{
-    extern __shared__ __attribute__((aligned(16))) float s_sh[];
-    const int base = blockIdx.x * 256;
-    const int idx = base + (int)threadIdx.x;
-    BwdIn in;
-    BwdState st;
-    if (idx < a.P) bwd_gather(a, idx, in);  // in flight during the SH staging
-    if (!STAGED) {
-        if (idx < a.P) {
-            const size_t w3 = (size_t)a.M * 3;
-            bwd_core(a, idx, in, st);
-            if (a.dL_dsh) {
-                float* dsh = a.dL_dsh + idx * w3;
-                // ncoef <= M: no read past the row; no write past it either (M < 16)
-                const bool acc = a.acc & ACC_SH;
-                if (a.shs) sh_bwd_range<0, 16>(st, a.shs + idx * w3, dsh, a.M, acc);
-                if (!acc)
-                    for (int k = a.shs ? 48 : 0; k < a.M * 3; k++) dsh[k] = 0.f;
-            }
-            bwd_finish(a, idx, st);
-        }
-        return;
-    }
-    staged_sh<256>(a, s_sh, base, min(256, a.P - base), threadIdx.x, [&](float* c0, float* cr, int kw) {
-        if (idx < a.P) {
-            bwd_core(a, idx, in, st);
-            sh_bwd_range<0, 1>(st, c0, c0);
-            sh_bwd_range<1, 16>(st, cr, cr, kw);
-            bwd_finish(a, idx, st);
-        }
-    });
-}
-
 // The multi-view batch: 256 / LPG Gaussians per workgroup, LPG lanes each (bwd_views_group).
 template <int LPG, bool STAGED>
 __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const PreprocessBwdViewsArgs A)
@@ -942,7 +759,7 @@ __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const Preproc
     const int idx = live ? base + gl : A.g_end - 1;  // clamped: all lanes take part in the reductions
     __shared__ float s_cam[MAX_VIEWS][CAM_FLOATS];
     BwdIn in;
-    bwd_gather(a, idx, in, false);
+    bwd_gather(a, idx, in);
     ViewIn vi;
     view_load(A, idx, v, vi);  // in flight during the camera and SH staging
     cams_to_lds(A, s_cam);
@@ -970,17 +787,6 @@ static bool staged_layout(const PreprocessBwdArgs& a)
     return interleaved || (a.dc && a.dL_ddc);
 }
 
-hipError_t launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s)
-{
-    if (a.P <= 0) return hipSuccess;
-    const dim3 grid((a.P + 255) / 256), block(256);
-    if (staged_layout(a))
-        hipLaunchKernelGGL((preprocess_bwd_kernel<true>), grid, block, staged_lds_bytes(256), s, a);
-    else
-        hipLaunchKernelGGL((preprocess_bwd_kernel<false>), grid, block, 0, s, a);
-    return hipGetLastError();
-}
-
 template <int LPG>
 static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
@@ -991,6 +797,13 @@ static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
     else
         hipLaunchKernelGGL((preprocess_bwd_views_kernel<LPG, false>), grid, block, 0, s, A);
     return hipGetLastError();
+}
+
+hipError_t launch_preprocess_bwd_single(const PreprocessBwdViewsArgs& A, hipStream_t s)
+{
+    if (A.V != 1 || !A.a.radii || A.g_begin != 0 || A.g_end != A.a.P) return hipErrorInvalidValue;
+    if (A.a.P <= 0) return hipSuccess;
+    return launch_views<1>(A, s);
 }
 
 hipError_t launch_preprocess_bwd_views(const PreprocessBwdViewsArgs& A, hipStream_t s)

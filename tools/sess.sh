@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box session in steps, each under its own time limit; the first failing step ends it.
 # Usage: tools/sess.sh <tag> <step>...   steps: test | testsel:<pytest selection> | bench | benchq |
-#        trace | hits | pmc
+#        trace | hits | pmc | uselib:<ab name> | ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-sess}
@@ -49,6 +49,8 @@ PY
     pmc) run pmc 400 bash tools/profile_pmc.sh "$TAG/pmc" ;;
     dist) run dist 700 bash tools/dist_rehearsal.sh "$TAG/dist" ;;
     calib) run calib 500 bash tools/hbm_calib.sh "$TAG/calib" ;;
+    uselib:*)  # ab/<name>.so becomes the in-tree library for the steps after this one
+          cp -f "ab/${st#uselib:}.so" gaussian-splatting-npu_amd/diff_gaussian_rasterization/libgsr_hip.so && echo "=== using ab/${st#uselib:}.so" ;;
     ab:*) run ab 900 bash tools/ab.sh ${st#ab:} ;;
     ab1:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred" run ab1 900 bash tools/ab.sh ${st#ab1:} ;;
     ab1np:*) BENCH_EXTRA="--views-total 1 --per-view --no-deferred --no-prefix-stream" run ab1np 900 bash tools/ab.sh ${st#ab1np:} ;;
