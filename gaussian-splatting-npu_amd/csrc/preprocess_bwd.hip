@@ -33,7 +33,8 @@ struct BwdIn {
     float old_mean[3], old_opacity, old_scale[3], old_rot[4];
 };
 
-// records in flight per lane (the V lanes of a Gaussian already gather side by side)
+// records in flight per lane (the V lanes of a Gaussian already gather side by side; twice as many
+// at one lane per Gaussian)
 #ifndef GSR_VIEW_REC_BATCH
 #define GSR_VIEW_REC_BATCH 4
 #endif
@@ -578,7 +579,9 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     const bool vis = has_view && (a.radii ? vi.drawn : vi.n > 0);
     float gs[GF_NUM];
     if (vis) {
-        gather_any<REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
+        // one lane per Gaussian: 8 records in flight (145 VGPRs; the SH staging caps it at 3 waves/SIMD
+        // anyway): 145 -> 141 us per 1080p view
+        gather_any<LPG == 1 ? 2 * REC_BATCH : REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
