@@ -135,7 +135,12 @@ int gsr_forward_prealloc(char* geometry_buffer, char* image_buffer, char* binnin
  * The render-pass gradients (dL_dmean2D (P,3), dL_dconic (P,2,2),
  * dL_dopacity (P), dL_dcolor (P,3), dL_dinvdepth (P)) are reduced on chip and
  * gathered per Gaussian in a fixed order: results are bitwise reproducible
- * run to run (the reference sums with float atomics). */
+ * run to run (the reference sums with float atomics).
+ * radii (may be NULL: the forward's own, in geom_buffer) gate each Gaussian as
+ * backward.cu:163,420 do; a Gaussian with radius 0 gets zeros in EVERY output,
+ * including the render-pass ones the reference would still report from its
+ * render backward -- the two agree for radii produced by the forward (radius 0
+ * <=> no tile <=> no record). */
 int gsr_backward(int P, int D, int M, int R,
                  const float* background,
                  int width, int height,
