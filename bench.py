@@ -151,6 +151,7 @@ def lib_sha256():
 
 
 PMC_CHILD_STEPS = 2  # the --pmc-child workload: 1 warm-up + 1 step
+PMC_COUNTED_STEPS = 1  # the steps after the child's marker kernel (tools/pmc_summary.MARKER)
 
 
 def workload_stamp(args, world, views_rank):
@@ -165,7 +166,8 @@ def pmc_traffic(args, world, timeout=240):
     """HBM traffic and VALU wave-instructions of every rasterizer operation, measured now on this
     build: three rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE -- together they exceed the 4 TCC
     counters of one pass -- and SQ_INSTS_VALU) over this script's own workload (`--pmc-child`:
-    this rank's views, PMC_CHILD_STEPS steps, nothing else), each a child process under a time
+    this rank's views, PMC_CHILD_STEPS steps of which the dispatches after the warm-up's marker
+    kernel are counted, nothing else), each a child process under a time
     limit; bytes = 2 FETCH_SIZE + WRITE_SIZE (KiB) per MI355X_MICROARCH.md §HBM.  Returns the
     pmc_summary totals over all dispatches of each operation (the caller divides by the number of
     calls), or None if rocprofv3 is absent or a pass fails."""
@@ -202,7 +204,8 @@ def pmc_traffic(args, world, timeout=240):
                 sys.stdout = old
         t = json.load(open(os.path.join(tmp, "pmc_traffic.json")))
         v = json.load(open(os.path.join(tmp, "pmc_valu.json")))
-        return {"bytes_total": t["bytes_total"], "winst_total": v["winst_total"]}
+        return {"bytes_total": t["bytes_total"], "winst_total": v["winst_total"],
+                "marked": bool(t.get("marked")) and bool(v.get("marked"))}
     except Exception:
         return None
     finally:
@@ -449,7 +452,14 @@ def main(argv=None):
             main_stream.wait_stream(st)
 
     if args.pmc_child:  # the workload of one --pmc pass (pmc_traffic): nothing printed, nothing timed
-        for _ in range(args.warmup + args.steps):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        # the marker (tools/pmc_summary.MARKER): the summary counts the dispatches after it only --
+        # the warm-up holds a first call's binning re-run, geometry dispatches no timed step has
+        torch.cuda._sleep(1)
+        torch.cuda.synchronize()
+        for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         return
@@ -562,9 +572,11 @@ def main(argv=None):
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
         sha = lib_sha256()
         stamp = workload_stamp(args, world, len(cams))
-        # calls of each operation during the PMC child's steps: launches per step (instrumented pass)
-        # x PMC_CHILD_STEPS; traffic per launch = the op's bytes over all its dispatches / its calls
-        calls = {k: v["launches"] / args.steps * PMC_CHILD_STEPS for k, v in kern.items()}
+        # calls of each operation during the PMC child's counted steps: launches per step (instrumented
+        # pass) x the steps after its marker (x all its steps when no marker was seen); traffic per
+        # launch = the op's bytes over those dispatches / its calls
+        n_pmc = PMC_COUNTED_STEPS if (pmc and pmc.get("marked")) else PMC_CHILD_STEPS
+        calls = {k: v["launches"] / args.steps * n_pmc for k, v in kern.items()}
         traffic_all, valu_all, traffic_src, vsrc = None, None, None, None
         if pmc:
             traffic_all = {k: round(v / calls[k]) for k, v in pmc["bytes_total"].items() if calls.get(k)}

@@ -29,6 +29,8 @@ SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "preprocess_views_kernel": "
          # SURVEY §8f side paths (bench.py aux leg)
          "knn_": "distCUDA2", "ssim_fwd_kernel": "ssim_fwd", "ssim_bwd_kernel": "ssim_bwd",
          "adam_update_multi_kernel": "sparse_adam"}
+# the kernel bench.py --pmc-child launches between its warm-up and its counted steps
+MARKER = "spin_kernel"
 # operations made of several kernels (several dispatches per call)
 MULTI = ("depth_sort", "tile_sort", "distCUDA2")
 
@@ -42,16 +44,27 @@ def short_name(k):
 
 def main(d, lib_sha256=None, workload=None, calls=None):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    marked = bool(files)
+    for f in files:
         with open(f) as fh:
-            for row in csv.DictReader(fh):
-                k = row.get("Kernel_Name", "")
-                c = row.get("Counter_Name", "")
-                try:
-                    v = float(row.get("Counter_Value", "nan"))
-                except ValueError:
-                    continue
-                acc[k][c].append((row.get("Dispatch_Id", ""), v))
+            rows = list(csv.DictReader(fh))
+        # bench.py --pmc-child launches a marker kernel (torch.cuda._sleep: spin_kernel) after its
+        # warm-up: only the dispatches after it are counted (the warm-up holds a first call's binning
+        # re-run, extra geometry dispatches that no timed step has)
+        marks = [int(r["Dispatch_Id"]) for r in rows if MARKER in r.get("Kernel_Name", "") and r.get("Dispatch_Id")]
+        first = min(marks) if marks else None
+        marked = marked and first is not None
+        for row in rows:
+            if first is not None and int(row.get("Dispatch_Id") or 0) < first:
+                continue
+            k = row.get("Kernel_Name", "")
+            c = row.get("Counter_Name", "")
+            try:
+                v = float(row.get("Counter_Value", "nan"))
+            except ValueError:
+                continue
+            acc[k][c].append((row.get("Dispatch_Id", ""), v))
     out = {}
     for k, cs in acc.items():
         if "gsr" not in k and "rocprim" not in k and "hipcub" not in k:
@@ -103,16 +116,19 @@ def main(d, lib_sha256=None, workload=None, calls=None):
     # figures only for that build and that workload
     json.dump({"lib_sha256": lib_sha256, "workload": workload,
                "bytes_per_launch": {k: round(v) for k, v in traffic.items()},
-               "bytes_total": {k: round(v) for k, v in t_tot.items()}, "dispatches": dict(t_n)},
+               "bytes_total": {k: round(v) for k, v in t_tot.items()}, "dispatches": dict(t_n),
+               "marked": marked},
               open(os.path.join(d, "pmc_traffic.json"), "w"), indent=1)
     # VALU wave-instructions per launch (bench.py's secondary, VALU-issue roofline)
     v_tot, v_n = totals(lambda e: e.get("SQ_INSTS_VALU"))
     valu = per_launch(v_tot, v_n)
     json.dump({"lib_sha256": lib_sha256, "workload": workload,
                "winst_per_launch": {k: round(v) for k, v in valu.items()},
-               "winst_total": {k: round(v) for k, v in v_tot.items()}, "dispatches": dict(v_n)},
+               "winst_total": {k: round(v) for k, v in v_tot.items()}, "dispatches": dict(v_n),
+               "marked": marked},
               open(os.path.join(d, "pmc_valu.json"), "w"), indent=1)
-    print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()}},
+    print(json.dumps({"kernels": out, "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()},
+                      "marked": marked},
                      indent=1))
 
 
