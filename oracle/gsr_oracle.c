@@ -652,13 +652,21 @@ static inline void atomic_addf(float* p, float v)
     *p += v;
 }
 
-/* backward.cu:452-638 (renderCUDA) for one tile */
+/* backward.cu:452-638 (renderCUDA) for one tile.  The reference adds every pixel's terms into the
+ * per-Gaussian sums with float atomics, in no fixed order.  With `ts` (tile sums, gsr_oracle_set_bwd_
+ * tile_sums) the same per-pixel terms are first added into per-list-entry sums of this tile (pixel
+ * order), which are then added into the per-Gaussian sums: the same terms in another summation
+ * order, without 10 atomics per contribution (the training tests' oracle loops). */
+enum { TS_M2X, TS_M2Y, TS_C0, TS_C1, TS_C3, TS_OP, TS_R, TS_G, TS_B, TS_INVD, TS_N };
 static void render_bwd_tile(const oracle_state* st, uint32_t tx, uint32_t ty, const float* bg, const float* colors,
                             const float* dL_dpixels, const float* dL_invdepths, float* dL_dmean2D, float* dL_dconic2D,
-                            float* dL_dopacity, float* dL_dcolors, float* dL_dinvdepths)
+                            float* dL_dopacity, float* dL_dcolors, float* dL_dinvdepths, float* ts)
 {
     const int W = st->W, H = st->H;
     const uint32_t* range = st->ranges + 2 * (ty * st->gx + tx);
+    if (ts) memset(ts, 0, sizeof(float) * TS_N * (size_t)(range[1] - range[0]));
+#define TS_ADD(field, ptr, v) \
+    do { if (ts) ts[(size_t)(k - range[0]) * TS_N + (field)] += (v); else atomic_addf((ptr), (v)); } while (0)
     const float ddelx_dx = 0.5 * W;
     const float ddely_dy = 0.5 * H;
     for (uint32_t ly = 0; ly < BLOCK_Y; ly++)
@@ -700,14 +708,14 @@ static void render_bwd_tile(const oracle_state* st, uint32_t tx, uint32_t ty, co
                     last_color[ch] = c;
                     const float dL_dchannel = dL_dpixel[ch];
                     dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
-                    atomic_addf(&dL_dcolors[gid * 3 + ch], dchannel_dcolor * dL_dchannel);
+                    TS_ADD(TS_R + ch, &dL_dcolors[gid * 3 + ch], dchannel_dcolor * dL_dchannel);
                 }
                 if (dL_dinvdepths) {
                     const float invd = 1.f / st->depths[gid];
                     accum_invdepth_rec = last_alpha * last_invdepth + (1.f - last_alpha) * accum_invdepth_rec;
                     last_invdepth = invd;
                     dL_dalpha += (invd - accum_invdepth_rec) * dL_invdepth;
-                    atomic_addf(&dL_dinvdepths[gid], dchannel_dcolor * dL_invdepth);
+                    TS_ADD(TS_INVD, &dL_dinvdepths[gid], dchannel_dcolor * dL_invdepth);
                 }
                 dL_dalpha *= T;
                 last_alpha = alpha;
@@ -719,14 +727,29 @@ static void render_bwd_tile(const oracle_state* st, uint32_t tx, uint32_t ty, co
                 const float gdy = G * dy;
                 const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                 const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                atomic_addf(&dL_dmean2D[3 * gid + 0], dL_dG * dG_ddelx * ddelx_dx);
-                atomic_addf(&dL_dmean2D[3 * gid + 1], dL_dG * dG_ddely * ddely_dy);
-                atomic_addf(&dL_dconic2D[4 * gid + 0], -0.5f * gdx * dx * dL_dG);
-                atomic_addf(&dL_dconic2D[4 * gid + 1], -0.5f * gdx * dy * dL_dG);
-                atomic_addf(&dL_dconic2D[4 * gid + 3], -0.5f * gdy * dy * dL_dG);
-                atomic_addf(&dL_dopacity[gid], G * dL_dalpha);
+                TS_ADD(TS_M2X, &dL_dmean2D[3 * gid + 0], dL_dG * dG_ddelx * ddelx_dx);
+                TS_ADD(TS_M2Y, &dL_dmean2D[3 * gid + 1], dL_dG * dG_ddely * ddely_dy);
+                TS_ADD(TS_C0, &dL_dconic2D[4 * gid + 0], -0.5f * gdx * dx * dL_dG);
+                TS_ADD(TS_C1, &dL_dconic2D[4 * gid + 1], -0.5f * gdx * dy * dL_dG);
+                TS_ADD(TS_C3, &dL_dconic2D[4 * gid + 3], -0.5f * gdy * dy * dL_dG);
+                TS_ADD(TS_OP, &dL_dopacity[gid], G * dL_dalpha);
             }
         }
+#undef TS_ADD
+    if (!ts) return;
+    for (uint32_t k = range[0]; k < range[1]; k++) {
+        const float* e = ts + (size_t)(k - range[0]) * TS_N;
+        const uint32_t gid = st->vals[k];
+        if (e[TS_M2X] != 0.0f) atomic_addf(&dL_dmean2D[3 * gid + 0], e[TS_M2X]);
+        if (e[TS_M2Y] != 0.0f) atomic_addf(&dL_dmean2D[3 * gid + 1], e[TS_M2Y]);
+        if (e[TS_C0] != 0.0f) atomic_addf(&dL_dconic2D[4 * gid + 0], e[TS_C0]);
+        if (e[TS_C1] != 0.0f) atomic_addf(&dL_dconic2D[4 * gid + 1], e[TS_C1]);
+        if (e[TS_C3] != 0.0f) atomic_addf(&dL_dconic2D[4 * gid + 3], e[TS_C3]);
+        if (e[TS_OP] != 0.0f) atomic_addf(&dL_dopacity[gid], e[TS_OP]);
+        for (int ch = 0; ch < 3; ch++)
+            if (e[TS_R + ch] != 0.0f) atomic_addf(&dL_dcolors[gid * 3 + ch], e[TS_R + ch]);
+        if (dL_dinvdepths && e[TS_INVD] != 0.0f) atomic_addf(&dL_dinvdepths[gid], e[TS_INVD]);
+    }
 }
 
 /* The same per-pixel walk with the gradient arithmetic in float64 -- the accuracy yardstick of the
@@ -818,6 +841,8 @@ static void render_bwd_tile_f64(const oracle_state* st, uint32_t tx, uint32_t ty
 }
 
 static int g_bwd_f64 = 0;
+static int g_bwd_tile_sums = 0;
+void gsr_oracle_set_bwd_tile_sums(int on) { g_bwd_tile_sums = on; }
 /* 1: gsr_oracle_backward runs the render backward in float64 (render_bwd_tile_f64) and rounds its
  * per-Gaussian sums to float32 once, before the (float32) preprocess backward. */
 void gsr_oracle_set_bwd_f64(int on) { g_bwd_f64 = on; }
@@ -1122,11 +1147,30 @@ int gsr_oracle_backward(void* p, const float* bg, const float* means3D, const fl
         if (dL_dinvdepths)
             for (size_t i = 0; i < Pn; i++) dL_dinvdepths[i] = (float)acc[11 * Pn + i];
         free(acc);
+    } else if (g_bwd_tile_sums) {
+        uint32_t maxlen = 0;
+        for (size_t t = 0; t < T; t++) maxlen = maxlen > st->ranges[2 * t + 1] - st->ranges[2 * t] ? maxlen : st->ranges[2 * t + 1] - st->ranges[2 * t];
+        int fail = 0;
+#pragma omp parallel
+        {
+            float* ts = (float*)malloc(((size_t)maxlen + 1) * TS_N * sizeof(float));
+            if (!ts) {
+#pragma omp atomic write
+                fail = 1;
+            } else {
+#pragma omp for schedule(dynamic, 4)
+                for (int t = 0; t < (int)T; t++)
+                    render_bwd_tile(st, (uint32_t)t % st->gx, (uint32_t)t / st->gx, bg, color_ptr, dL_dpix,
+                                    dL_dinvdepth_pix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepths, ts);
+                free(ts);
+            }
+        }
+        if (fail) return -1;
     } else {
 #pragma omp parallel for schedule(dynamic, 4)
         for (int t = 0; t < (int)T; t++)
             render_bwd_tile(st, (uint32_t)t % st->gx, (uint32_t)t / st->gx, bg, color_ptr, dL_dpix, dL_dinvdepth_pix,
-                            dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepths);
+                            dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepths, NULL);
     }
 
     const float* cov3D_ptr = cov3D_precomp ? cov3D_precomp : st->cov3D;

@@ -101,9 +101,12 @@ class OracleRaster:
                                  out.ctypes.data_as(ctypes.c_void_p))
         return out
 
-    def backward(self, dL_dcolor, dL_dinvdepth=None, f64=False):
+    def backward(self, dL_dcolor, dL_dinvdepth=None, f64=False, tile_sums=False):
         """f64: the render backward's arithmetic in float64 (gsr_oracle_set_bwd_f64) -- the
-        accuracy yardstick of tests/common.check_rel_truth, not the reference's float32 order."""
+        accuracy yardstick of tests/common.check_rel_truth, not the reference's float32 order.
+        tile_sums: each pixel's float32 terms summed per tile list entry first, then per Gaussian
+        (gsr_oracle_set_bwd_tile_sums) instead of one atomic add per term -- another order of the
+        same terms, several times faster on dense scenes (the training tests' oracle loops)."""
         a = self.args
         P, M = self.P, self.M
         g = dict(dL_dmean2D=np.zeros((P, 3), np.float32), dL_dconic=np.zeros((P, 2, 2), np.float32),
@@ -114,6 +117,7 @@ class OracleRaster:
         dc = _np(dL_dcolor)
         di = _np(dL_dinvdepth)
         lib().gsr_oracle_set_bwd_f64(ctypes.c_int(int(bool(f64))))
+        lib().gsr_oracle_set_bwd_tile_sums(ctypes.c_int(int(bool(tile_sums))))
         rc = lib().gsr_oracle_backward(
             ctypes.c_void_p(self.h), _p(a["bg"]), _p(a["means3D"]), _p(a["shs"]), _p(a["colors"]),
             _p(a["opacities"]), _p(a["scales"]), ctypes.c_float(self.scale_modifier), _p(a["rots"]),
@@ -123,6 +127,7 @@ class OracleRaster:
             _p(g["dL_dsh"]) if M else None, _p(g["dL_dscales"]), _p(g["dL_drotations"]),
             ctypes.c_int(self.nthreads))
         lib().gsr_oracle_set_bwd_f64(ctypes.c_int(0))
+        lib().gsr_oracle_set_bwd_tile_sums(ctypes.c_int(0))
         if rc != 0:
             raise RuntimeError("oracle backward failed")
         return g

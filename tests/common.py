@@ -124,6 +124,7 @@ REL_FLOOR = 1e-3
 REL_P999 = 1e-3
 REL_OUT = 1e-2
 REL_OUT_FRAC = 1e-4
+REL_LEFT_OUT_FRAC = 0.1  # check_rel: at most this share of the rows may be left out as decision suspects
 
 
 def rel_stats(hip, ref, floor=REL_FLOOR):
@@ -154,8 +155,12 @@ def check_rel(name, hip, ref, affected=None, truth_stats=None):
         ref = np.asarray(ref).reshape(len(keep), -1)[keep]
     st = rel_stats(hip, ref)
     bound = REL_P999 if truth_stats is None else max(REL_P999, (1 + TRUTH_FACTOR) * truth_stats["p999"] + TRUTH_SLACK)
-    PARITY_LOG.append({"name": name + " rel", "rows_left_out": 0 if affected is None else int((~keep).sum()),
-                       "p999_bound": bound, **st})
+    left_out = 0 if affected is None else int((~keep).sum())
+    PARITY_LOG.append({"name": name + " rel", "rows_left_out": left_out, "p999_bound": bound, **st})
+    # the rows left out (decision suspects' walks) stay a small share of the Gaussians (measured: at most
+    # 7.3 % on the chair fixture, whose 100k Gaussians are densely packed behind few pixels)
+    assert left_out <= REL_LEFT_OUT_FRAC * max(len(keep) if affected is not None else 0, 1), \
+        f"{name}: {left_out} rows left out of the per-element check"
     assert st["p999"] <= bound, f"{name}: 99.9th percentile relative error {st['p999']:.3e} > {bound:.3e} ({st})"
     assert st["n_over_REL_OUT"] <= max(2, REL_OUT_FRAC * st["considered"]), f"{name}: {st}"
     return st
@@ -206,6 +211,12 @@ def allclose_rel(a, b, rtol=GRAD_RTOL, atol=GRAD_ATOL):
 # element beyond GRAD_RTOL of max|ref| (or beyond REL_OUT relative to itself) must belong to such
 # a Gaussian; outside that set the plain tolerance holds, inside it GRAD_RTOL_ATTRIBUTED.
 GRAD_RTOL_ATTRIBUTED = 2e-3
+# and only a few of the attributed Gaussians may actually be off beyond GRAD_RTOL: at most
+# max(ATTR_ROWS_MIN, ATTR_ROWS_FRAC x the walks' Gaussians) rows (measured through round 4: at most
+# 16 rows of 17,250 for the 8-view sum, a ratio of at most 0.0018 per view), so a real regression
+# cannot hide among the thousands of Gaussians a handful of flipped pixels' walks pass
+ATTR_ROWS_MIN = 64
+ATTR_ROWS_FRAC = 0.01
 
 
 def flip_gaussians(flip, nc_hip, nc_ora, vals, ranges, W, H, P):
@@ -254,4 +265,6 @@ def check_grad_attributed(name, hip, ref, affected, rtol_attr=GRAD_RTOL_ATTRIBUT
         f"{name}: {st['unattributed_rows']} Gaussians off beyond tolerance outside every flipped pixel's walk "
         f"(rows {np.flatnonzero(unattr)[:8].tolist()}, {st})")
     assert st["max_rel_to_max_inside"] <= rtol_attr, f"{name}: attributed error too large ({st})"
+    assert st["attributed_rows"] <= max(ATTR_ROWS_MIN, ATTR_ROWS_FRAC * st["affected_gaussians"]), \
+        f"{name}: {st['attributed_rows']} attributed rows off beyond tolerance ({st})"
     return st

@@ -34,9 +34,37 @@ import synthetic  # noqa: E402
 
 SCENE = "/root/reference/nerf_synthetic/chair"
 FRAMES = (0, 1, 2)
-# (frame, sh_degree, antialiasing, background): iteration 1 of training renders at SH degree 0
-# (active_sh_degree starts at 0, train.py:95-96); one view at degree 3 with AA, one on white
-CASES = ((0, 0, False, (0.0, 0.0, 0.0)), (1, 3, True, (0.0, 0.0, 0.0)), (2, 0, False, (1.0, 1.0, 1.0)))
+# (frame, sh_degree, antialiasing, background, perturbed): iteration 1 of training renders at SH
+# degree 0 (active_sh_degree starts at 0, train.py:95-96); one view at degree 3 with AA, one on white.
+# create_from_pcd's identity rotations and isotropic scales make dL/drotations identically zero, so
+# cases 3 and 4 render the cloud with seeded random rotations and anisotropic scales (the fixture's
+# `rot_perturbed` / `scale_perturbed`): the cov3D -> (scale, rotation) chain of
+# backward.cu:330-393 on real geometry
+CASES = ((0, 0, False, (0.0, 0.0, 0.0), False), (1, 3, True, (0.0, 0.0, 0.0), False),
+         (2, 0, False, (1.0, 1.0, 1.0), False), (0, 3, False, (0.0, 0.0, 0.0), True),
+         (2, 0, True, (1.0, 1.0, 1.0), True))
+PERTURB_SEED = 7
+
+
+def perturbation(scale, seed=PERTURB_SEED):
+    """Seeded unit quaternions and per-axis scale factors exp(U(-0.7, 0.7)) around the isotropic
+    create_from_pcd scale (float64 math, stored as float32 in the fixture)."""
+    rng = np.random.default_rng(seed)
+    P = scale.shape[0]
+    q = rng.standard_normal((P, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    s = np.asarray(scale, np.float64)[:, None] * np.exp(rng.uniform(-0.7, 0.7, (P, 3)))
+    return q.astype(np.float32), s.astype(np.float32)
+
+
+def perturbed_scene(scene, f):
+    """The scene with the fixture's perturbed rotations and scales."""
+    out = dict(scene)
+    out["rotations"] = torch.from_numpy(np.ascontiguousarray(f["rot_perturbed"]))
+    out["scales"] = torch.from_numpy(np.ascontiguousarray(f["scale_perturbed"]))
+    return out
+
+
 GRAD_NAMES = ("dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
               "dL_drotations")
 
@@ -89,13 +117,15 @@ def main():
            "scale": scene["scales"][:, 0].numpy().copy(), "opacity": scene["opacities"][0, 0].numpy().copy(),
            "tanfovx": np.array([c.tanfovx for c in full], np.float32),
            "tanfovy": np.array([c.tanfovy for c in full], np.float32)}
-    for i, (frame, deg, aa, bg) in enumerate(CASES):
+    out["rot_perturbed"], out["scale_perturbed"] = perturbation(out["scale"])
+    pscene = perturbed_scene(scene, out)
+    for i, (frame, deg, aa, bg, pert) in enumerate(CASES):
         cam = full[frame]
-        o, g = run_case(scene, cam, deg, aa, bg, grad_seed=100 + i)
+        o, g = run_case(pscene if pert else scene, cam, deg, aa, bg, grad_seed=100 + i)
         for k, v in digests(o, g).items():
             out[f"case{i}_{k}"] = v
-        print(f"case {i}: frame {frame} deg {deg} aa {aa} bg {bg}: L={o.num_rendered} "
-              f"visible={(o.radii > 0).sum()}")
+        print(f"case {i}: frame {frame} deg {deg} aa {aa} bg {bg} perturbed {pert}: L={o.num_rendered} "
+              f"visible={(o.radii > 0).sum()} |dL/drot|={np.abs(g['dL_drotations']).sum():.4g}")
     np.savez_compressed(os.path.join(HERE, "chair", "nerf_chair.npz"), **out)
 
 

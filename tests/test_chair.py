@@ -27,13 +27,16 @@ class FixtureCamera:
 
 
 def load_chair():
-    """(fixture dict, activated Gaussians, [cases: (camera, sh_degree, antialiasing, bg, grad_seed)])."""
+    """(fixture dict, activated Gaussians, [cases: (camera, sh_degree, antialiasing, bg, grad_seed,
+    scene)]) -- each case's scene is the create_from_pcd cloud or, for the perturbed cases, that cloud
+    with the fixture's random rotations and anisotropic scales."""
     import make_chair
     f = dict(np.load(FIX))
     scene = ns.initial_gaussians(f["xyz"], f["rgb"], f["dist2"], scale=f["scale"], opacity=f["opacity"])
+    pscene = make_chair.perturbed_scene(scene, f)
     cases = []
-    for i, (frame, deg, aa, bg) in enumerate(make_chair.CASES):
-        cases.append((FixtureCamera(f, frame), deg, aa, bg, 100 + i))
+    for i, (frame, deg, aa, bg, pert) in enumerate(make_chair.CASES):
+        cases.append((FixtureCamera(f, frame), deg, aa, bg, 100 + i, pscene if pert else scene))
     return f, scene, cases
 
 
@@ -66,11 +69,25 @@ def test_chair_inputs():
         assert p[3] > 0 and abs(p[0] / p[3]) < 0.2 and abs(p[1] / p[3]) < 0.2
 
 
-@pytest.mark.parametrize("case", [0])
+def test_chair_perturbation():
+    """The perturbed cases' rotations are unit quaternions and their scales anisotropic around the
+    create_from_pcd scale (the stored arrays are the generator's, made in float64)."""
+    import make_chair
+    f, scene, cases = load_chair()
+    q, s = make_chair.perturbation(f["scale"])
+    np.testing.assert_allclose(f["rot_perturbed"], q, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(f["scale_perturbed"], s, rtol=1e-6)
+    np.testing.assert_allclose(np.linalg.norm(f["rot_perturbed"].astype(np.float64), axis=1), 1.0, atol=1e-6)
+    ratio = f["scale_perturbed"].max(1) / f["scale_perturbed"].min(1)
+    assert np.median(ratio) > 1.5
+    assert sum(c[5] is not scene for c in cases) == 2
+
+
+@pytest.mark.parametrize("case", [0, 3])
 def test_chair_oracle_reproduces_digests(case):
     import make_chair
     f, scene, cases = load_chair()
-    cam, deg, aa, bg, seed = cases[case]
+    cam, deg, aa, bg, seed, scene = cases[case]
     o, g = make_chair.run_case(scene, cam, deg, aa, bg, seed, nthreads=3)
     d = make_chair.digests(o, g)
     for k, v in d.items():

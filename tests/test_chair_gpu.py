@@ -39,12 +39,12 @@ def test_chair_distcuda2_bit_exact(chair):
     np.testing.assert_array_equal(d, f["dist2"])
 
 
-@pytest.mark.parametrize("case", [0, 1, 2])
+@pytest.mark.parametrize("case", [0, 1, 2, 3, 4])
 def test_chair_case(chair, case):
     import diff_gaussian_rasterization as dgr
     from test_gpu_parity import _img_state
-    f, scene, cases = chair
-    cam, deg, aa, bg, seed = cases[case]
+    f, _, cases = chair
+    cam, deg, aa, bg, seed, scene = cases[case]
     H, W, P = cam.image_height, cam.image_width, scene["means3D"].shape[0]
     o, og = make_chair.run_case(scene, cam, deg, aa, bg, seed, nthreads=min(16, os.cpu_count() or 1))
     d = make_chair.digests(o, og)

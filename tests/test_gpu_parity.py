@@ -251,16 +251,19 @@ def test_8k_view_three_pass_tile_sort():
     common.check_render("8k 3k", _hip_render(s, kw, color.cpu().numpy(), inv.cpu().numpy()), _ora_render(o))
 
 
-@pytest.mark.parametrize("H,W", [(256, 4080), (256, 4096), (4080, 256), (4096, 256)])
-def test_packed_rect_boundary_keys_bit_exact(H, W):
-    """The depth sort carries the tile rect packed into one word (a byte per bound) on grids of at
-    most 255 x 255 tiles and gathers the u16x4 rect by id above that: 255 and 256 tiles along
-    either axis (rect bounds up to 255 / 256) give keys, ids and ranges bit-identical to the oracle.
-    The backward too: render_bwd locates a record's mask bit from the packed rect in the render
-    record up to 255 tiles and from the Gaussian's first record slot above -- every gradient
-    against the oracle on both sides of the boundary."""
+@pytest.mark.parametrize("H,W,P", [(256, 4080, 3000), (256, 4096, 3000), (4080, 256, 3000), (4096, 256, 3000),
+                                   (256, 4080, 3001), (256, 4096, 3003), (256, 256, 1001), (256, 256, 3)])
+def test_packed_rect_boundary_keys_bit_exact(H, W, P):
+    """The 255 / 256-tile boundary: up to 255 x 255 tiles the depth sort carries the tile rect packed
+    into one word (a byte per bound) and the tile ranges come from the rects' 2-D difference array
+    (tile_hist + the tile-order prefix sums; the tile sort writes no tile ids); above it the depth
+    sort gathers the u16x4 rect by id and the ranges come from tile_ranges over the sorted tile ids.
+    255 and 256 tiles along either axis give keys, ids and ranges bit-identical to the oracle, and
+    every gradient matches it on both sides (render_bwd finds a record's mask bit from the
+    Gaussian's first record slot, emit_start, on both).  P not a multiple of 4 (3001, 3003, 1001,
+    3) covers tile_hist's tail, the last P mod 4 rects it adds outside its 16-B loads."""
     dgr = _dgr()
-    case = common.make_case(P=3000, H=H, W=W)
+    case = common.make_case(P=P, H=H, W=W)
     o, og = common.run_oracle(case, nthreads=8, backward=True)
     s = _settings(case)
     sc = {k: v.to(DEV) for k, v in case["scene"].items()}
