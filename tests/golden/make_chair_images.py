@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Generates tests/golden/chair/chair_images.npz: the NeRF-synthetic chair's training and test
-images at train.py's `-r 4` resolution (200 x 200) with their cameras, for the "PSNR vs ref"
-training test (tests/test_chair_train.py).
+"""Generates tests/golden/chair/chair_images.npz and chair_images_r2.npz: the NeRF-synthetic chair's
+training and test images at train.py's `-r 4` (200 x 200) and `-r 2` (400 x 400) resolutions with
+their cameras, for the "PSNR vs ref" training tests (tests/test_chair_train.py).
 
 What the reference does with a frame (restated, not imported):
 * scene/dataset_readers.py:228-271 readCamerasFromTransforms: R, T from `transform_matrix`
@@ -40,13 +40,13 @@ TRAIN = tuple(range(0, 100, 4))   # 25 of the 100 training frames
 TEST = tuple(range(0, 200, 25))   # 8 of the 200 test frames
 
 
-def frames(split, idx):
-    cams = ns.read_transforms(os.path.join(SCENE, f"transforms_{split}.json"), frames=set(idx), width=RES,
-                              height=RES)
+def frames(split, idx, res=RES):
+    cams = ns.read_transforms(os.path.join(SCENE, f"transforms_{split}.json"), frames=set(idx), width=res,
+                              height=res)
     imgs, full = [], []
     for R, T, fovx, fovy, w, h, path in cams:
         im = Image.open(os.path.join(SCENE, path + ".png"))
-        imgs.append(np.array(im.resize((RES, RES))))  # PILtoTorch's resize (default filter)
+        imgs.append(np.array(im.resize((res, res))))  # PILtoTorch's resize (default filter)
         full.append(ns.camera(R, T, fovx, fovy, w, h))
     return np.stack(imgs), full, [c[6] for c in cams]
 
@@ -67,10 +67,10 @@ def nerfpp_radius(split="train"):
     return float(np.max(np.linalg.norm(centers - center, axis=0)) * 1.1)
 
 
-def main():
-    out = {"extent": np.float64(nerfpp_radius()), "res": np.int32(RES)}
+def main(res=RES, name="chair_images.npz"):
+    out = {"extent": np.float64(nerfpp_radius()), "res": np.int32(res)}
     for split, idx in (("train", TRAIN), ("test", TEST)):
-        imgs, full, paths = frames(split, idx)
+        imgs, full, paths = frames(split, idx, res)
         out[f"{split}_rgba"] = imgs
         out[f"{split}_frames"] = np.array(idx, np.int32)
         out[f"{split}_paths"] = np.array(paths)
@@ -81,9 +81,10 @@ def main():
         print(split, imgs.shape, "alpha>0:", float((imgs[..., 3] > 0).mean()))
     with open(os.path.join(SCENE, "transforms_train.json")) as f:
         out["camera_angle_x"] = np.float64(json.load(f)["camera_angle_x"])
-    np.savez_compressed(os.path.join(HERE, "chair", "chair_images.npz"), **out)
+    np.savez_compressed(os.path.join(HERE, "chair", name), **out)
     print("extent", out["extent"])
 
 
 if __name__ == "__main__":
     main()
+    main(400, "chair_images_r2.npz")  # train.py -r 2: the longer HIP-only run (test_chair_train_py_hip_long)

@@ -48,7 +48,8 @@ pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
 HERE = os.path.dirname(os.path.abspath(__file__))
-IMAGES = os.path.join(HERE, "golden", "chair", "chair_images.npz")
+IMAGES = os.path.join(HERE, "golden", "chair", "chair_images.npz")        # -r 4: 200 x 200
+IMAGES_R2 = os.path.join(HERE, "golden", "chair", "chair_images_r2.npz")  # -r 2: 400 x 400
 CLOUD = os.path.join(HERE, "golden", "chair", "nerf_chair.npz")
 ITERS = 200
 SEED = 0
@@ -90,8 +91,8 @@ class View:
         self.H, self.W = self.original_image.shape[1:]
 
 
-def _load():
-    f = dict(np.load(IMAGES))
+def _load(images=IMAGES):
+    f = dict(np.load(images))
     c = dict(np.load(CLOUD))
     train = [View(f, "train", i) for i in range(len(f["train_frames"]))]
     test = [View(f, "test", i) for i in range(len(f["test_frames"]))]
@@ -264,19 +265,19 @@ def _hip_test_psnrs(dgr, act, test, sh_degree):
     return np.array(full), np.array(masked)
 
 
-LONG_ITERS = 3500
-REPORT_AT = (1000, 2000, 3000, 3500)
+LONG_ITERS = 7000  # train.py's first testing iteration (--test_iterations default 7000 30000)
+REPORT_AT = (1000, 3000, 5000, 7000)
 
 
 def test_chair_train_py_hip_long():
-    """train.py's loop on the HIP drop-ins past its first densifications, SH degree steps and opacity
-    reset (multiview.DataParallelTrainer in one process: train.py:93-186 with densify_and_prune every
-    100 iterations from 500, reset_opacity at 3000, oneupSHdegree every 1000): training_report's PSNR
+    """train.py's loop on the HIP drop-ins at `-r 2` (400 x 400) up to its first test iteration
+    (multiview.DataParallelTrainer in one process: train.py:93-186 with densify_and_prune every 100
+    iterations from 500, reset_opacity every 3000, oneupSHdegree every 1000): training_report's PSNR
     and the masked PSNR of the 8 test views at REPORT_AT go to the parity statistics.  No oracle loop
-    (it would take an hour on the host); asserted: the masked PSNR rises and the model grows."""
+    (hours on the host); asserted: the masked PSNR rises and densification changes the model."""
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import multiview
-    train, test, raw0, extent, P0 = _load()
+    train, test, raw0, extent, P0 = _load(IMAGES_R2)
     trainer = multiview.DataParallelTrainer({k: v.to(DEV) for k, v in raw0.items()}, optimizer="sparse_adam",
                                             spatial_lr_scale=extent, seed=SEED)
     views_by_degree = {d: [(_settings(dgr, v, d), v.original_image.to(DEV), {"alpha_mask": v.alpha_mask.to(DEV)})
@@ -296,7 +297,7 @@ def test_chair_train_py_hip_long():
                 f, m = _hip_test_psnrs(dgr, _activate(trainer.params), test, degree)
             report.append({"iteration": it, "P": int(trainer.P), "psnr": round(float(f.mean()), 4),
                            "masked_psnr": round(float(m.mean()), 4)})
-    stats = {"name": "chair train.py loop on the HIP drop-ins (8 test views, 200x200)", "P_start": P0,
+    stats = {"name": "chair train.py loop on the HIP drop-ins (8 test views, 400x400)", "P_start": P0,
              "psnr_start": round(float(f_start.mean()), 4), "masked_psnr_start": round(float(m_start.mean()), 4),
              "report": report}
     common.PARITY_LOG.append(stats)

@@ -54,7 +54,8 @@ def _settings(case, antialiasing):
 
 
 def _grad_check(name, hip, ref, affected, suspect_rows, truth=None):
-    common.check_grad_attributed(name, hip, ref, affected)
+    # outliers may sit in the walk of any decision suspect (common.DECISION_ATOL), not only of a flipped pixel
+    common.check_grad_attributed(name, hip, ref, suspect_rows)
     so = common.check_rel_truth(name, hip, ref, truth, suspect_rows)[1] if truth is not None else None
     # per element, not only relative to the max
     common.check_rel(name, hip, ref, suspect_rows, so)
