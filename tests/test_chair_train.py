@@ -11,9 +11,10 @@ and evaluates both on held-out test views with training_report's PSNR (train.py:
 utils/image_utils.py:17-19).
 
 What is restated from the reference (not imported):
-  * data: tests/golden/chair/chair_images.npz (make_chair_images.py): 25 training and 8 test frames
-    at `-r 4` (200 x 200), loaded as loadCam / Camera / PILtoTorch do: original_image = the RGB
-    channels of the resized RGBA frame, alpha_mask = its alpha (utils/camera_utils.py:20-66,
+  * data: tests/golden/chair/chair_frames.npz (make_chair_images.py): 25 training and 8 test frames
+    (the dataset's PNG files), loaded at `-r 4` (200 x 200) as loadCam / Camera / PILtoTorch do:
+    original_image = the RGB channels of the resized RGBA frame, alpha_mask = its alpha
+    (utils/camera_utils.py:20-66,
     scene/cameras.py:40-47); black background (ModelParams white_background default False);
   * initialisation: create_from_pcd on the dataset's points3d.ply (tests/golden/chair/
     nerf_chair.npz, gaussian_model.py:149-176): SH degree 3 stored, active degree 0 (it rises
@@ -48,10 +49,11 @@ pytestmark = pytest.mark.gpu
 
 DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
 HERE = os.path.dirname(os.path.abspath(__file__))
-IMAGES = os.path.join(HERE, "golden", "chair", "chair_images.npz")        # -r 4: 200 x 200
-IMAGES_R2 = os.path.join(HERE, "golden", "chair", "chair_images_r2.npz")  # -r 2: 400 x 400
+FRAMES = os.path.join(HERE, "golden", "chair", "chair_frames.npz")  # the dataset's PNG files + cameras
 CLOUD = os.path.join(HERE, "golden", "chair", "nerf_chair.npz")
 ITERS = 200
+RES = 200        # train.py -r 4 (the oracle loop's cost grows with the pixels)
+LONG_RES = 800   # the dataset's resolution (train.py's default -r for 800-pixel frames)
 SEED = 0
 SH_MAX, SH_ACTIVE = 3, 0
 PSNR_TOL_DB = 0.05
@@ -77,25 +79,31 @@ def get_expon_lr_func(lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, ma
 
 
 class View:
-    """A loaded camera: matrices from the fixture, original_image and alpha_mask as Camera has them."""
+    """A loaded camera (utils/camera_utils.py:20-66 loadCam at `-r 800 // res`, scene/cameras.py:40-47):
+    the matrices from the fixture; original_image and alpha_mask from PILtoTorch of the PNG frame
+    (utils/general_utils.py:21-27: PIL resize with its default filter, / 255)."""
 
-    def __init__(self, f, split, i):
+    def __init__(self, f, split, i, res):
+        import io
+        from PIL import Image
         self.world_view_transform = torch.from_numpy(f[f"{split}_viewmatrix"][i].copy())
         self.full_proj_transform = torch.from_numpy(f[f"{split}_projmatrix"][i].copy())
         self.camera_center = torch.from_numpy(f[f"{split}_campos"][i].copy())
         self.tanfovx, self.tanfovy = (float(x) for x in f[f"{split}_tanfov"][i])
-        rgba = torch.from_numpy(f[f"{split}_rgba"][i].copy()) / 255.0          # PILtoTorch
+        o = f[f"{split}_png_offsets"]
+        image = Image.open(io.BytesIO(f[f"{split}_png"][o[i]:o[i + 1]].tobytes()))
+        rgba = torch.from_numpy(np.array(image.resize((res, res)))) / 255.0  # PILtoTorch
         rgba = rgba.permute(2, 0, 1)
         self.original_image = rgba[:3].clamp(0.0, 1.0).contiguous()
         self.alpha_mask = rgba[3:4].contiguous()
         self.H, self.W = self.original_image.shape[1:]
 
 
-def _load(images=IMAGES):
-    f = dict(np.load(images))
+def _load(res):
+    f = dict(np.load(FRAMES))
     c = dict(np.load(CLOUD))
-    train = [View(f, "train", i) for i in range(len(f["train_frames"]))]
-    test = [View(f, "test", i) for i in range(len(f["test_frames"]))]
+    train = [View(f, "train", i, res) for i in range(len(f["train_frames"]))]
+    test = [View(f, "test", i, res) for i in range(len(f["test_frames"]))]
     # create_from_pcd (gaussian_model.py:149-176), raw (pre-activation) parameters; the activated
     # scale / opacity as stored in the cloud fixture, so both loops start from the same bits
     scene = ns.initial_gaussians(c["xyz"], c["rgb"], c["dist2"], scale=c["scale"], opacity=c["opacity"])
@@ -222,7 +230,7 @@ def _train_gpu(raw, train, extent, P):
 
 def test_chair_training_psnr_matches_oracle_loop():
     import diff_gaussian_rasterization as dgr
-    train, test, raw0, extent, P = _load()
+    train, test, raw0, extent, P = _load(RES)
     assert len(train) == 25 and len(test) == 8 and P == 100_000
     (f0, m0) = _test_psnrs(raw0, test)
     raw_cpu = _train_cpu(raw0, train, extent, P)
@@ -270,14 +278,14 @@ REPORT_AT = (1000, 3000, 5000, 7000)
 
 
 def test_chair_train_py_hip_long():
-    """train.py's loop on the HIP drop-ins at `-r 2` (400 x 400) up to its first test iteration
+    """train.py's loop on the HIP drop-ins at the frames' 800 x 800 up to its first test iteration
     (multiview.DataParallelTrainer in one process: train.py:93-186 with densify_and_prune every 100
     iterations from 500, reset_opacity every 3000, oneupSHdegree every 1000): training_report's PSNR
     and the masked PSNR of the 8 test views at REPORT_AT go to the parity statistics.  No oracle loop
     (hours on the host); asserted: the masked PSNR rises and densification changes the model."""
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import multiview
-    train, test, raw0, extent, P0 = _load(IMAGES_R2)
+    train, test, raw0, extent, P0 = _load(LONG_RES)
     trainer = multiview.DataParallelTrainer({k: v.to(DEV) for k, v in raw0.items()}, optimizer="sparse_adam",
                                             spatial_lr_scale=extent, seed=SEED)
     views_by_degree = {d: [(_settings(dgr, v, d), v.original_image.to(DEV), {"alpha_mask": v.alpha_mask.to(DEV)})
@@ -297,7 +305,7 @@ def test_chair_train_py_hip_long():
                 f, m = _hip_test_psnrs(dgr, _activate(trainer.params), test, degree)
             report.append({"iteration": it, "P": int(trainer.P), "psnr": round(float(f.mean()), 4),
                            "masked_psnr": round(float(m.mean()), 4)})
-    stats = {"name": "chair train.py loop on the HIP drop-ins (8 test views, 400x400)", "P_start": P0,
+    stats = {"name": "chair train.py loop on the HIP drop-ins (8 test views, 800x800)", "P_start": P0,
              "psnr_start": round(float(f_start.mean()), 4), "masked_psnr_start": round(float(m_start.mean()), 4),
              "report": report}
     common.PARITY_LOG.append(stats)
