@@ -30,10 +30,12 @@
 namespace gsr {
 
 constexpr int RS_THREADS = 256;
+constexpr int RS_THREADS_WIDE = 512;            // 9-bit passes: 4,096-key chunks
 constexpr int RS_ITEMS = 8;                     // elements per thread, long sorts (the tile sort; 16: -20 % slower)
 constexpr int RS_ITEMS_SHORT = 8;               // short sorts (the depth sort; 4 measures the same)
 constexpr int RS_SHORT_MAX = 1 << 21;           // n up to which a sort counts as short
 constexpr int RS_MAXBINS = 256;
+constexpr int RS_SCRATCH_BINS = 512;            // count-matrix rows reserved per sort (9-bit depth digits)
 
 // Kernel-name tags: which sort a radix pass belongs to (the depth sort, the tile sort's later
 // passes, distCUDA2's cell sort) -- the kernels are identical, the names let a profile (rocprofv3
@@ -44,7 +46,58 @@ struct CellSort;
 
 __device__ __forceinline__ uint32_t digit_of(uint32_t k, int shift, uint32_t mask) { return (k >> shift) & mask; }
 
-// (1) counts[d * nchunks + c] = number of elements of chunk c with digit d (view blockIdx.y).
+// The count matrix of a pass: chunk-major, counts[c * nb + d] (cmaj: each chunk's counts are one
+// contiguous write of the count kernel and one contiguous read of the scatter kernel, and the scan
+// over the chunks reads 16 digits = 64 B per chunk row -- for passes of at most CS_CHUNKS chunks, which
+// one LDS block of radix_colscan_kernel scans: the depth sort), or digit-major counts[d * nchunks + c]
+// (one row-scan workgroup per digit: the tile sort's thousands of chunks).
+#ifndef GSR_COLSCAN
+#define GSR_COLSCAN 1
+#endif
+__device__ __forceinline__ size_t cm_index(uint32_t d, uint32_t c, uint32_t nb, uint32_t nchunks, bool cmaj)
+{
+    return cmaj ? (size_t)c * nb + d : (size_t)d * nchunks + c;
+}
+
+// The depth sort in three 9-bit passes (depth_sort_passes): passes 1 and 2 take key bits [0, 9) and
+// [9, 18); pass 3 takes bits [18, 32) RELATIVE to the smallest key that is not 0xFFFFFFFF (culled):
+// digit = (k >> 18) - (min >> 18), and 511 for 0xFFFFFFFF.  That is monotone in k, so the three passes
+// sort exactly, whenever the keys other than 0xFFFFFFFF span at most 511 values of k >> 18 (visible
+// depths within a factor of ~2^16: 0.2 ... 13,000).  Pass 1 gathers the range (per-chunk min / max,
+// reduced by an extra workgroup of its row scan into RangeWord); a wider range makes pass 3 take raw
+// bits [18, 27) and a fourth 5-bit pass on bits [27, 32) run -- the fourth pass's kernels exit at once
+// otherwise, and pass 3 is then the last pass (it writes the final arrays).
+// mode: DIG_RAW (k >> shift) & mask; DIG_REL (the relative digit above when the range fits, else raw);
+// DIG_SKIP (the kernels exit when the range fits).
+enum DigitMode { DIG_RAW = 0, DIG_REL = 1, DIG_SKIP = 2 };
+struct RangeWord { uint32_t base, fits; };  // min >> rel_shift of the keys other than 0xFFFFFFFF; range fits
+struct Digit {
+    int shift;
+    uint32_t mask;
+    bool rel;
+    uint32_t base;
+    __device__ __forceinline__ uint32_t operator()(uint32_t k) const
+    {
+        return rel ? (k == 0xFFFFFFFFu ? mask : (k >> shift) - base) : (k >> shift) & mask;
+    }
+};
+// (mode, range) -> the digit function of a pass; *skip: a DIG_SKIP pass whose range fits
+__device__ __forceinline__ Digit make_digit(int shift, int nbits, int mode, const RangeWord* range, bool* skip)
+{
+    Digit d{shift, (1u << nbits) - 1u, false, 0u};
+    *skip = false;
+    if (mode != DIG_RAW) {
+        const uint32_t fits = __builtin_amdgcn_readfirstlane(range->fits);
+        if (mode == DIG_REL && fits) {
+            d.rel = true;
+            d.base = __builtin_amdgcn_readfirstlane(range->base);
+        }
+        *skip = mode == DIG_SKIP && fits;
+    }
+    return d;
+}
+
+// (1) counts[cm_index(d, c)] = number of elements of chunk c with digit d (view blockIdx.y).
 struct CountJob {
     const uint32_t* keys;
     int n, nchunks;
@@ -53,41 +106,76 @@ struct CountJob {
     // the top bits of the id word, see TileSortJob)
     const uint2* pairs_hi;
     int hi_shift;
+    int mode;                  // DigitMode
+    const RangeWord* range;    // (DIG_REL / DIG_SKIP)
+    uint32_t* cmin;            // non-null: per-chunk min / max of the keys other than 0xFFFFFFFF
+    uint32_t* cmax;
+    bool cmaj;                 // chunk-major count matrix (cm_index)
 };
-template <int ITEMS, typename KIND>
-__global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
+template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS>
+__global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
     const CountJob& J = B.v[blockIdx.y];
     if ((int)blockIdx.x >= J.nchunks) return;  // past this view's chunks (uniform)
+    bool skip;
+    const Digit dig = make_digit(shift, nbits, J.mode, J.range, &skip);
+    if (skip) return;
     const uint32_t* keys = J.keys;
     const int n = J.n;
-    __shared__ uint32_t h[4][RS_MAXBINS];
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t h[NW][MAXB];
+    __shared__ uint32_t s_mm[2][NW];
     const int tid = threadIdx.x, w = tid >> 6;
-    const uint32_t nb = 1u << nbits, mask = nb - 1u;
-    for (int q = 0; q < 4; q++) h[q][tid] = 0;
+    const uint32_t nb = 1u << nbits;
+    for (int q = 0; q < NW; q++)
+        for (int d = tid; d < MAXB; d += NT) h[q][d] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * (RS_THREADS * ITEMS);
+    const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
     uint32_t k[ITEMS];
+    // the range of the keys other than 0xFFFFFFFF (the depth sort's first pass; `full`: every k[i]
+    // is a key of this chunk, else the ones at an index < n)
+    auto chunk_range = [&](bool full) {
+        if (!J.cmin) return;
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            const bool in = full || base + (size_t)i * NT + tid < (size_t)n;
+            if (in && k[i] != 0xFFFFFFFFu) {
+                mn = min(mn, k[i]);
+                mx = max(mx, k[i]);
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+        }
+        if ((tid & 63) == 0) {
+            s_mm[0][w] = mn;
+            s_mm[1][w] = mx;
+        }
+    };
     if (!keys) {  // keys in the pairs' high bits (8-B loads; the slot word rides along unused)
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) k[i] = J.pairs_hi[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)].y >> J.hi_shift;
+        for (int i = 0; i < ITEMS; i++) k[i] = J.pairs_hi[min(base + (size_t)i * NT + tid, (size_t)n - 1)].y >> J.hi_shift;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++)
-            if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
-    } else if (base + RS_THREADS * ITEMS <= (size_t)n && ((uintptr_t)keys & 15) == 0 && ITEMS % 4 == 0) {
+            if (base + (size_t)i * NT + tid < (size_t)n) atomicAdd(&h[w][dig(k[i])], 1u);
+    } else if (base + NT * ITEMS <= (size_t)n && ((uintptr_t)keys & 15) == 0 && ITEMS % 4 == 0) {
         // full chunk: 16-byte loads (a histogram does not care which thread counts which key)
         const uint4* k4 = reinterpret_cast<const uint4*>(keys + base);
 #pragma unroll
         for (int j = 0; j < ITEMS / 4; j++) {
-            const uint4 q = k4[j * RS_THREADS + tid];
+            const uint4 q = k4[j * NT + tid];
             k[4 * j] = q.x; k[4 * j + 1] = q.y; k[4 * j + 2] = q.z; k[4 * j + 3] = q.w;
         }
+        chunk_range(true);
         // a wave whose 64 keys share one digit (the depth keys' top byte, mostly) adds once: 64
         // same-address LDS atomics would serialise
         const int lane = tid & 63;
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
-            const uint32_t d = digit_of(k[i], shift, mask);
+            const uint32_t d = dig(k[i]);
             const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
             if (__all(d == d0)) {
                 if (lane == 0) atomicAdd(&h[w][d0], 64u);
@@ -97,14 +185,28 @@ __global__ void __launch_bounds__(RS_THREADS) radix_count_kernel(const ViewBatch
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * RS_THREADS + tid, (size_t)n - 1)];
+        for (int i = 0; i < ITEMS; i++) k[i] = keys[min(base + (size_t)i * NT + tid, (size_t)n - 1)];
+        chunk_range(false);
 #pragma unroll
         for (int i = 0; i < ITEMS; i++)
-            if (base + (size_t)i * RS_THREADS + tid < (size_t)n) atomicAdd(&h[w][digit_of(k[i], shift, mask)], 1u);
+            if (base + (size_t)i * NT + tid < (size_t)n) atomicAdd(&h[w][dig(k[i])], 1u);
     }
     __syncthreads();
-    if ((uint32_t)tid < nb)
-        J.counts[(size_t)tid * J.nchunks + blockIdx.x] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    for (uint32_t d = tid; d < nb; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < NW; q++) c += h[q][d];
+        J.counts[cm_index(d, blockIdx.x, nb, J.nchunks, J.cmaj)] = c;
+    }
+    if (J.cmin && tid == 0) {
+        uint32_t mn = s_mm[0][0], mx = s_mm[1][0];
+        for (int q = 1; q < NW; q++) {
+            mn = min(mn, s_mm[0][q]);
+            mx = max(mx, s_mm[1][q]);
+        }
+        J.cmin[blockIdx.x] = mn;
+        J.cmax[blockIdx.x] = mx;
+    }
 }
 
 // (2) one workgroup per digit: exclusive scan of counts[d, 0..nchunks) in place; the row total
@@ -113,13 +215,62 @@ struct RowJob {
     uint32_t* counts;
     int nchunks;
     uint32_t* totals;
+    int mode;                  // DIG_SKIP: exit when the range fits
+    const RangeWord* range;
+    // non-null (the depth sort's first pass): workgroup `nbins` (one past the digit rows) reduces the
+    // per-chunk min / max into *range_out for a relative pass on bits [rel_shift, rel_shift + rel_bits)
+    const uint32_t* cmin;
+    const uint32_t* cmax;
+    RangeWord* range_out;
+    int nbins, rel_shift, rel_bits;
 };
+// the extra workgroup of a row scan: the keys' range from the per-chunk min / max (RowJob)
+__device__ void reduce_range(const RowJob& J)
+{
+    __shared__ uint32_t s_mm[2][4];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (int c = tid; c < J.nchunks; c += RS_THREADS) {
+        mn = min(mn, J.cmin[c]);
+        mx = max(mx, J.cmax[c]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    }
+    if (lane == 0) {
+        s_mm[0][w] = mn;
+        s_mm[1][w] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        mn = min(min(s_mm[0][0], s_mm[0][1]), min(s_mm[0][2], s_mm[0][3]));
+        mx = max(max(s_mm[1][0], s_mm[1][1]), max(s_mm[1][2], s_mm[1][3]));
+        RangeWord r;
+        if (mn > mx) {  // nothing but 0xFFFFFFFF
+            r.base = 0u;
+            r.fits = 1u;
+        } else {
+            r.base = mn >> J.rel_shift;
+            // the largest relative digit stays below 2^rel_bits - 1, the digit of 0xFFFFFFFF
+            r.fits = ((mx >> J.rel_shift) - r.base) <= (1u << J.rel_bits) - 2u ? 1u : 0u;
+        }
+        *J.range_out = r;
+    }
+}
 template <typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBatch<RowJob> B)
 {
-    uint32_t* counts = B.v[blockIdx.y].counts;
-    const int nchunks = B.v[blockIdx.y].nchunks;
-    uint32_t* totals = B.v[blockIdx.y].totals;
+    const RowJob& J = B.v[blockIdx.y];
+    if (J.cmin && (int)blockIdx.x == J.nbins) {
+        reduce_range(J);
+        return;
+    }
+    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
+    uint32_t* counts = J.counts;
+    const int nchunks = J.nchunks;
+    uint32_t* totals = J.totals;
     __shared__ uint32_t s_wave[4];
     __shared__ uint32_t s_carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -155,9 +306,15 @@ constexpr int RS_ROW_LDS = 12288;
 template <typename KIND>
 __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const ViewBatch<RowJob> RB)
 {
-    uint32_t* counts = RB.v[blockIdx.y].counts;
-    const int nchunks = RB.v[blockIdx.y].nchunks;
-    uint32_t* totals = RB.v[blockIdx.y].totals;
+    const RowJob& J = RB.v[blockIdx.y];
+    if (J.cmin && (int)blockIdx.x == J.nbins) {
+        reduce_range(J);
+        return;
+    }
+    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
+    uint32_t* counts = J.counts;
+    const int nchunks = J.nchunks;
+    uint32_t* totals = J.totals;
     __shared__ uint32_t s_row[RS_ROW_LDS];
     __shared__ uint32_t s_wave[4];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -201,6 +358,78 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const Vie
     for (int c = tid; c < nchunks; c += RS_THREADS) row[c] = s_row[c];
 }
 
+// (2') GSR_COLSCAN: the exclusive scan over the chunks of each digit's counts, on the chunk-major
+// matrix: workgroup g takes digits [16 g, 16 g + 16); thread (dl = tid >> 4, sg = tid & 15) scans a
+// contiguous segment of chunks of digit 16 g + dl; blocks of CS_CHUNKS chunks are staged in LDS with
+// every load in flight (16 digits = 64 contiguous bytes per chunk row), each digit's running total
+// carried from block to block.  Workgroup ceil(nbins / 16) (the depth sort's first pass) reduces the
+// keys' range instead.
+constexpr int CS_DIG = 16;
+constexpr int CS_CHUNKS = 960;  // chunks per LDS block (960 x 17 words = 64 KB)
+template <typename KIND>
+__global__ void __launch_bounds__(RS_THREADS) radix_colscan_kernel(const ViewBatch<RowJob> B)
+{
+    const RowJob& J = B.v[blockIdx.y];
+    const int ngroups = (J.nbins + CS_DIG - 1) / CS_DIG;
+    if (J.cmin && (int)blockIdx.x == ngroups) {
+        reduce_range(J);
+        return;
+    }
+    if ((int)blockIdx.x >= ngroups) return;
+    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
+    __shared__ uint32_t s_col[CS_CHUNKS * (CS_DIG + 1)];  // [chunk][digit], rows padded to 17 words
+    const int tid = threadIdx.x, dl = tid >> 4, sg = tid & 15;
+    const uint32_t nb = (uint32_t)J.nbins, nchunks = (uint32_t)J.nchunks;
+    const uint32_t d0 = blockIdx.x * CS_DIG;
+    const uint32_t nd = min((uint32_t)CS_DIG, nb - d0);
+    uint32_t* counts = J.counts;
+    uint32_t carry = 0;  // this thread's digit (sg == 15 keeps the column total)
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += CS_CHUNKS) {
+        const uint32_t nc = min((uint32_t)CS_CHUNKS, nchunks - c0);
+        constexpr int U = 8;
+        for (uint32_t i0 = tid; i0 < nc * CS_DIG; i0 += U * RS_THREADS) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t i = i0 + u * RS_THREADS, c = i >> 4, dd = i & 15;
+                v[u] = (i < nc * CS_DIG && dd < nd) ? counts[(size_t)(c0 + c) * nb + d0 + dd] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t i = i0 + u * RS_THREADS;
+                if (i < nc * CS_DIG) s_col[(i >> 4) * (CS_DIG + 1) + (i & 15)] = v[u];
+            }
+        }
+        __syncthreads();
+        // segment scan: 16 segments of ceil(nc / 16) chunks per digit
+        const uint32_t seg = (nc + 15) / 16;
+        const uint32_t j0 = min(sg * seg, nc), j1 = min(j0 + seg, nc);
+        uint32_t sum = 0;
+        for (uint32_t j = j0; j < j1; j++) sum += s_col[j * (CS_DIG + 1) + dl];
+        uint32_t x = sum;  // inclusive scan over the 16 segments of this digit (lanes 16 dl' .. 16 dl' + 15)
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 16);
+            if (sg >= o) x += y;
+        }
+        const uint32_t block_total = (uint32_t)__shfl((int)x, 15, 16);
+        uint32_t run = carry + x - sum;
+        for (uint32_t j = j0; j < j1; j++) {
+            const uint32_t c = s_col[j * (CS_DIG + 1) + dl];
+            s_col[j * (CS_DIG + 1) + dl] = run;
+            run += c;
+        }
+        carry += block_total;
+        __syncthreads();
+        for (uint32_t i = tid; i < nc * CS_DIG; i += RS_THREADS) {
+            const uint32_t c = i >> 4, dd = i & 15;
+            if (dd < nd) counts[(size_t)(c0 + c) * nb + d0 + dd] = s_col[c * (CS_DIG + 1) + dd];
+        }
+        __syncthreads();  // s_col reuse
+    }
+    if (sg == 0 && (uint32_t)dl < nd) J.totals[d0 + dl] = carry;
+}
+
 struct SortPassArgs {
     int n, shift, nbits, nchunks;
     const uint32_t* keys_in;
@@ -224,11 +453,15 @@ struct SortPassArgs {
     // PAIR, > 0: there is no key array; the key is vals_in[i].y >> key_hi_shift and out_y receives
     // v.y with those bits cleared (the tile sort's second pass, see TileSortJob)
     int key_hi_shift;
+    int mode;                // DigitMode (a DIG_REL pass with both the ping-pong and the final outputs
+    const RangeWord* range;  // set is the last pass when the range fits)
+    bool cmaj;               // chunk-major count matrix (cm_index)
 };
 
 // Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
 // one barrier to add the preceding waves' totals (s4: 4 words, not reused before a later barrier).
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
+template <int WAVES>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sw)
 {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     uint32_t x = v;
@@ -237,36 +470,64 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
         const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
         if (lane >= d) x += y;
     }
-    if (lane == 63) s4[w] = x;
+    if (lane == 63) sw[w] = x;
     __syncthreads();
     uint32_t pre = x - v;
-    for (int q = 0; q < w; q++) pre += s4[q];
+    for (int q = 0; q < w; q++) pre += sw[q];
     return pre;
 }
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4) { return block_excl_scan<4>(v, s4); }
 
-// (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.
-template <int ITEMS, bool PAIR, typename KIND, int NBITS>
-__global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
+// (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.  NBITS <= 9: up to
+// 512 digits (two per thread in the digit-indexed steps).
+template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS>
+__global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
     if ((int)blockIdx.x >= a.nchunks) return;  // past this view's chunks (uniform)
-    constexpr int TILE = RS_THREADS * ITEMS;
+    bool skip;
+    const Digit dig = make_digit(a.shift, NBITS, a.mode, a.range, &skip);
+    if (skip) return;
+    // the pass writes the final arrays: no ping-pong output, or a relative pass whose range fits
+    const bool is_last = a.keys_out == nullptr || dig.rel;
+    constexpr int TILE = NT * ITEMS;
+    constexpr int NB = 1 << NBITS;
+    constexpr int NBA = NB < NT ? NT : NB;  // digit-indexed arrays: at least one per thread
+    constexpr int DPT = NBA / NT;                     // digits per thread (1 or 2)
+    static_assert(NB <= 2 * NT, "at most 9-bit digits");
     using Val = typename std::conditional<PAIR, uint2, uint32_t>::type;
-    __shared__ uint32_t s_cnt[4][RS_MAXBINS];  // per-wave running digit counts, then per-wave prefixes
-    __shared__ uint32_t s_blk[RS_MAXBINS];     // block-local start of each digit
-    __shared__ uint32_t s_base[RS_MAXBINS];    // global start of each digit for this chunk
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t s_cnt[NW][NBA];  // per-wave running digit counts, then per-wave prefixes
+    __shared__ uint32_t s_blk[NBA];     // block-local start of each digit
+    __shared__ uint32_t s_base[NBA];    // global start of each digit for this chunk
     __shared__ uint32_t s_keys[TILE];
     __shared__ Val s_vals[TILE];
-    __shared__ uint32_t s_w0[4], s_w1[4];      // wave totals of the two block scans
+    __shared__ uint32_t s_w0[NW], s_w1[NW];    // wave totals of the two block scans
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t nb = 1u << NBITS, mask = nb - 1u;  // the digit width (== a.nbits): unrolled ranking
     const uint32_t chunk = blockIdx.x;
-    for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
-    // digit offsets: exclusive scan of the totals (in s_base), plus this chunk's row prefix
-    const uint32_t tot = (uint32_t)tid < nb ? a.totals[tid] : 0u;
-    const uint32_t rowp = (uint32_t)tid < nb ? a.row_prefix[(size_t)tid * a.nchunks + chunk] : 0u;
-    const uint32_t gbase = block_excl_scan256(tot, s_w0) + rowp;  // its barrier also publishes s_cnt = 0
+#pragma unroll
+    for (int i = 0; i < DPT; i++)
+        for (int q = 0; q < NW; q++) s_cnt[q][tid * DPT + i] = 0;
+    // digit offsets: exclusive scan of the totals, plus this chunk's row prefix (thread t owns digits
+    // [t DPT, t DPT + DPT))
+    uint32_t tot[DPT], rowp[DPT], tsum = 0;
+#pragma unroll
+    for (int i = 0; i < DPT; i++) {
+        const uint32_t d = (uint32_t)(tid * DPT + i);
+        tot[i] = d < (uint32_t)NB ? a.totals[d] : 0u;
+        rowp[i] = d < (uint32_t)NB ? a.row_prefix[cm_index(d, chunk, NB, a.nchunks, a.cmaj)] : 0u;
+        tsum += tot[i];
+    }
+    uint32_t gbase[DPT];
+    {
+        uint32_t run = block_excl_scan<NW>(tsum, s_w0);  // its barrier also publishes s_cnt = 0
+#pragma unroll
+        for (int i = 0; i < DPT; i++) {
+            gbase[i] = run + rowp[i];
+            run += tot[i];
+        }
+    }
 
     const size_t base = (size_t)chunk * TILE;
     const int nvalid = (int)min((size_t)TILE, (size_t)a.n - base);
@@ -305,7 +566,7 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     for (int i = 0; i < ITEMS; i++) {
         const int li = w * (ITEMS * 64) + i * 64 + lane;
         const bool valid = li < nvalid;
-        const uint32_t d = digit_of(key[i], a.shift, mask);
+        const uint32_t d = dig(key[i]);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < NBITS; b++) {
@@ -321,22 +582,36 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     __syncthreads();
 
     // per-digit block totals, per-wave exclusive prefixes, block-local digit starts
-    const uint32_t c0 = s_cnt[0][tid], c1 = s_cnt[1][tid], c2 = s_cnt[2][tid], c3 = s_cnt[3][tid];
-    const uint32_t total = c0 + c1 + c2 + c3;
-    s_cnt[0][tid] = 0;
-    s_cnt[1][tid] = c0;
-    s_cnt[2][tid] = c0 + c1;
-    s_cnt[3][tid] = c0 + c1 + c2;
-    const uint32_t blk_start = block_excl_scan256(total, s_w1);
-    s_blk[tid] = blk_start;
-    s_base[tid] = gbase;
+    uint32_t dtot[DPT], bsum = 0;
+#pragma unroll
+    for (int i = 0; i < DPT; i++) {
+        const int d = tid * DPT + i;
+        uint32_t run = 0;
+#pragma unroll
+        for (int q = 0; q < NW; q++) {  // per-wave exclusive prefixes of the digit
+            const uint32_t c = s_cnt[q][d];
+            s_cnt[q][d] = run;
+            run += c;
+        }
+        dtot[i] = run;
+        bsum += run;
+    }
+    {
+        uint32_t run = block_excl_scan<NW>(bsum, s_w1);
+#pragma unroll
+        for (int i = 0; i < DPT; i++) {
+            s_blk[tid * DPT + i] = run;
+            s_base[tid * DPT + i] = gbase[i];
+            run += dtot[i];
+        }
+    }
     __syncthreads();
 
     // scatter into LDS in block-local sorted (stable) order
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) {
         if (rank[i] != 0xFFFFFFFFu) {
-            const uint32_t d = digit_of(key[i], a.shift, mask);
+            const uint32_t d = dig(key[i]);
             const uint32_t lpos = s_blk[d] + s_cnt[w][d] + rank[i];
             s_keys[lpos] = key[i];
             s_vals[lpos] = val[i];
@@ -346,13 +621,13 @@ __global__ void __launch_bounds__(RS_THREADS) radix_scatter_kernel(const ViewBat
     // contiguous write-out: runs of one digit map to consecutive global addresses
 #pragma unroll
     for (int i = 0; i < ITEMS; i++) {
-        const int lpos = i * RS_THREADS + tid;
+        const int lpos = i * NT + tid;
         if (lpos < nvalid) {
             const uint32_t k = s_keys[lpos];
-            const uint32_t d = digit_of(k, a.shift, mask);
+            const uint32_t d = dig(k);
             const uint32_t dst = s_base[d] + ((uint32_t)lpos - s_blk[d]);
             const Val v = s_vals[lpos];
-            if (a.keys_out) {
+            if (!is_last) {
                 a.keys_out[dst] = k;
                 reinterpret_cast<Val*>(a.vals_out)[dst] = v;
             } else {
@@ -523,7 +798,7 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_count_kernel(const Vie
         }
     }
     __syncthreads();
-    if ((uint32_t)tid < nb) J.counts[(size_t)tid * J.nchunks + c] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
+    if ((uint32_t)tid < nb) J.counts[cm_index(tid, c, nb, J.nchunks, false)] = h[0][tid] + h[1][tid] + h[2][tid] + h[3][tid];
 }
 
 template <int ITEMS, int NBITS>
@@ -546,7 +821,7 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     const uint32_t nb = 1u << nbits, mask = nb - 1u;
     for (int q = 0; q < 4; q++) s_cnt[q][tid] = 0;
     const uint32_t tot = (uint32_t)tid < nb ? J.totals[tid] : 0u;
-    const uint32_t rowp = (uint32_t)tid < nb ? J.counts[(size_t)tid * J.nchunks + c] : 0u;
+    const uint32_t rowp = (uint32_t)tid < nb ? J.counts[cm_index(tid, c, nb, J.nchunks, false)] : 0u;
     const uint32_t gbase = block_excl_scan256(tot, s_w0) + rowp;
     s_base[tid] = gbase;
     reinterpret_cast<uint64_t*>(s_own)[tid] = 0ull;  // the first round's owner marks start from zero
@@ -790,17 +1065,21 @@ __global__ void __launch_bounds__(256) debug_keys_kernel(int L, const uint32_t* 
 }
 
 static inline int rs_items(int n) { return n <= RS_SHORT_MAX ? RS_ITEMS_SHORT : RS_ITEMS; }
+static inline size_t rs_chunks_tile(int n, int tile) { return ((size_t)(n > 0 ? n : 0) + tile - 1) / tile; }
 static inline size_t rs_chunks(int n)
 {
     const size_t tile = (size_t)RS_THREADS * rs_items(n);
     return ((size_t)(n > 0 ? n : 0) + tile - 1) / tile;
 }
 
-// Scratch of one sort: the (bins x chunks) count matrix and the bin totals (reused by every pass).
+// Scratch of one sort: the (bins x chunks) count matrix and the bin totals (reused by every pass),
+// then the per-chunk key min / max and the RangeWord of a three-pass depth sort.
+static inline size_t rs_count_bytes(int n) { return align_up(rs_chunks(n) * RS_SCRATCH_BINS * 4 + 256, 256); }
+static inline size_t rs_totals_bytes() { return align_up(RS_SCRATCH_BINS * 4, 256); }
 size_t radix_status_bytes(int n, int npass)
 {
     (void)npass;
-    return align_up(rs_chunks(n) * RS_MAXBINS * 4 + 256, 256) + align_up(RS_MAXBINS * 4, 256);
+    return rs_count_bytes(n) + rs_totals_bytes() + align_up(2 * rs_chunks(n) * 4 + 64, 256);
 }
 static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 2048 && RS_MAXBINS == 256,
               "2,048-key chunks");
@@ -825,14 +1104,53 @@ static hipError_t for_groups(int V, F f)
 static inline uint32_t* sort_counts(const SortJob& j) { return reinterpret_cast<uint32_t*>(j.scratch); }
 static inline uint32_t* sort_totals(const SortJob& j)
 {
-    return reinterpret_cast<uint32_t*>(j.scratch + align_up(rs_chunks(j.n) * RS_MAXBINS * 4 + 256, 256));
+    return reinterpret_cast<uint32_t*>(j.scratch + rs_count_bytes(j.n));
 }
+// per-chunk min (nchunks words), max (nchunks words), then the RangeWord (8-B aligned)
+static inline uint32_t* sort_minmax(const SortJob& j)
+{
+    return reinterpret_cast<uint32_t*>(j.scratch + rs_count_bytes(j.n) + rs_totals_bytes());
+}
+static inline RangeWord* sort_range(const SortJob& j)
+{
+    return reinterpret_cast<RangeWord*>(sort_minmax(j) + 2 * ((rs_chunks(j.n) + 1) & ~(size_t)1));
+}
+
+// (2) for a pass of nbins digits over (up to) maxc chunks: the per-digit exclusive scans over the
+// chunks and the digit totals (+ the range workgroup)
+static inline bool chunk_major(int maxc) { return GSR_COLSCAN && maxc <= CS_CHUNKS; }
+template <typename KIND>
+static void launch_scan_rows(const ViewBatch<RowJob>& rb, int nv, int nbins, int maxc, bool range, hipStream_t s)
+{
+    const dim3 b(RS_THREADS);
+    if (chunk_major(maxc)) {
+        const dim3 g((unsigned)((nbins + CS_DIG - 1) / CS_DIG + (range ? 1 : 0)), (unsigned)nv);
+        hipLaunchKernelGGL(radix_colscan_kernel<KIND>, g, b, 0, s, rb);
+        return;
+    }
+    const dim3 g((unsigned)(nbins + (range ? 1 : 0)), (unsigned)nv);
+    if (maxc <= RS_ROW_LDS)
+        hipLaunchKernelGGL(radix_rowscan_lds_kernel<KIND>, g, b, 0, s, rb);
+    else
+        hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, g, b, 0, s, rb);
+}
+
+// One radix pass of a sort: digit width, key shift, DigitMode.
+struct PassSpec { int w, shift, mode; };
+// The full 32-bit key sorts (the depth sort) in three 9-bit passes, the third relative to the keys'
+// minimum, plus a 5-bit fourth pass that runs only when the keys' range is too wide (DigitMode).
+constexpr int DEPTH3_PASSES = 4;
+constexpr PassSpec DEPTH3[DEPTH3_PASSES] = {{9, 0, DIG_RAW}, {9, 9, DIG_RAW}, {9, 18, DIG_REL}, {5, 27, DIG_SKIP}};
+#ifndef GSR_DEPTH3
+#define GSR_DEPTH3 1
+#endif
 
 template <typename KIND>
 static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
 {
     if (nbits < 1) nbits = 1;
-    const int npass = (nbits + 7) / 8;
+    const bool depth3 = GSR_DEPTH3 && nbits == 32 && shift0 == 0 && std::is_same<KIND, DepthSort>::value;
+    const int npass = depth3 ? DEPTH3_PASSES : (nbits + 7) / 8;
     return for_groups(V, [&](int v0, int nv) -> hipError_t {
         int maxc = 0;
         bool pair = false;
@@ -853,18 +1171,43 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
         }
         int shift = shift0;
         for (int p = 0; p < npass; p++) {
-            const int w = nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced digit widths
+            const int w = depth3 ? DEPTH3[p].w : nbits / npass + (p < nbits % npass ? 1 : 0);  // balanced widths
+            if (depth3) shift = DEPTH3[p].shift;
+            const int mode = depth3 ? DEPTH3[p].mode : DIG_RAW;
+            // 9-bit passes rank 4,096-key chunks with 512 threads, so that each digit's run in a chunk
+            // stays as long as an 8-bit pass's over 2,048 keys (coalesced write-out)
+            const bool wide = w > 8;
+            const int nt = wide ? RS_THREADS_WIDE : RS_THREADS;
+            int maxc_p = 0;
+            for (int v = 0; v < nv; v++) maxc_p = max(maxc_p, (int)rs_chunks_tile(jobs[v0 + v].n, nt * RS_ITEMS));
             const bool last = p == npass - 1;
+            // a relative pass is the last one when its range fits: it gets the final outputs too
+            const bool final_out = last || mode == DIG_REL;
             ViewBatch<CountJob> cb;
             ViewBatch<RowJob> rb;
             ViewBatch<SortPassArgs> sb;
             cb.n = rb.n = sb.n = nv;
             for (int v = 0; v < nv; v++) {
                 const SortJob& j = jobs[v0 + v];
-                const int nchunks = (int)rs_chunks(j.n);
+                const int nchunks = (int)rs_chunks_tile(j.n, nt * RS_ITEMS);
                 cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j), j.key_hi_shift ? j.pairs : nullptr, j.key_hi_shift};
                 if (j.key_hi_shift) cb.v[v].keys = nullptr;
+                cb.v[v].mode = mode;
+                cb.v[v].range = sort_range(j);
+                cb.v[v].cmaj = chunk_major(maxc_p);
                 rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
+                rb.v[v].mode = mode;
+                rb.v[v].range = sort_range(j);
+                if (depth3 && p == 0) {  // the keys' range, for the relative pass
+                    cb.v[v].cmin = sort_minmax(j);
+                    cb.v[v].cmax = sort_minmax(j) + nchunks;
+                    rb.v[v].cmin = cb.v[v].cmin;
+                    rb.v[v].cmax = cb.v[v].cmax;
+                    rb.v[v].range_out = sort_range(j);
+                    rb.v[v].nbins = 1 << w;
+                    rb.v[v].rel_shift = DEPTH3[2].shift;
+                    rb.v[v].rel_bits = DEPTH3[2].w;
+                }
                 SortPassArgs& a = sb.v[v];
                 a.n = j.n;
                 a.shift = shift;
@@ -877,22 +1220,34 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.out_x = j.out_x;
                 a.out_y = j.out_y;
                 a.sorted_keys = j.sorted_keys;
-                a.rects = (last && !pair) ? j.rects : nullptr;
+                a.rects = (final_out && !pair) ? j.rects : nullptr;
                 a.rects4_in = p == 0 ? j.rects4 : nullptr;
-                a.sorted_rects = (last && (!pair || j.rects4)) ? j.sorted_rects : nullptr;
+                a.sorted_rects = (final_out && (!pair || j.rects4)) ? j.sorted_rects : nullptr;
                 a.sorted_counts = j.sorted_counts;
                 a.row_prefix = sort_counts(j);
                 a.totals = sort_totals(j);
                 a.key_hi_shift = j.key_hi_shift;
+                a.mode = mode;
+                a.range = sort_range(j);
+                a.cmaj = chunk_major(maxc_p);
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
-            const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
-            hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND>), g, b, 0, s, cb, shift, w);
-            if (maxc <= RS_ROW_LDS)
-                hipLaunchKernelGGL(radix_rowscan_lds_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+            const dim3 g((unsigned)maxc_p, (unsigned)nv), b(RS_THREADS), bw(RS_THREADS_WIDE);
+            if (wide)
+                hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, 512, RS_THREADS_WIDE>), g, bw, 0, s, cb, shift, w);
             else
-                hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, dim3(1u << w, (unsigned)nv), b, 0, s, rb);
+                hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS>), g, b, 0, s, cb, shift, w);
+            for (int v = 0; v < nv; v++) rb.v[v].nbins = 1 << w;
+            launch_scan_rows<KIND>(rb, nv, 1 << w, maxc_p, depth3 && p == 0, s);
+            if (wide) {
+                if (pair)
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
+                else
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
+                shift += w;
+                continue;
+            }
             switch (w * 2 + (pair ? 1 : 0)) {
 #define GSR_SCATTER_W(W_)                                                                                   \
     case 2 * W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, W_>), g, b, 0, s, sb); break; \
@@ -976,10 +1331,9 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
         const dim3 g((unsigned)maxc, (unsigned)nv), b(RS_THREADS);
         if (phases & FUSED_COUNT) {
             hipLaunchKernelGGL(fused_pass1_count_kernel, g, b, 0, s, fb, gx, T, w1);
-            if (maxc <= RS_ROW_LDS)
-                hipLaunchKernelGGL(radix_rowscan_lds_kernel<TileSort>, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
-            else
-                hipLaunchKernelGGL(radix_rowscan_kernel<TileSort>, dim3(1u << w1, (unsigned)nv), b, 0, s, rb);
+            for (int v = 0; v < nv; v++) rb.v[v].nbins = 1 << w1;
+            // (the fused pass's count matrix is digit-major: thousands of 256-rank chunks)
+            launch_scan_rows<TileSort>(rb, nv, 1 << w1, max(maxc, CS_CHUNKS + 1), false, s);
         }
         if (!(phases & FUSED_SCATTER)) return hipGetLastError();
         switch (w1) {  // the first pass's digit width: ceil(msb(T) / passes) -- 7 at 1080p
