@@ -112,7 +112,7 @@ struct CountJob {
     uint32_t* cmax;
     bool cmaj;                 // chunk-major count matrix (cm_index)
 };
-template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS>
+template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS, bool LOOP = false>
 __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
     const CountJob& J = B.v[blockIdx.y];
@@ -127,10 +127,12 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
     __shared__ uint32_t s_mm[2][NW];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t nb = 1u << nbits;
+    // one chunk per workgroup -- or (LOOP: a DIG_SKIP pass's small grid) several
+    for (uint32_t chunk = blockIdx.x; chunk < (uint32_t)J.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)J.nchunks) {
     for (int q = 0; q < NW; q++)
         for (int d = tid; d < MAXB; d += NT) h[q][d] = 0;
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
+    const size_t base = (size_t)chunk * (NT * ITEMS);
     uint32_t k[ITEMS];
     // the range of the keys other than 0xFFFFFFFF (the depth sort's first pass; `full`: every k[i]
     // is a key of this chunk, else the ones at an index < n)
@@ -196,7 +198,7 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
         uint32_t c = 0;
 #pragma unroll
         for (int q = 0; q < NW; q++) c += h[q][d];
-        J.counts[cm_index(d, blockIdx.x, nb, J.nchunks, J.cmaj)] = c;
+        J.counts[cm_index(d, chunk, nb, J.nchunks, J.cmaj)] = c;
     }
     if (J.cmin && tid == 0) {
         uint32_t mn = s_mm[0][0], mx = s_mm[1][0];
@@ -204,8 +206,10 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
             mn = min(mn, s_mm[0][q]);
             mx = max(mx, s_mm[1][q]);
         }
-        J.cmin[blockIdx.x] = mn;
-        J.cmax[blockIdx.x] = mx;
+        J.cmin[chunk] = mn;
+        J.cmax[chunk] = mx;
+    }
+    __syncthreads();  // LDS reuse by the next chunk
     }
 }
 
@@ -480,7 +484,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.  NBITS <= 9: up to
 // 512 digits (two per thread in the digit-indexed steps).
-template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS>
+template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS, bool LOOP = false>
 __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
@@ -505,7 +509,8 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
     __shared__ uint32_t s_w0[NW], s_w1[NW];    // wave totals of the two block scans
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t chunk = blockIdx.x;
+    // one chunk per workgroup -- or (LOOP: a DIG_SKIP pass's small grid) several
+    for (uint32_t chunk = blockIdx.x; chunk < (uint32_t)a.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)a.nchunks) {
 #pragma unroll
     for (int i = 0; i < DPT; i++)
         for (int q = 0; q < NW; q++) s_cnt[q][tid * DPT + i] = 0;
@@ -650,6 +655,8 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
                 if (a.sorted_keys) a.sorted_keys[dst] = k;
             }
         }
+    }
+    __syncthreads();  // LDS reuse by the next chunk
     }
 }
 
@@ -1233,9 +1240,13 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
-            const dim3 g((unsigned)maxc_p, (unsigned)nv), b(RS_THREADS), bw(RS_THREADS_WIDE);
+            // a DIG_SKIP pass mostly exits at once: a small grid walks the chunks when it does run
+            const dim3 g((unsigned)(mode == DIG_SKIP ? min(maxc_p, 64) : maxc_p), (unsigned)nv), b(RS_THREADS),
+                bw(RS_THREADS_WIDE);
             if (wide)
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, 512, RS_THREADS_WIDE>), g, bw, 0, s, cb, shift, w);
+            else if (mode == DIG_SKIP)
+                hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS, RS_THREADS, true>), g, b, 0, s, cb, shift, w);
             else
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS>), g, b, 0, s, cb, shift, w);
             for (int v = 0; v < nv; v++) rb.v[v].nbins = 1 << w;
@@ -1245,6 +1256,15 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                     hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
                 else
                     hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
+                shift += w;
+                continue;
+            }
+            if (mode == DIG_SKIP) {  // the depth sort's fourth pass: 5-bit digits
+                if (w != 5) return hipErrorInvalidValue;
+                if (pair)
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 5, RS_THREADS, true>), g, b, 0, s, sb);
+                else
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 5, RS_THREADS, true>), g, b, 0, s, sb);
                 shift += w;
                 continue;
             }
