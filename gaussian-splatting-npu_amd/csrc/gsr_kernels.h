@@ -219,6 +219,10 @@ struct SortJob {  // radix_sort's arguments for one view
     // > 0 (one pass, pairs given, keys_in null): the key is pairs[i].y >> key_hi_shift, and out_y
     // gets pairs[i].y with those bits cleared
     int key_hi_shift = 0;
+    // (with key_hi_shift, instead of pairs) the pairs as two arrays: x[i], y[i] -- the count kernel then
+    // reads the 4-B y words only
+    const uint32_t* soa_x = nullptr;
+    const uint32_t* soa_y = nullptr;
 };
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };

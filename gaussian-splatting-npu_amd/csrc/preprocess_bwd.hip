@@ -534,8 +534,14 @@ __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int i
 }
 
 // The batch's cameras in LDS (view 16, proj 16, campos 3, focal_x, focal_y, tan_fovx, tan_fovy),
-// read by the lanes of each view instead of through two dependent global loads per lane.
-constexpr int CAM_FLOATS = 40;
+// read by the lanes of each view instead of through two dependent global loads per lane.  The rows
+// are GSR_CAM_STRIDE floats apart: an odd stride puts the 8 views' copies of one camera field in 8
+// different banks (a 40-float stride put views v and v + 4 in one bank: every camera read of a
+// wave, which holds lanes of all 8 views, took two LDS cycles).
+#ifndef GSR_CAM_STRIDE
+#define GSR_CAM_STRIDE 41
+#endif
+constexpr int CAM_FLOATS = GSR_CAM_STRIDE;
 __device__ __forceinline__ void cams_to_lds(const PreprocessBwdViewsArgs& A, float (*s_cam)[CAM_FLOATS])
 {
     for (int t = threadIdx.x; t < A.V * CAM_FLOATS; t += blockDim.x) {

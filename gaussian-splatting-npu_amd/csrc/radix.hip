@@ -106,6 +106,7 @@ struct CountJob {
     // the top bits of the id word, see TileSortJob)
     const uint2* pairs_hi;
     int hi_shift;
+    const uint32_t* hi_words;  // (instead of pairs_hi) the 4-B words holding the key in their high bits
     int mode;                  // DigitMode
     const RangeWord* range;    // (DIG_REL / DIG_SKIP)
     uint32_t* cmin;            // non-null: per-chunk min / max of the keys other than 0xFFFFFFFF
@@ -159,7 +160,10 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
     };
     if (!keys) {  // keys in the pairs' high bits (8-B loads; the slot word rides along unused)
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) k[i] = J.pairs_hi[min(base + (size_t)i * NT + tid, (size_t)n - 1)].y >> J.hi_shift;
+        for (int i = 0; i < ITEMS; i++) {
+            const size_t e = min(base + (size_t)i * NT + tid, (size_t)n - 1);
+            k[i] = (J.hi_words ? J.hi_words[e] : J.pairs_hi[e].y) >> J.hi_shift;
+        }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++)
             if (base + (size_t)i * NT + tid < (size_t)n) atomicAdd(&h[w][dig(k[i])], 1u);
@@ -457,6 +461,7 @@ struct SortPassArgs {
     // PAIR, > 0: there is no key array; the key is vals_in[i].y >> key_hi_shift and out_y receives
     // v.y with those bits cleared (the tile sort's second pass, see TileSortJob)
     int key_hi_shift;
+    const uint32_t* vals_in_y;  // non-null: the pairs as two arrays, x = vals_in[i], y = vals_in_y[i]
     int mode;                // DigitMode (a DIG_REL pass with both the ping-pong and the final outputs
     const RangeWord* range;  // set is the last pass when the range fits)
     bool cmaj;               // chunk-major count matrix (cm_index)
@@ -542,8 +547,15 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
     // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
     if (PAIR && a.key_hi_shift) {  // the key rides in the payload's high bits
+        if (a.vals_in_y) {
 #pragma unroll
-        for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
+            for (int i = 0; i < ITEMS; i++) {
+                if constexpr (PAIR) val[i] = make_uint2(a.vals_in[gidx(i)], a.vals_in_y[gidx(i)]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < ITEMS; i++) val[i] = reinterpret_cast<const Val*>(a.vals_in)[gidx(i)];
+        }
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
             if constexpr (PAIR) key[i] = val[i].y >> a.key_hi_shift;
@@ -672,6 +684,9 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
 // running output position from round to round, so a chunk of any size stays stable.
 // ---------------------------------------------------------------------------
 constexpr int FE_RANKS = 256;
+#ifndef GSR_TILE_SOA
+#define GSR_TILE_SOA 1
+#endif
 
 struct FusedPassArgs {
     int P, L, nchunks;
@@ -690,8 +705,11 @@ struct FusedPassArgs {
     uint32_t* valid;
     uint2* ranges;
     // > 0 (two passes, no tile ids wanted): no key array; the pass writes (slot, id | (tile >> w1)
-    // << pack_shift) and the second pass takes its key from those bits
+    // << pack_shift) and the second pass takes its key from those bits -- as two arrays (soa_x: slot,
+    // soa_y: the id word), so that the second pass's count kernel reads 4 B per instance, not 8
     int pack_shift, pack_w1;
+    uint32_t* soa_x;
+    uint32_t* soa_y;
 };
 
 // GSR_FE_AOS: a rank's fields as one 16-B {start, x0 | y0 << 16, w, 1/w} and one 8-B {record start,
@@ -952,7 +970,12 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
                 const uint2 v = make_uint2(s.rec[j] + local, s.g[j]);
 #endif
                 if (J.pack_shift) {
-                    J.vals_out[dst] = make_uint2(v.x, v.y | ((k >> J.pack_w1) << J.pack_shift));
+                    if (J.soa_x) {
+                        J.soa_x[dst] = v.x;
+                        J.soa_y[dst] = v.y | ((k >> J.pack_w1) << J.pack_shift);
+                    } else {
+                        J.vals_out[dst] = make_uint2(v.x, v.y | ((k >> J.pack_w1) << J.pack_shift));
+                    }
                 } else if (!last) {
                     J.keys_out[dst] = k;
                     J.vals_out[dst] = v;
@@ -1163,10 +1186,11 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
         bool pair = false;
         for (int v = 0; v < nv; v++) {
             maxc = max(maxc, (int)rs_chunks(jobs[v0 + v].n));
-            pair = jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr;
+            pair = jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr || jobs[v0 + v].soa_x != nullptr;
         }
         for (int v = 0; v < nv; v++)  // one payload width per launch
-            if ((jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr) != pair) return hipErrorInvalidValue;
+            if ((jobs[v0 + v].pairs != nullptr || jobs[v0 + v].rects4 != nullptr || jobs[v0 + v].soa_x != nullptr) != pair)
+                return hipErrorInvalidValue;
         if (maxc == 0) return hipSuccess;
         const uint32_t* kin[VIEW_BATCH];
         const uint32_t* vin[VIEW_BATCH];
@@ -1174,7 +1198,9 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             kin[v] = jobs[v0 + v].keys_in;
             vin[v] = reinterpret_cast<const uint32_t*>(jobs[v0 + v].pairs);
             // keys carried in the pairs' high bits: one pass only (the bits hold one digit)
-            if (jobs[v0 + v].key_hi_shift && (npass != 1 || !jobs[v0 + v].pairs)) return hipErrorInvalidValue;
+            if (jobs[v0 + v].key_hi_shift && (npass != 1 || !(jobs[v0 + v].pairs || jobs[v0 + v].soa_x)))
+                return hipErrorInvalidValue;
+            if (jobs[v0 + v].soa_x) vin[v] = jobs[v0 + v].soa_x;
         }
         int shift = shift0;
         for (int p = 0; p < npass; p++) {
@@ -1199,6 +1225,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 const int nchunks = (int)rs_chunks_tile(j.n, nt * RS_ITEMS);
                 cb.v[v] = {kin[v], j.n, nchunks, sort_counts(j), j.key_hi_shift ? j.pairs : nullptr, j.key_hi_shift};
                 if (j.key_hi_shift) cb.v[v].keys = nullptr;
+                cb.v[v].hi_words = j.key_hi_shift ? j.soa_y : nullptr;
                 cb.v[v].mode = mode;
                 cb.v[v].range = sort_range(j);
                 cb.v[v].cmaj = chunk_major(maxc_p);
@@ -1234,6 +1261,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.row_prefix = sort_counts(j);
                 a.totals = sort_totals(j);
                 a.key_hi_shift = j.key_hi_shift;
+                a.vals_in_y = (p == 0 && j.soa_x) ? j.soa_y : nullptr;
                 a.mode = mode;
                 a.range = sort_range(j);
                 a.cmaj = chunk_major(maxc_p);
@@ -1331,9 +1359,14 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             // bytes per instance instead of 12 and the second reads 8 instead of 12
             a.pack_shift = 0;
             a.pack_w1 = w1;
+            a.soa_x = a.soa_y = nullptr;
             if (GSR_TILE_PACK && npass == 2 && !j.out_tiles && (uint64_t)j.P <= (1ull << (32 - (nbits - w1)))) {
                 a.pack_shift = 32 - (nbits - w1);
                 a.keys_out = nullptr;
+                if (GSR_TILE_SOA) {  // the v1 ping-pong region (8 B per instance) as two 4-B arrays
+                    a.soa_x = j.v1;
+                    a.soa_y = j.v1 + align_up(4 * (size_t)(j.L > 0 ? j.L : 0), 256) / 4;
+                }
             }
             a.out_slot = j.out_slot;
             a.out_ids = j.out_ids;
@@ -1345,6 +1378,11 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             rest[v] = {j.L, a.pack_shift ? nullptr : j.k1, reinterpret_cast<const uint2*>(j.v1), j.k0, j.v0, j.k1, j.v1,
                        j.out_slot, j.out_ids, j.out_tiles, j.scratch, nullptr, nullptr, nullptr};
             rest[v].key_hi_shift = a.pack_shift;
+            if (a.soa_x) {
+                rest[v].pairs = nullptr;
+                rest[v].soa_x = a.soa_x;
+                rest[v].soa_y = a.soa_y;
+            }
             packed = a.pack_shift != 0;
         }
         if (maxc == 0) return hipSuccess;
