@@ -59,6 +59,21 @@ __device__ __forceinline__ size_t cm_index(uint32_t d, uint32_t c, uint32_t nb, 
     return cmaj ? (size_t)c * nb + d : (size_t)d * nchunks + c;
 }
 
+// XCD-aware chunk order of the scatter kernels: workgroups are dealt round-robin over the 8 XCDs
+// (blocks b and b + 8 share one, MI355X_MICROARCH.md §Workgroup dispatch), so with grid.x a multiple
+// of 8 (scatter_grid) the chunks [x q, (x + 1) q) of block class x = b % 8 run on one XCD, in order.
+// A digit's output runs from consecutive chunks are adjacent in memory: their partial cache lines
+// then meet in one L2 instead of being written back from several.  A bijection on [0, grid.x).
+#ifndef GSR_XCD_CHUNKS
+#define GSR_XCD_CHUNKS 1
+#endif
+__device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t gx)
+{
+    if (!GSR_XCD_CHUNKS || (gx & 7u)) return b;
+    return (b & 7u) * (gx >> 3) + (b >> 3);
+}
+static inline unsigned scatter_grid(int maxc) { return GSR_XCD_CHUNKS ? (unsigned)((maxc + 7) & ~7) : (unsigned)maxc; }
+
 // The depth sort in three 9-bit passes (depth_sort_passes): passes 1 and 2 take key bits [0, 9) and
 // [9, 18); pass 3 takes bits [18, 32) RELATIVE to the smallest key that is not 0xFFFFFFFF (culled):
 // digit = (k >> 18) - (min >> 18), and 511 for 0xFFFFFFFF.  That is monotone in k, so the three passes
@@ -493,7 +508,8 @@ template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS, b
 __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
-    if ((int)blockIdx.x >= a.nchunks) return;  // past this view's chunks (uniform)
+    const uint32_t c0 = LOOP ? blockIdx.x : xcd_chunk(blockIdx.x, gridDim.x);
+    if ((int)c0 >= a.nchunks) return;  // past this view's chunks (uniform)
     bool skip;
     const Digit dig = make_digit(a.shift, NBITS, a.mode, a.range, &skip);
     if (skip) return;
@@ -515,7 +531,7 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     // one chunk per workgroup -- or (LOOP: a DIG_SKIP pass's small grid) several
-    for (uint32_t chunk = blockIdx.x; chunk < (uint32_t)a.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)a.nchunks) {
+    for (uint32_t chunk = c0; chunk < (uint32_t)a.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)a.nchunks) {
 #pragma unroll
     for (int i = 0; i < DPT; i++)
         for (int q = 0; q < NW; q++) s_cnt[q][tid * DPT + i] = 0;
@@ -832,6 +848,8 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
     constexpr int nbits = NBITS;  // the digit width, a compile-time constant (unrolled ballot ranking)
     constexpr int TILE = RS_THREADS * ITEMS;
     const FusedPassArgs& J = B.v[blockIdx.y];
+    // (no xcd_chunk here: a chunk's instance count falls with the depth of its ranks, and contiguous
+    // depth ranges per XCD unbalance the XCDs -- measured +16 %)
     const int c = (int)blockIdx.x;
     if (c >= J.nchunks) return;  // past this view's chunks (uniform)
     __shared__ FeRanks s;
@@ -1271,6 +1289,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             // a DIG_SKIP pass mostly exits at once: a small grid walks the chunks when it does run
             const dim3 g((unsigned)(mode == DIG_SKIP ? min(maxc_p, 64) : maxc_p), (unsigned)nv), b(RS_THREADS),
                 bw(RS_THREADS_WIDE);
+            const dim3 gs(mode == DIG_SKIP ? g.x : scatter_grid(maxc_p), (unsigned)nv);  // (xcd_chunk)
             if (wide)
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, 512, RS_THREADS_WIDE>), g, bw, 0, s, cb, shift, w);
             else if (mode == DIG_SKIP)
@@ -1281,9 +1300,9 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             launch_scan_rows<KIND>(rb, nv, 1 << w, maxc_p, depth3 && p == 0, s);
             if (wide) {
                 if (pair)
-                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), gs, bw, 0, s, sb);
                 else
-                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 9, RS_THREADS_WIDE>), g, bw, 0, s, sb);
+                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 9, RS_THREADS_WIDE>), gs, bw, 0, s, sb);
                 shift += w;
                 continue;
             }
@@ -1297,9 +1316,9 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 continue;
             }
             switch (w * 2 + (pair ? 1 : 0)) {
-#define GSR_SCATTER_W(W_)                                                                                   \
-    case 2 * W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, W_>), g, b, 0, s, sb); break; \
-    case 2 * W_ + 1: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, W_>), g, b, 0, s, sb); break;
+#define GSR_SCATTER_W(W_)                                                                                    \
+    case 2 * W_: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, W_>), gs, b, 0, s, sb); break; \
+    case 2 * W_ + 1: hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, W_>), gs, b, 0, s, sb); break;
                 GSR_SCATTER_W(1) GSR_SCATTER_W(2) GSR_SCATTER_W(3) GSR_SCATTER_W(4)
                 GSR_SCATTER_W(5) GSR_SCATTER_W(6) GSR_SCATTER_W(7) GSR_SCATTER_W(8)
 #undef GSR_SCATTER_W
@@ -1394,8 +1413,9 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             launch_scan_rows<TileSort>(rb, nv, 1 << w1, max(maxc, CS_CHUNKS + 1), false, s);
         }
         if (!(phases & FUSED_SCATTER)) return hipGetLastError();
+        const dim3 gs((unsigned)maxc, (unsigned)nv);
         switch (w1) {  // the first pass's digit width: ceil(msb(T) / passes) -- 7 at 1080p
-#define GSR_FUSED_W(W_) case W_: hipLaunchKernelGGL((fused_pass1_scatter_kernel<RS_ITEMS, W_>), g, b, 0, s, fb, gx); break;
+#define GSR_FUSED_W(W_) case W_: hipLaunchKernelGGL((fused_pass1_scatter_kernel<RS_ITEMS, W_>), gs, b, 0, s, fb, gx); break;
             GSR_FUSED_W(1) GSR_FUSED_W(2) GSR_FUSED_W(3) GSR_FUSED_W(4)
             GSR_FUSED_W(5) GSR_FUSED_W(6) GSR_FUSED_W(7) GSR_FUSED_W(8)
 #undef GSR_FUSED_W
