@@ -15,13 +15,16 @@ def families(name):
     return "other"
 
 
+STEP_MARK = ("preprocess_fwd_kernel", "ELi8E")  # the 8-view batch's preprocess starts a step
+
+
 def main(db):
     c = sqlite3.connect(db)
     scols = [r[1] for r in c.execute("pragma table_info(rocpd_info_kernel_symbol)")]
     name_col = "kernel_name" if "kernel_name" in scols else "display_name"
     rows = list(c.execute(f"select d.start, d.end, s.{name_col} from rocpd_kernel_dispatch d join "
                           f"rocpd_info_kernel_symbol s on d.kernel_id = s.id order by d.start"))
-    starts = [i for i, r in enumerate(rows) if "preprocess_fwd_kernel" in r[2] and "ELi8E" in r[2]]
+    starts = [i for i, r in enumerate(rows) if STEP_MARK[0] in r[2] and STEP_MARK[1] in r[2]]
     steps = list(zip(starts[-6:-1], starts[-5:]))
     acc = collections.defaultdict(float)
     total = 0.0
@@ -42,7 +45,7 @@ def timeline(db, which=-3):
     c = sqlite3.connect(db)
     rows = list(c.execute("select d.start, d.end, s.kernel_name from rocpd_kernel_dispatch d join "
                           "rocpd_info_kernel_symbol s on d.kernel_id = s.id order by d.start"))
-    starts = [i for i, r in enumerate(rows) if "preprocess_fwd_kernel" in r[2] and "ELi8E" in r[2]]
+    starts = [i for i, r in enumerate(rows) if STEP_MARK[0] in r[2] and STEP_MARK[1] in r[2]]
     a, b = starts[which], starts[which + 1]
     t0 = rows[a][0]
     for s, e, n in rows[a:b]:
@@ -50,6 +53,9 @@ def timeline(db, which=-3):
 
 
 if __name__ == "__main__":
+    if "--single" in sys.argv:  # the single-view step: preprocess_fwd_kernel<true, 1>
+        sys.argv.remove("--single")
+        STEP_MARK = ("preprocess_fwd_kernel", "ELi1E")
     main(sys.argv[1])
     if len(sys.argv) > 2:
         timeline(sys.argv[1])
