@@ -28,6 +28,9 @@ namespace {
 thread_local std::string g_err;
 thread_local uint32_t* g_pinned = nullptr;
 constexpr uint32_t L_PENDING = 0xFFFFFFFFu;  // h[2] before the scan stores num_rendered (< 2^31)
+// forward_geometry_wait: the depth keys' range was too wide for the three-pass depth sort (h[1]); the
+// forward is re-run with four passes (set_depth_wide) -- internal, never returned to a caller
+constexpr int GSR_RERUN_WIDE = -100;
 
 int fail(int code, const char* msg)
 {
@@ -347,6 +350,7 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
     int rc = pinned(slot, &h);
     if (rc) return rc;
     h[0] = 0;
+    h[1] = 0;  // the depth sort's "range too wide" flag
     __atomic_store_n(&h[2], L_PENDING, __ATOMIC_RELEASE);
     uint32_t* h_dev = nullptr;
     HIP_TRY(hipHostGetDevicePointer((void**)&h_dev, h, 0));
@@ -454,6 +458,7 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, char* ib, in
         SortJob j = {P, a.dkey, nullptr, k0, v0, k1, v1, sorted_ids, nullptr, nullptr, gb + g.off[GEOM_RADIX_SCRATCH],
                      a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                      a.rect4};
+        j.host_wide = h_dev + 1;
         e = radix_sort_batch(&j, 1, DEPTH_BITS, s);
     }
     if (debug && e == hipSuccess) e = hipStreamSynchronize(s);
@@ -519,6 +524,10 @@ static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rend
     if (__atomic_load_n(&h[2], __ATOMIC_ACQUIRE) == L_PENDING) return fail(GSR_ERR_HIP, "scan did not publish num_rendered");
     if (h[0] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (__atomic_load_n(&h[1], __ATOMIC_ACQUIRE)) {  // (stored before the scan ran: visible with L)
+        set_depth_wide(true);
+        return GSR_RERUN_WIDE;
+    }
     if (h[2] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
     *num_rendered = (int)h[2];
     return GSR_OK;
@@ -545,6 +554,11 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
     if (rc) return rc;
     rc = forward_geometry_wait(h, ps, num_rendered);
     const int rj = prefix_end((hipStream_t)stream, ps);
+    if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
+        return gsr_forward_geometry_dc(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
+                                       colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                       viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                       radii, debug, stream, num_rendered);
     return rc ? rc : rj;
 }
 
@@ -755,6 +769,12 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     *num_rendered = L;
     if (rc) {
         prefix_end((hipStream_t)stream, ps);
+        if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
+            return gsr_forward_prealloc_dc(geometry_buffer, image_buffer, binning_buffer, binning_capacity, P, D, M,
+                                           background, width, height, means3D, dc, shs, colors_precomp, opacities,
+                                           scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                                           cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing, out_color, depth,
+                                           radii, debug, stream, num_rendered, rendered);
         return rc;
     }
     if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity)  // caller allocates
@@ -838,6 +858,7 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                     at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]), a.rect4};
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
+        dsort[v].host_wide = hdev[v] + 1;
     }
     // the record-slot scans (read only by the fused tile sort) on the auxiliary stream, beside the
     // depth sorts
@@ -891,6 +912,12 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
     }
     if (rc) {
         prefix_end(caller, ps);
+        if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
+            return gsr_forward_views(V, P, D, M, background, width, height, means3D, dc, shs, colors_precomp,
+                                     opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrices,
+                                     projmatrices, campos, tan_fovx, tan_fovy, prefiltered, antialiasing,
+                                     geometry_buffers, image_buffers, binning_buffers, binning_capacity, out_colors,
+                                     out_invdepths, radii, debug, stream, num_rendered, rendered);
         return rc;
     }
     // views whose binning buffer holds them: emission fused into the tile sort, tile ranges and
@@ -1458,6 +1485,14 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
     return GSR_OK;
 }
 
+int gsr_debug_depth_wide(void) { return depth_wide() ? 1 : 0; }
+
+int gsr_debug_set_depth_wide(int on)
+{
+    set_depth_wide(on != 0);
+    return GSR_OK;
+}
+
 size_t gsr_debug_depth_sort_workspace_size(int n)
 {
     const size_t q = align_up(4 * (size_t)(n > 0 ? n : 0), 256);
@@ -1476,6 +1511,18 @@ int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* w
     uint32_t* v1 = reinterpret_cast<uint32_t*>(workspace + 3 * q);
     // the forward's call (forward_geometry_sort) without the rect gather
     HIP_TRY(radix_sort(n, DEPTH_BITS, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr, workspace + 4 * q, s));
+    if (!depth_wide()) {  // three passes: the range word says whether they sufficed (else four, as the forward)
+        uint32_t rw[2] = {0u, 1u};
+        HIP_TRY(hipMemcpyAsync(rw, workspace + 4 * q + radix_range_offset(n), 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (!rw[1]) {
+            set_depth_wide(true);
+            const hipError_t e = radix_sort(n, DEPTH_BITS, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr,
+                                            workspace + 4 * q, s);
+            set_depth_wide(false);
+            HIP_TRY(e);
+        }
+    }
     return GSR_OK;
 }
 

@@ -223,7 +223,15 @@ struct SortJob {  // radix_sort's arguments for one view
     // reads the 4-B y words only
     const uint32_t* soa_x = nullptr;
     const uint32_t* soa_y = nullptr;
+    // the three-pass depth sort: a pinned host word set to 1 when the keys' range was too wide for it
+    uint32_t* host_wide = nullptr;
 };
+// After a depth sort reported a range too wide for three 9-bit passes (SortJob::host_wide): every
+// later depth sort runs four 8-bit passes (process-wide).
+void set_depth_wide(bool on);
+bool depth_wide();
+// byte offset, inside a sort's scratch (radix_status_bytes(n)), of its {base, fits} range word
+size_t radix_range_offset(int n);
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };
 // V independent stable sorts over the same bit width (key bits [shift0, shift0 + nbits)), pass by

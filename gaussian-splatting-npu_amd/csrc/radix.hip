@@ -74,17 +74,16 @@ __device__ __forceinline__ uint32_t xcd_chunk(uint32_t b, uint32_t gx)
 }
 static inline unsigned scatter_grid(int maxc) { return GSR_XCD_CHUNKS ? (unsigned)((maxc + 7) & ~7) : (unsigned)maxc; }
 
-// The depth sort in three 9-bit passes (depth_sort_passes): passes 1 and 2 take key bits [0, 9) and
-// [9, 18); pass 3 takes bits [18, 32) RELATIVE to the smallest key that is not 0xFFFFFFFF (culled):
+// The depth sort in three 9-bit passes: passes 1 and 2 take key bits [0, 9) and [9, 18); pass 3
+// takes bits [18, 32) RELATIVE to the smallest key that is not 0xFFFFFFFF (culled):
 // digit = (k >> 18) - (min >> 18), and 511 for 0xFFFFFFFF.  That is monotone in k, so the three passes
-// sort exactly, whenever the keys other than 0xFFFFFFFF span at most 511 values of k >> 18 (visible
+// sort exactly whenever the keys other than 0xFFFFFFFF span at most 511 values of k >> 18 (visible
 // depths within a factor of ~2^16: 0.2 ... 13,000).  Pass 1 gathers the range (per-chunk min / max,
-// reduced by an extra workgroup of its row scan into RangeWord); a wider range makes pass 3 take raw
-// bits [18, 27) and a fourth 5-bit pass on bits [27, 32) run -- the fourth pass's kernels exit at once
-// otherwise, and pass 3 is then the last pass (it writes the final arrays).
-// mode: DIG_RAW (k >> shift) & mask; DIG_REL (the relative digit above when the range fits, else raw);
-// DIG_SKIP (the kernels exit when the range fits).
-enum DigitMode { DIG_RAW = 0, DIG_REL = 1, DIG_SKIP = 2 };
+// reduced by an extra workgroup of its scan into RangeWord).  A wider range is reported to the host
+// (SortJob::host_wide, a pinned word it reads with num_rendered): the forward then runs again with
+// the four-pass 8-bit sort (set_depth_wide), and keeps it from then on.
+// mode: DIG_RAW (k >> shift) & mask; DIG_REL (the relative digit above when the range fits, else raw).
+enum DigitMode { DIG_RAW = 0, DIG_REL = 1 };
 struct RangeWord { uint32_t base, fits; };  // min >> rel_shift of the keys other than 0xFFFFFFFF; range fits
 struct Digit {
     int shift;
@@ -96,18 +95,13 @@ struct Digit {
         return rel ? (k == 0xFFFFFFFFu ? mask : (k >> shift) - base) : (k >> shift) & mask;
     }
 };
-// (mode, range) -> the digit function of a pass; *skip: a DIG_SKIP pass whose range fits
-__device__ __forceinline__ Digit make_digit(int shift, int nbits, int mode, const RangeWord* range, bool* skip)
+// (mode, range) -> the digit function of a pass
+__device__ __forceinline__ Digit make_digit(int shift, int nbits, int mode, const RangeWord* range)
 {
     Digit d{shift, (1u << nbits) - 1u, false, 0u};
-    *skip = false;
-    if (mode != DIG_RAW) {
-        const uint32_t fits = __builtin_amdgcn_readfirstlane(range->fits);
-        if (mode == DIG_REL && fits) {
-            d.rel = true;
-            d.base = __builtin_amdgcn_readfirstlane(range->base);
-        }
-        *skip = mode == DIG_SKIP && fits;
+    if (mode == DIG_REL && __builtin_amdgcn_readfirstlane(range->fits)) {
+        d.rel = true;
+        d.base = __builtin_amdgcn_readfirstlane(range->base);
     }
     return d;
 }
@@ -123,19 +117,17 @@ struct CountJob {
     int hi_shift;
     const uint32_t* hi_words;  // (instead of pairs_hi) the 4-B words holding the key in their high bits
     int mode;                  // DigitMode
-    const RangeWord* range;    // (DIG_REL / DIG_SKIP)
+    const RangeWord* range;    // (DIG_REL)
     uint32_t* cmin;            // non-null: per-chunk min / max of the keys other than 0xFFFFFFFF
     uint32_t* cmax;
     bool cmaj;                 // chunk-major count matrix (cm_index)
 };
-template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS, bool LOOP = false>
+template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS>
 __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
     const CountJob& J = B.v[blockIdx.y];
     if ((int)blockIdx.x >= J.nchunks) return;  // past this view's chunks (uniform)
-    bool skip;
-    const Digit dig = make_digit(shift, nbits, J.mode, J.range, &skip);
-    if (skip) return;
+    const Digit dig = make_digit(shift, nbits, J.mode, J.range);
     const uint32_t* keys = J.keys;
     const int n = J.n;
     constexpr int NW = NT / 64;
@@ -143,8 +135,8 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
     __shared__ uint32_t s_mm[2][NW];
     const int tid = threadIdx.x, w = tid >> 6;
     const uint32_t nb = 1u << nbits;
-    // one chunk per workgroup -- or (LOOP: a DIG_SKIP pass's small grid) several
-    for (uint32_t chunk = blockIdx.x; chunk < (uint32_t)J.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)J.nchunks) {
+    {
+    const uint32_t chunk = blockIdx.x;
     for (int q = 0; q < NW; q++)
         for (int d = tid; d < MAXB; d += NT) h[q][d] = 0;
     __syncthreads();
@@ -228,7 +220,6 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
         J.cmin[chunk] = mn;
         J.cmax[chunk] = mx;
     }
-    __syncthreads();  // LDS reuse by the next chunk
     }
 }
 
@@ -238,8 +229,7 @@ struct RowJob {
     uint32_t* counts;
     int nchunks;
     uint32_t* totals;
-    int mode;                  // DIG_SKIP: exit when the range fits
-    const RangeWord* range;
+    uint32_t* host_wide;       // (range_out) pinned host word: set to 1 when the range does not fit
     // non-null (the depth sort's first pass): workgroup `nbins` (one past the digit rows) reduces the
     // per-chunk min / max into *range_out for a relative pass on bits [rel_shift, rel_shift + rel_bits)
     const uint32_t* cmin;
@@ -280,6 +270,7 @@ __device__ void reduce_range(const RowJob& J)
             r.fits = ((mx >> J.rel_shift) - r.base) <= (1u << J.rel_bits) - 2u ? 1u : 0u;
         }
         *J.range_out = r;
+        if (!r.fits && J.host_wide) __hip_atomic_store(J.host_wide, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 template <typename KIND>
@@ -290,7 +281,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_kernel(const ViewBat
         reduce_range(J);
         return;
     }
-    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
     uint32_t* counts = J.counts;
     const int nchunks = J.nchunks;
     uint32_t* totals = J.totals;
@@ -334,7 +324,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_rowscan_lds_kernel(const Vie
         reduce_range(J);
         return;
     }
-    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
     uint32_t* counts = J.counts;
     const int nchunks = J.nchunks;
     uint32_t* totals = J.totals;
@@ -399,7 +388,6 @@ __global__ void __launch_bounds__(RS_THREADS) radix_colscan_kernel(const ViewBat
         return;
     }
     if ((int)blockIdx.x >= ngroups) return;
-    if (J.mode == DIG_SKIP && __builtin_amdgcn_readfirstlane(J.range->fits)) return;
     __shared__ uint32_t s_col[CS_CHUNKS * (CS_DIG + 1)];  // [chunk][digit], rows padded to 17 words
     const int tid = threadIdx.x, dl = tid >> 4, sg = tid & 15;
     const uint32_t nb = (uint32_t)J.nbins, nchunks = (uint32_t)J.nchunks;
@@ -477,8 +465,8 @@ struct SortPassArgs {
     // v.y with those bits cleared (the tile sort's second pass, see TileSortJob)
     int key_hi_shift;
     const uint32_t* vals_in_y;  // non-null: the pairs as two arrays, x = vals_in[i], y = vals_in_y[i]
-    int mode;                // DigitMode (a DIG_REL pass with both the ping-pong and the final outputs
-    const RangeWord* range;  // set is the last pass when the range fits)
+    int mode;                // DigitMode
+    const RangeWord* range;
     bool cmaj;               // chunk-major count matrix (cm_index)
 };
 
@@ -504,17 +492,14 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* s4)
 
 // (3) stable rank + scatter of one chunk.  PAIR: the payload is two u32 words.  NBITS <= 9: up to
 // 512 digits (two per thread in the digit-indexed steps).
-template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS, bool LOOP = false>
+template <int ITEMS, bool PAIR, typename KIND, int NBITS, int NT = RS_THREADS>
 __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortPassArgs> B)
 {
     const SortPassArgs& a = B.v[blockIdx.y];
-    const uint32_t c0 = LOOP ? blockIdx.x : xcd_chunk(blockIdx.x, gridDim.x);
-    if ((int)c0 >= a.nchunks) return;  // past this view's chunks (uniform)
-    bool skip;
-    const Digit dig = make_digit(a.shift, NBITS, a.mode, a.range, &skip);
-    if (skip) return;
-    // the pass writes the final arrays: no ping-pong output, or a relative pass whose range fits
-    const bool is_last = a.keys_out == nullptr || dig.rel;
+    const uint32_t chunk = xcd_chunk(blockIdx.x, gridDim.x);
+    if ((int)chunk >= a.nchunks) return;  // past this view's chunks (uniform)
+    const Digit dig = make_digit(a.shift, NBITS, a.mode, a.range);
+    const bool is_last = a.keys_out == nullptr;
     constexpr int TILE = NT * ITEMS;
     constexpr int NB = 1 << NBITS;
     constexpr int NBA = NB < NT ? NT : NB;  // digit-indexed arrays: at least one per thread
@@ -530,8 +515,7 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
     __shared__ uint32_t s_w0[NW], s_w1[NW];    // wave totals of the two block scans
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    // one chunk per workgroup -- or (LOOP: a DIG_SKIP pass's small grid) several
-    for (uint32_t chunk = c0; chunk < (uint32_t)a.nchunks; chunk = LOOP ? chunk + gridDim.x : (uint32_t)a.nchunks) {
+    {
 #pragma unroll
     for (int i = 0; i < DPT; i++)
         for (int q = 0; q < NW; q++) s_cnt[q][tid * DPT + i] = 0;
@@ -684,7 +668,6 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
             }
         }
     }
-    __syncthreads();  // LDS reuse by the next chunk
     }
 }
 
@@ -1183,21 +1166,29 @@ static void launch_scan_rows(const ViewBatch<RowJob>& rb, int nv, int nbins, int
         hipLaunchKernelGGL(radix_rowscan_kernel<KIND>, g, b, 0, s, rb);
 }
 
+size_t radix_range_offset(int n)
+{
+    return rs_count_bytes(n) + rs_totals_bytes() + 4 * 2 * ((rs_chunks(n) + 1) & ~(size_t)1);
+}
+
 // One radix pass of a sort: digit width, key shift, DigitMode.
 struct PassSpec { int w, shift, mode; };
 // The full 32-bit key sorts (the depth sort) in three 9-bit passes, the third relative to the keys'
-// minimum, plus a 5-bit fourth pass that runs only when the keys' range is too wide (DigitMode).
-constexpr int DEPTH3_PASSES = 4;
-constexpr PassSpec DEPTH3[DEPTH3_PASSES] = {{9, 0, DIG_RAW}, {9, 9, DIG_RAW}, {9, 18, DIG_REL}, {5, 27, DIG_SKIP}};
+// minimum (DigitMode); after a range that did not fit (set_depth_wide), four 8-bit passes.
+constexpr int DEPTH3_PASSES = 3;
+constexpr PassSpec DEPTH3[DEPTH3_PASSES] = {{9, 0, DIG_RAW}, {9, 9, DIG_RAW}, {9, 18, DIG_REL}};
 #ifndef GSR_DEPTH3
 #define GSR_DEPTH3 1
 #endif
+static bool g_depth_wide = !GSR_DEPTH3;
+void set_depth_wide(bool on) { g_depth_wide = on || !GSR_DEPTH3; }
+bool depth_wide() { return g_depth_wide; }
 
 template <typename KIND>
 static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
 {
     if (nbits < 1) nbits = 1;
-    const bool depth3 = GSR_DEPTH3 && nbits == 32 && shift0 == 0 && std::is_same<KIND, DepthSort>::value;
+    const bool depth3 = !g_depth_wide && nbits == 32 && shift0 == 0 && std::is_same<KIND, DepthSort>::value;
     const int npass = depth3 ? DEPTH3_PASSES : (nbits + 7) / 8;
     return for_groups(V, [&](int v0, int nv) -> hipError_t {
         int maxc = 0;
@@ -1232,8 +1223,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             int maxc_p = 0;
             for (int v = 0; v < nv; v++) maxc_p = max(maxc_p, (int)rs_chunks_tile(jobs[v0 + v].n, nt * RS_ITEMS));
             const bool last = p == npass - 1;
-            // a relative pass is the last one when its range fits: it gets the final outputs too
-            const bool final_out = last || mode == DIG_REL;
+            const bool final_out = last;
             ViewBatch<CountJob> cb;
             ViewBatch<RowJob> rb;
             ViewBatch<SortPassArgs> sb;
@@ -1248,8 +1238,6 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 cb.v[v].range = sort_range(j);
                 cb.v[v].cmaj = chunk_major(maxc_p);
                 rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
-                rb.v[v].mode = mode;
-                rb.v[v].range = sort_range(j);
                 if (depth3 && p == 0) {  // the keys' range, for the relative pass
                     cb.v[v].cmin = sort_minmax(j);
                     cb.v[v].cmax = sort_minmax(j) + nchunks;
@@ -1259,6 +1247,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                     rb.v[v].nbins = 1 << w;
                     rb.v[v].rel_shift = DEPTH3[2].shift;
                     rb.v[v].rel_bits = DEPTH3[2].w;
+                    rb.v[v].host_wide = j.host_wide;
                 }
                 SortPassArgs& a = sb.v[v];
                 a.n = j.n;
@@ -1286,14 +1275,10 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
-            // a DIG_SKIP pass mostly exits at once: a small grid walks the chunks when it does run
-            const dim3 g((unsigned)(mode == DIG_SKIP ? min(maxc_p, 64) : maxc_p), (unsigned)nv), b(RS_THREADS),
-                bw(RS_THREADS_WIDE);
-            const dim3 gs(mode == DIG_SKIP ? g.x : scatter_grid(maxc_p), (unsigned)nv);  // (xcd_chunk)
+            const dim3 g((unsigned)maxc_p, (unsigned)nv), b(RS_THREADS), bw(RS_THREADS_WIDE);
+            const dim3 gs(scatter_grid(maxc_p), (unsigned)nv);  // (xcd_chunk)
             if (wide)
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, 512, RS_THREADS_WIDE>), g, bw, 0, s, cb, shift, w);
-            else if (mode == DIG_SKIP)
-                hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS, RS_THREADS, true>), g, b, 0, s, cb, shift, w);
             else
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS>), g, b, 0, s, cb, shift, w);
             for (int v = 0; v < nv; v++) rb.v[v].nbins = 1 << w;
@@ -1303,15 +1288,6 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                     hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), gs, bw, 0, s, sb);
                 else
                     hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 9, RS_THREADS_WIDE>), gs, bw, 0, s, sb);
-                shift += w;
-                continue;
-            }
-            if (mode == DIG_SKIP) {  // the depth sort's fourth pass: 5-bit digits
-                if (w != 5) return hipErrorInvalidValue;
-                if (pair)
-                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 5, RS_THREADS, true>), g, b, 0, s, sb);
-                else
-                    hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, false, KIND, 5, RS_THREADS, true>), g, b, 0, s, sb);
                 shift += w;
                 continue;
             }

@@ -66,6 +66,9 @@ def _load():
     lib.gsr_debug_depth_sort_workspace_size.argtypes = [_i]
     lib.gsr_debug_depth_sort_workspace_size.restype = _sz
     lib.gsr_debug_depth_sort.argtypes = [_vp, _i, _vp, _vp, _vp]
+    if hasattr(lib, "gsr_debug_set_depth_wide"):  # (test hooks; absent from libraries built before them)
+        lib.gsr_debug_depth_wide.argtypes = []
+        lib.gsr_debug_set_depth_wide.argtypes = [_i]
     for n in ("gsr_geometry_layout", "gsr_binning_layout"):
         getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
     lib.gsr_image_layout.argtypes = [_i, _i, ctypes.POINTER(_sz), _i]
@@ -700,6 +703,17 @@ def depth_sort(keys):
     _check(lib.gsr_debug_depth_sort(keys.data_ptr(), n, ids.data_ptr(), ws.data_ptr(),
                                     _stream(keys.device)))
     return ids
+
+
+def depth_wide():
+    """True once a forward saw visible depths too widely spread for the three-pass depth sort: every
+    later depth sort of the process runs four 8-bit passes (test hook)."""
+    return bool(lib.gsr_debug_depth_wide())
+
+
+def set_depth_wide(on):
+    """Test hook: force (True) or release (False) the four-pass depth sort."""
+    _check(lib.gsr_debug_set_depth_wide(1 if on else 0))
 
 
 def fusedssim(C1, C2, img1, img2):

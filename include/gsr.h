@@ -391,6 +391,13 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
 size_t gsr_debug_depth_sort_workspace_size(int n);
 int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* workspace, gsr_stream_t stream);
 
+/* The depth sort runs three 9-bit passes, the third relative to the smallest visible key; a forward
+ * whose visible depth keys span too wide a range for that (depths beyond a factor of ~2^16) is re-run
+ * with four 8-bit passes, which every later forward of the process then keeps.  Test hooks: read /
+ * set that mode (1 = four passes). */
+int gsr_debug_depth_wide(void);
+int gsr_debug_set_depth_wide(int on);
+
 /* Byte offsets of the arrays inside each opaque state buffer (n entries
  * written, count of arrays returned; entry [count] is the total size).  For
  * parity tests and debugging only; the layout is private to this library. */

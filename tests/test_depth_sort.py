@@ -1,6 +1,7 @@
-"""The forward's depth sort on its own (csrc/radix.hip radix_sort over 32 bits, 4 x 8-bit LSD
-passes, via the parity helper gsr_debug_depth_sort): the first half of the reference's tile|depth
-key sort (rasterizer_impl.cu:306-311, cub::DeviceRadixSort::SortPairs, stable).
+"""The forward's depth sort on its own (csrc/radix.hip radix_sort over 32 bits: three 9-bit LSD
+passes, the third relative to the smallest key other than 0xFFFFFFFF, or four 8-bit passes when the
+keys span too wide a range -- via the parity helper gsr_debug_depth_sort): the first half of the
+reference's tile|depth key sort (rasterizer_impl.cu:306-311, cub::DeviceRadixSort::SortPairs, stable).
 
 Cases: ties, ranges crossing powers of two, the widest range (tiny and huge floats together), one
 distinct key, culled keys (0xFFFFFFFF, sorted last) mixed in or alone, digit boundaries, and sizes
@@ -62,3 +63,73 @@ def test_depth_sort_full_size_and_repeat():
     b = _C.depth_sort(kt)
     np.testing.assert_array_equal(a.cpu().numpy().view(np.uint32), np.argsort(keys, kind="stable"))
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wide", [False, True])
+def test_depth_sort_both_modes(wide):
+    """The same keys through the three-pass sort (range fits) and the forced four-pass sort."""
+    from diff_gaussian_rasterization import _C
+    r = np.random.default_rng(17)
+    keys = _floats(r, 250_000, 0.25, 40.0)
+    keys[r.random(keys.size) < 0.1] = CULLED
+    kt = torch.from_numpy(keys.view(np.int32).copy()).cuda()
+    was = _C.depth_wide()
+    _C.set_depth_wide(wide)
+    try:
+        ids = _C.depth_sort(kt).cpu().numpy().view(np.uint32)
+    finally:
+        _C.set_depth_wide(was)
+    np.testing.assert_array_equal(ids, np.argsort(keys, kind="stable").astype(np.uint32))
+
+
+@pytest.mark.gpu
+def test_forward_with_too_wide_depth_range_reruns_bit_exact():
+    """A forward whose visible depths span 0.3 ... 50,000 (beyond the three-pass sort's factor of
+    ~2^16): the pass-1 range reduction flags it in the pinned word read with num_rendered, the forward
+    re-runs with four 8-bit passes, and keys / values / ranges / radii / image match the oracle bit
+    for bit (the render by check_render); the four-pass mode then sticks (released after the test)."""
+    import common
+    import synthetic
+    from diff_gaussian_rasterization import _C
+    case = common.make_case(P=4000, H=256, W=256)
+    cam = case["cam"]
+    g = torch.Generator().manual_seed(3)
+    P = 4000
+    # along the camera's view ray: depth d log-uniform in [0.3, 5e4], lateral offsets within the view
+    C = torch.tensor(cam.camera_center.numpy(), dtype=torch.float64)
+    fwd = -C / C.norm()
+    up = torch.tensor([0.0, 1.0, 0.0], dtype=torch.float64)
+    right = torch.linalg.cross(fwd, up)
+    right /= right.norm()
+    up2 = torch.linalg.cross(right, fwd)
+    d = torch.exp(torch.rand(P, generator=g, dtype=torch.float64) * (np.log(5e4) - np.log(0.3)) + np.log(0.3))
+    lat = (torch.rand(P, 2, generator=g, dtype=torch.float64) - 0.5) * 0.6 * d[:, None]
+    means = C + d[:, None] * fwd + lat[:, :1] * right + lat[:, 1:] * up2
+    sc = case["scene"]
+    sc["means3D"] = means.float().contiguous()
+    sc["scales"] = (sc["scales"] * (d[:, None].float() * 0.5)).contiguous()
+    o, _ = common.run_oracle(case, nthreads=8, backward=False)
+    assert o.num_rendered > 0
+    dev = torch.device("cuda:0")
+    was = _C.depth_wide()
+    _C.set_depth_wide(False)
+    try:
+        e = torch.Tensor([])
+        s = {k: v.to(dev) for k, v in sc.items()}
+        L, color, radii, geom, binning, img, inv = _C.rasterize_gaussians(
+            case["bg"].to(dev), s["means3D"], e, s["opacities"], s["scales"], s["rotations"], 1.0, e,
+            cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.tanfovx, cam.tanfovy, 256, 256,
+            s["shs"], 3, cam.camera_center.to(dev), False, False, False)
+        torch.cuda.synchronize()
+        assert _C.depth_wide(), "the wide depth range should have switched the depth sort to four passes"
+        assert L == o.num_rendered
+        np.testing.assert_array_equal(radii.cpu().numpy(), o.radii)
+        keys, vals, ranges = _C.sorted_keys(geom, binning, img, P, L, 256, 256)
+        np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
+        np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
+        np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+        common.check_render("wide depth range", {"color": color.cpu().numpy(), "invdepth": inv.cpu().numpy()},
+                            {"color": o.color, "invdepth": o.invdepth})
+    finally:
+        _C.set_depth_wide(was)
