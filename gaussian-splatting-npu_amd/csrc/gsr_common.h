@@ -200,7 +200,8 @@ enum ImageArray {
 enum BinArray {
     BIN_POINT_LIST = 0,   // u32[L] Gaussian id of sorted position
     BIN_SORTED_TILES,     // u32[L] tile id of sorted position
-    BIN_SLOT,             // u32[L] gradient-record slot of sorted position
+    BIN_SLOT,             // u32[L] gradient-record slot of sorted position (GSR_SLOT_LOCAL: minus the
+                          // Gaussian's emit_start, i.e. the instance's index in its rect)
     BIN_GRAD_INST,        // f32x12[L] per-(tile, Gaussian) gradient records (backward); during the forward
                           // it hosts the tile sort's ping-pong buffers (24 B/instance)
     BIN_RADIX_SCRATCH,    // count matrix + digit totals of the tile sort
@@ -243,6 +244,11 @@ constexpr int TILE_DIFF_MAX_CELLS = 8704;
 // the tile sort's second digit carried in the id word (radix.hip tile_sort_fused_batch)
 #ifndef GSR_TILE_PACK
 #define GSR_TILE_PACK 1
+#endif
+// BIN_SLOT holds each instance's index inside its Gaussian's tile rect (its record slot minus the
+// Gaussian's emit_start) instead of the absolute record slot
+#ifndef GSR_SLOT_LOCAL
+#define GSR_SLOT_LOCAL 1
 #endif
 __host__ __device__ inline bool use_tile_diff(uint32_t grid_x, uint32_t grid_y)
 {

@@ -743,7 +743,10 @@ __device__ __forceinline__ void fe_stage(const FusedPassArgs& J, int c, FeRanks&
         wd = max((rc.y & 0xFFFFu) - x0, 1u);
         if (IDS) {
             g = J.sorted_ids[k];
-            rec = J.rec_start[g];
+            // GSR_SLOT_LOCAL: the instance's index inside its Gaussian's rect is stored instead of the
+            // absolute record slot (render_bwd adds emit_start[id], which it loads anyway): no
+            // dependent gather of the record start behind the id here
+            rec = GSR_SLOT_LOCAL ? 0u : J.rec_start[g];
         }
     }
     s.start[tid] = start;

@@ -749,11 +749,11 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         // only entries that contributed somewhere in the forward are read (43 % of the entries
         // below tmax contributed nowhere: their 48-B record gathers are skipped)
-        uint32_t es = 0;  // the Gaussian's first record slot (its record mask bit at the store)
+        uint32_t es = 0;  // the Gaussian's first record slot (its record mask bit, the slot at the store)
         if (m != 0) {
             const float4* r = a.splat + 3 * (size_t)id;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
-            if (GSR_REC_MASK) es = a.emit_start[id];
+            if (GSR_REC_MASK || GSR_SLOT_LOCAL) es = a.emit_start[id];
             s_rec[0][lane] = r0;
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;
@@ -847,7 +847,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // one 48-B record per contributing entry, stored by its own lane
         if (m != 0) {
-            float* rec = a.grad_inst + (size_t)myslot * GRAD_REC;
+            const uint32_t slot = GSR_SLOT_LOCAL ? es + myslot : myslot;  // (BIN_SLOT: the index in the rect)
+            float* rec = a.grad_inst + (size_t)slot * GRAD_REC;
             float t[GF_NUM];
 #pragma unroll
             for (int f = 0; f < GF_NUM; f++) t[f] = s_acc[0][f][lane] + s_acc[1][f][lane];
@@ -857,9 +858,9 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
             // then finds the records without a dependent load of the valid words), else in the valid
             // words: one atomic per record either way
-            const uint32_t local = myslot - es;
+            const uint32_t local = slot - es;
             if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
-            else atomicOr(&a.valid[myslot >> 5], 1u << (myslot & 31u));
+            else atomicOr(&a.valid[slot >> 5], 1u << (slot & 31u));
         }
         __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
     }

@@ -576,7 +576,14 @@ class SparseGaussianAdam(torch.optim.Adam):
         super().__init__(params=params, lr=lr, eps=eps)
 
     @torch.no_grad()
-    def step(self, visibility, N):
+    def step(self, visibility, N, rows=None):
+        """rows = (g0, g1): update only Gaussians [g0, g1) (visibility and every parameter restricted
+        to those rows) -- the multi-GPU trainer steps each Gaussian range as soon as its gradient
+        all-reduce has landed (multiview.DataParallelTrainer.reduce_and_step)."""
+        if rows is not None:
+            g0, g1 = int(rows[0]), int(rows[1])
+            if not 0 <= g0 <= g1 <= int(N):
+                raise RuntimeError(f"rows {rows} outside [0, {int(N)})")
         batch = []
         for group in self.param_groups:
             lr = group["lr"]
@@ -593,5 +600,11 @@ class SparseGaussianAdam(torch.optim.Adam):
                 state["exp_avg_sq"] = torch.zeros_like(param, memory_format=torch.preserve_format)
             if param.numel() != (param.numel() // N) * N:
                 raise RuntimeError(f"parameter of {param.numel()} elements is not N = {N} rows")
-            batch.append((param, param.grad, state["exp_avg"], state["exp_avg_sq"], lr, eps))
-        _C.adam_update_groups(batch, visibility, 0.9, 0.999, N)
+            ts = (param, param.grad, state["exp_avg"], state["exp_avg_sq"])
+            if rows is not None:  # the rows of Gaussians [g0, g1): contiguous slices of each tensor
+                ts = tuple(t.view(int(N), -1)[g0:g1] for t in ts)
+            batch.append(ts + (lr, eps))
+        if rows is None:
+            _C.adam_update_groups(batch, visibility, 0.9, 0.999, N)
+        elif g1 > g0:
+            _C.adam_update_groups(batch, visibility[g0:g1], 0.9, 0.999, g1 - g0)

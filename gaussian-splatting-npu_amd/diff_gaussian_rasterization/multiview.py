@@ -309,9 +309,12 @@ class DataParallelTrainer:
     """
 
     def __init__(self, raw, lr=None, optimizer="sparse_adam", lambda_dssim=0.2, bg=None, group=None, batched=True,
-                 seed=0, exposures=None, spatial_lr_scale=None, opt=None):
+                 seed=0, exposures=None, spatial_lr_scale=None, opt=None, pipeline_chunks=4):
         import diff_gaussian_rasterization as dgr
         self._dgr = dgr
+        # > 1 (sparse Adam, several ranks): the gradient all-reduce and the optimizer step pipelined
+        # over this many Gaussian ranges (reduce_and_step) in iterations without densification
+        self.pipeline_chunks = pipeline_chunks
         dev = raw["xyz"].device
         self.device = dev
         self.group = group
@@ -515,9 +518,45 @@ class DataParallelTrainer:
                 g["lr"] = self.xyz_schedule(iteration)
                 return g["lr"]
 
+    def _pipelined(self):
+        return (self.sparse and self.pipeline_chunks > 1 and not self._skip_step and dist.is_initialized()
+                and dist.get_world_size(self.group) > 1)
+
+    @torch.no_grad()
+    def reduce_and_step(self, chunks=None):
+        """Steps 3 + 4 pipelined over Gaussian ranges: every range's
+        rows of each gradient and of the visibility counts go to an asynchronous all_reduce(SUM) at
+        once; then, range by range, the optimizer waits for that range's collectives only and runs
+        SparseGaussianAdam on its rows -- range k's update runs while range k+1 is still being
+        reduced.  Bit-identical to reduce() + optimizer_step(): the same sums, a row-wise update.
+        (Iterations that densify or reset opacities keep the unpipelined order: the reference
+        densifies between the reduction and the step.)"""
+        P = self.P
+        chunks = max(1, min(chunks or self.pipeline_chunks, P))
+        bounds = [(P * k // chunks, P * (k + 1) // chunks) for k in range(chunks)]
+        works = []
+        for g0, g1 in bounds:
+            w = [dist.all_reduce(self.params[k].grad.view(P, -1)[g0:g1], op=dist.ReduceOp.SUM, group=self.group,
+                                 async_op=True) for k in TRAIN_GROUPS]
+            w.append(dist.all_reduce(self.visible_count[g0:g1], op=dist.ReduceOp.SUM, group=self.group,
+                                     async_op=True))
+            works.append(w)
+        if self.exposures is not None:
+            dist.all_reduce(self.exposures.grad, op=dist.ReduceOp.SUM, group=self.group)
+            self.exposure_optimizer.step()
+        visible = torch.empty((P,), dtype=torch.bool, device=self.device)  # (each range's rows after its reduction)
+        for (g0, g1), w in zip(bounds, works):
+            for x in w:
+                x.wait()
+            visible[g0:g1] = self.visible_count[g0:g1] > 0
+            self.optimizer.step(visible, P, rows=(g0, g1))
+
     def step(self, views, depth_weight=0.0):
         self.zero_grad()
         losses = self.render_and_backward(views, depth_weight)
+        if self._pipelined():
+            self.reduce_and_step()
+            return losses
         self.reduce()
         self.optimizer_step()
         return losses
@@ -532,6 +571,12 @@ class DataParallelTrainer:
         self.zero_grad()
         track = iteration < o.densify_until_iter
         losses = self.render_and_backward(views, self.depth_l1_weight(iteration), track_stats=track)
+        densify = track and ((iteration > o.densify_from_iter and iteration % o.densification_interval == 0) or
+                             iteration % o.opacity_reset_interval == 0 or
+                             (white_background and iteration == o.densify_from_iter))
+        if not densify and self._pipelined():
+            self.reduce_and_step()
+            return losses, None
         self.reduce()
         did = None
         if track:

@@ -7,7 +7,9 @@ after ITERS steps of train.py's iteration (sparse Adam, L1 + D-SSIM, separate-DC
 parameters of both ranks must be bit-identical to each other AND to a single process that renders
 the same views and sums the two ranks' gradient buffers itself (x0 + x1: a two-rank all-reduce adds
 each element once, and float addition commutes), and the reduced densification statistics must
-equal the single process's.
+equal the single process's.  The ranks run the pipelined reduction (DataParallelTrainer.
+reduce_and_step: each Gaussian range's all-reduce followed by its sparse-Adam rows), the single
+process the unpipelined optimizer step: bit-identical.
 """
 import contextlib
 import os
