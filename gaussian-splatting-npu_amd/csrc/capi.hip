@@ -597,7 +597,9 @@ static TileSortJob fused_tile_sort_job(char* gb, char* bb, char* ib, int P, int 
     j.v0 = reinterpret_cast<uint32_t*>(w + 4 * q);  // u32x2 payloads
     j.v1 = reinterpret_cast<uint32_t*>(w + 6 * q);
     j.scratch = bb + b.off[BIN_RADIX_SCRATCH];
-    j.out_slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
+    j.slotless = slots_from_rect((uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X),
+                                 (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y));
+    j.out_slot = j.slotless ? nullptr : at<uint32_t>(bb, b.off[BIN_SLOT]);
     j.out_ids = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
     j.out_tiles = diff ? nullptr : at<uint32_t>(bb, b.off[BIN_SORTED_TILES]);
     j.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
@@ -1017,7 +1019,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = R > 0 ? at<float>(bb, b.off[BIN_GRAD_INST]) : nullptr;
-    r.slot = R > 0 ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
+    r.slot = R > 0 && !slots_from_rect(gx, gy) ? at<uint32_t>(bb, b.off[BIN_SLOT]) : nullptr;
     r.valid = R > 0 ? at<uint32_t>(bb, b.off[BIN_VALID]) : nullptr;
     r.hit = R > 0 ? at<uint8_t>(bb, b.off[BIN_HIT]) : nullptr;
     r.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);
@@ -1115,7 +1117,7 @@ static RenderBwdArgs render_bwd_args(int P, int R, const float* background, int 
     r.dL_dpixels = dL_dpix;
     r.dL_invdepths = dL_invdepths;
     r.grad_inst = at<float>(bb, b.off[BIN_GRAD_INST]);
-    r.slot = at<uint32_t>(bb, b.off[BIN_SLOT]);
+    r.slot = slots_from_rect(gx, gy) ? nullptr : at<uint32_t>(bb, b.off[BIN_SLOT]);  // (render_bwd derives them)
     r.valid = at<uint32_t>(bb, b.off[BIN_VALID]);
     r.hit = at<uint8_t>(bb, b.off[BIN_HIT]);
     r.emit_start = at<uint32_t>(gb, g.off[GEOM_EMIT_START]);

@@ -166,7 +166,8 @@ enum GeomArray {
     GEOM_RGB,             // f32[3P]
     GEOM_TILES_TOUCHED,   // u32[P]
     GEOM_POINT_OFFSETS,   // u32[P] inclusive scan of tiles_touched in depth order
-    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, 0} {ka, kb, kc, opacity} {r, g, b, 1/depth}
+    GEOM_SPLAT,           // f32x12[P] render record: {x, y, cullK, packed rect bits (0 on grids of more than
+                          // 255 tiles per axis)} {ka, kb, kc, opacity} {r, g, b, 1/depth}
                           // (ka, kb, kc) = -log2(e) * (a/2, b, c/2) of the conic; cullK scaled by log2(e)/2
     GEOM_DKEY,            // u32[P] depth-sort key: depth bits, 0xFFFFFFFF if culled
     GEOM_SORTED_IDS,      // u32[P] Gaussian ids in (depth bits, index) order
@@ -250,6 +251,23 @@ constexpr int TILE_DIFF_MAX_CELLS = 8704;
 #ifndef GSR_SLOT_LOCAL
 #define GSR_SLOT_LOCAL 1
 #endif
+// on grids of packed rects (rect_packable): no record slots at all -- render_bwd derives an instance's
+// index in its Gaussian's rect from the packed rect preprocess stores in the render record's free word
+// (SPLAT word 3) and the tile, and the tile sort moves 4 B per instance instead of 8
+#ifndef GSR_SLOT_RECT
+#define GSR_SLOT_RECT 1
+#endif
+__host__ __device__ inline bool slots_from_rect(uint32_t grid_x, uint32_t grid_y)
+{
+    return GSR_SLOT_LOCAL && GSR_SLOT_RECT && rect_packable(grid_x, grid_y);
+}
+// the instance of tile (tx, ty) in the packed rect r: its index in the rect's y-major order
+// (duplicateWithKeys, rasterizer_impl.cu:98-109)
+__host__ __device__ inline uint32_t rect_local(uint32_t r, uint32_t tx, uint32_t ty)
+{
+    const uint32_t x0 = r & 0xFFu, y0 = (r >> 8) & 0xFFu, x1 = (r >> 16) & 0xFFu;
+    return (ty - y0) * (x1 - x0) + (tx - x0);
+}
 __host__ __device__ inline bool use_tile_diff(uint32_t grid_x, uint32_t grid_y)
 {
     return GSR_TILE_DIFF && rect_packable(grid_x, grid_y) && (grid_x + 1) * (grid_y + 1) <= (uint32_t)TILE_DIFF_MAX_CELLS &&

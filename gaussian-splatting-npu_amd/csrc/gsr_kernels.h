@@ -256,6 +256,7 @@ struct TileSortJob {
     uint32_t* out_tiles;          // BIN_SORTED_TILES
     uint32_t* valid;              // BIN_VALID, cleared
     uint2* ranges;                // IMG_RANGES, cleared
+    bool slotless;                // slots_from_rect: no record slots written (render_bwd derives them)
 };
 size_t fused_pass1_scratch_bytes(int P);
 // phases: FUSED_COUNT = the first pass's histogram and row scan (needs neither L nor the binning

@@ -216,7 +216,8 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     constexpr float LOG2E = 1.4426950408889634f;
     if (cullK >= 0.f && cullK < 1.0e37f) cullK = cullK * (0.5f * LOG2E);
     float4* sp = a.splat + 3 * (size_t)idx;
-    sp[0] = make_float4(pix_x, pix_y, cullK, 0.0f);
+    // (word 3: the packed tile rect, from which render_bwd derives an instance's record slot)
+    sp[0] = make_float4(pix_x, pix_y, cullK, a.rect4 ? __uint_as_float(rect_pack(rminx, rminy, rmaxx, rmaxy)) : 0.0f);
     sp[1] = make_float4((-0.5f * LOG2E) * conic_x, (-LOG2E) * conic_y, (-0.5f * LOG2E) * conic_z, opacity);
     sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
 }

@@ -546,7 +546,15 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
     const uint64_t lt = (1ull << lane) - 1ull;
     // issue every load of the chunk before the first ballot (unconditional, clamped addresses)
     auto gidx = [&](int i) { return base + (size_t)min(w * (ITEMS * 64) + i * 64 + lane, nvalid - 1); };
-    if (PAIR && a.key_hi_shift) {  // the key rides in the payload's high bits
+    if (!PAIR && a.key_hi_shift) {  // one-word payload whose high bits hold the key
+#pragma unroll
+        for (int i = 0; i < ITEMS; i++) {
+            if constexpr (!PAIR) {
+                val[i] = a.vals_in[gidx(i)];
+                key[i] = val[i] >> a.key_hi_shift;
+            }
+        }
+    } else if (PAIR && a.key_hi_shift) {  // the key rides in the payload's high bits
         if (a.vals_in_y) {
 #pragma unroll
             for (int i = 0; i < ITEMS; i++) {
@@ -564,7 +572,7 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) key[i] = a.keys_in[gidx(i)];
     }
-    if (PAIR && a.key_hi_shift) {
+    if (a.key_hi_shift) {
     } else if (PAIR && a.rects4_in) {  // first pass of a rect-carrying sort: (index, packed rect)
 #pragma unroll
         for (int i = 0; i < ITEMS; i++) {
@@ -657,7 +665,7 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
                         a.sorted_counts[dst] = ((rc.y & 0xFFFFu) - (rc.x & 0xFFFFu)) * ((rc.y >> 16) - (rc.x >> 16));
                     }
                 } else {
-                    if (a.out_x) a.out_x[dst] = v;
+                    if (a.out_x) a.out_x[dst] = a.key_hi_shift ? v & ((1u << a.key_hi_shift) - 1u) : v;
                     if (a.rects) {
                         const uint2 rc = a.rects[v];
                         a.sorted_rects[dst] = rc;
@@ -974,8 +982,8 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
                 const uint2 v = make_uint2(s.rec[j] + local, s.g[j]);
 #endif
                 if (J.pack_shift) {
-                    if (J.soa_x) {
-                        J.soa_x[dst] = v.x;
+                    if (J.soa_y) {
+                        if (J.soa_x) J.soa_x[dst] = v.x;  // (no slot array: slots_from_rect)
                         J.soa_y[dst] = v.y | ((k >> J.pack_w1) << J.pack_shift);
                     } else {
                         J.vals_out[dst] = make_uint2(v.x, v.y | ((k >> J.pack_w1) << J.pack_shift));
@@ -984,7 +992,7 @@ __global__ void __launch_bounds__(RS_THREADS) fused_pass1_scatter_kernel(const V
                     J.keys_out[dst] = k;
                     J.vals_out[dst] = v;
                 } else {
-                    J.out_slot[dst] = v.x;
+                    if (J.out_slot) J.out_slot[dst] = v.x;
                     J.out_ids[dst] = v.y;
                     if (J.out_tiles) J.out_tiles[dst] = k;
                 }
@@ -1210,9 +1218,10 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             kin[v] = jobs[v0 + v].keys_in;
             vin[v] = reinterpret_cast<const uint32_t*>(jobs[v0 + v].pairs);
             // keys carried in the pairs' high bits: one pass only (the bits hold one digit)
-            if (jobs[v0 + v].key_hi_shift && (npass != 1 || !(jobs[v0 + v].pairs || jobs[v0 + v].soa_x)))
+            if (jobs[v0 + v].key_hi_shift && (npass != 1 || !(jobs[v0 + v].pairs || jobs[v0 + v].soa_y)))
                 return hipErrorInvalidValue;
             if (jobs[v0 + v].soa_x) vin[v] = jobs[v0 + v].soa_x;
+            else if (jobs[v0 + v].soa_y) vin[v] = jobs[v0 + v].soa_y;  // one-word payload
         }
         int shift = shift0;
         for (int p = 0; p < npass; p++) {
@@ -1362,11 +1371,11 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
                 a.pack_shift = 32 - (nbits - w1);
                 a.keys_out = nullptr;
                 if (GSR_TILE_SOA) {  // the v1 ping-pong region (8 B per instance) as two 4-B arrays
-                    a.soa_x = j.v1;
+                    a.soa_x = j.slotless ? nullptr : j.v1;
                     a.soa_y = j.v1 + align_up(4 * (size_t)(j.L > 0 ? j.L : 0), 256) / 4;
                 }
             }
-            a.out_slot = j.out_slot;
+            a.out_slot = j.slotless ? nullptr : j.out_slot;
             a.out_ids = j.out_ids;
             a.out_tiles = j.out_tiles;
             a.valid = j.valid;
@@ -1376,10 +1385,11 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
             rest[v] = {j.L, a.pack_shift ? nullptr : j.k1, reinterpret_cast<const uint2*>(j.v1), j.k0, j.v0, j.k1, j.v1,
                        j.out_slot, j.out_ids, j.out_tiles, j.scratch, nullptr, nullptr, nullptr};
             rest[v].key_hi_shift = a.pack_shift;
-            if (a.soa_x) {
+            if (a.soa_y) {  // (slotless: the id words alone, a one-word payload)
                 rest[v].pairs = nullptr;
                 rest[v].soa_x = a.soa_x;
                 rest[v].soa_y = a.soa_y;
+                if (!a.soa_x) rest[v].out_x = j.out_ids, rest[v].out_y = nullptr;
             }
             packed = a.pack_shift != 0;
         }

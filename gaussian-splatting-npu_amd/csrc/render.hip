@@ -736,15 +736,16 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     uint32_t next_id = 0, next_slot = 0, next_hit = 0;
     if (tmax > 0) {
         next_id = a.point_list[range.x + min(pfirst + lane, last)];
-        next_slot = a.slot[range.x + min(pfirst + lane, last)];
+        if (a.slot) next_slot = a.slot[range.x + min(pfirst + lane, last)];
         next_hit = a.hit[range.x + min(pfirst + lane, last)];
     }
     for (int p0 = pfirst; p0 >= 0; p0 -= 64) {
         const int pos_l = p0 + lane;  // this lane's entry; lane order = list order
-        const uint32_t id = next_id, myslot = next_slot, hit = next_hit;
+        const uint32_t id = next_id, hit = next_hit;
+        uint32_t myslot = next_slot;  // (without a.slot: from the record's packed rect, below)
         const int pn = max(p0 - 64, 0) + lane;  // (the first batch re-reads itself: never used)
         next_id = a.point_list[range.x + pn];
-        next_slot = a.slot[range.x + pn];
+        if (a.slot) next_slot = a.slot[range.x + pn];
         next_hit = a.hit[range.x + pn];
         const uint32_t m = pos_l < (int)tmax ? hit : 0u;
         // only entries that contributed somewhere in the forward are read (43 % of the entries
@@ -754,6 +755,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             const float4* r = a.splat + 3 * (size_t)id;
             const float4 r0 = r[0], r1 = r[1], r2 = r[2];
             if (GSR_REC_MASK || GSR_SLOT_LOCAL) es = a.emit_start[id];
+            if (!a.slot) myslot = rect_local(__float_as_uint(r0.w), tx, ty);
             s_rec[0][lane] = r0;
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;

@@ -108,7 +108,11 @@ def test_python_surface():
     import inspect
     assert issubclass(dgr.SparseGaussianAdam, __import__("torch").optim.Adam)
     assert "dc" in inspect.signature(dgr.GaussianRasterizer.forward).parameters
-    assert list(inspect.signature(dgr.SparseGaussianAdam.step).parameters) == ["self", "visibility", "N"]
+    # the reference's step(visibility, N); `rows` (a Gaussian range, for the pipelined data-parallel
+    # step) is an optional extra
+    params = inspect.signature(dgr.SparseGaussianAdam.step).parameters
+    assert list(params)[:3] == ["self", "visibility", "N"]
+    assert all(p.default is not inspect.Parameter.empty for p in list(params.values())[3:])
     assert dgr.GaussianRasterizationSettings._fields == (
         "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
         "sh_degree", "campos", "prefiltered", "debug", "antialiasing")
