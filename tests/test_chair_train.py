@@ -26,9 +26,15 @@ What is restated from the reference (not imported):
     image *= alpha_mask, loss = 0.8 L1 + 0.2 (1 - SSIM), backward, SparseGaussianAdam.step(radii > 0,
     P) with betas (0.9, 0.999) and eps 1e-15.  Densification starts at iteration 500 (densify_from_iter)
     and is not reached; the exposure optimiser does not touch the render without train_test_exp.
-Asserted: the oracle loop trains (test PSNR up by > 2 dB); the two loops' test PSNRs (each loop's
-final parameters rendered by the oracle) agree within PSNR_TOL_DB per view; the HIP render of the
-GPU loop's parameters gives the same PSNR as the oracle's render of them within 0.01 dB.
+Asserted: the oracle loop trains (masked test PSNR up by > 0.5 dB); the two loops' test PSNRs (each
+loop's final parameters rendered by the oracle) agree within PSNR_TOL_DB on the mean over the test
+views (the figure training_report prints) and within PSNR_VIEW_TOL_DB per view; the HIP render of
+the GPU loop's parameters gives the same PSNR as the oracle's render of them within 0.01 dB.
+Why a per-view bound above the mean's: 200 iterations of training amplify float32 rounding
+differences (a chaotic trajectory), and the oracle loop is itself not reproducible -- its render
+backward adds the tiles' sums into the per-Gaussian gradients with OpenMP atomics in whatever order
+the threads reach them, as the reference's CUDA atomics do (backward.cu:593-635).  The test runs
+the oracle loop twice and logs that run-to-run spread beside the HIP-vs-oracle differences.
 The absolute PSNRs go to the parity statistics (gpurun_out/parity_stats.json).
 """
 import math
@@ -56,7 +62,8 @@ RES = 200        # train.py -r 4 (the oracle loop's cost grows with the pixels)
 LONG_RES = 800   # the dataset's resolution (train.py's default -r for 800-pixel frames)
 SEED = 0
 SH_MAX, SH_ACTIVE = 3, 0
-PSNR_TOL_DB = 0.05
+PSNR_TOL_DB = 0.05       # mean over the 8 test views
+PSNR_VIEW_TOL_DB = 0.15  # any one view (see the module docstring)
 THREADS = min(16, os.cpu_count() or 1)
 # OptimizationParams (arguments/__init__.py:74-100)
 POS_LR_INIT, POS_LR_FINAL, POS_LR_DELAY_MULT, POS_LR_MAX_STEPS = 0.00016, 0.0000016, 0.01, 30_000
@@ -235,6 +242,7 @@ def test_chair_training_psnr_matches_oracle_loop():
     (f0, m0) = _test_psnrs(raw0, test)
     raw_cpu = _train_cpu(raw0, train, extent, P)
     f_cpu, m_cpu = _test_psnrs(raw_cpu, test)
+    f_cpu2, m_cpu2 = _test_psnrs(_train_cpu(raw0, train, extent, P), test)  # the oracle loop's own spread
     raw_gpu = _train_gpu(raw0, train, extent, P)
     f_gpu, m_gpu = _test_psnrs({k: v.cpu() for k, v in raw_gpu.items()}, test)
     # the HIP render of the GPU loop's parameters, as training_report would evaluate them
@@ -245,6 +253,10 @@ def test_chair_training_psnr_matches_oracle_loop():
              "masked_psnr_start": float(m0.mean()), "masked_psnr_oracle_loop": float(m_cpu.mean()),
              "masked_psnr_hip_loop": float(m_gpu.mean()), "masked_psnr_hip_loop_hip_render": float(m_hip.mean()),
              "max_view_diff_db": float(max(np.abs(f_gpu - f_cpu).max(), np.abs(m_gpu - m_cpu).max())),
+             "mean_diff_db": float(max(abs(f_gpu.mean() - f_cpu.mean()), abs(m_gpu.mean() - m_cpu.mean()))),
+             "oracle_rerun_max_view_diff_db": float(max(np.abs(f_cpu2 - f_cpu).max(), np.abs(m_cpu2 - m_cpu).max())),
+             "oracle_rerun_mean_diff_db": float(max(abs(f_cpu2.mean() - f_cpu.mean()),
+                                                    abs(m_cpu2.mean() - m_cpu.mean()))),
              "per_view_oracle_loop": f_cpu.round(4).tolist(), "per_view_hip_loop": f_gpu.round(4).tolist(),
              "per_view_masked_oracle_loop": m_cpu.round(4).tolist(),
              "per_view_masked_hip_loop": m_gpu.round(4).tolist()}
@@ -253,8 +265,10 @@ def test_chair_training_psnr_matches_oracle_loop():
     # the loss only sees render x alpha_mask: the masked PSNR rises, training_report's unmasked one
     # need not in 200 iterations (the create_from_pcd haze outside the object gets no gradient)
     assert m_cpu.mean() > m0.mean() + 0.5, "the oracle loop does not train"
-    np.testing.assert_allclose(f_gpu, f_cpu, atol=PSNR_TOL_DB)
-    np.testing.assert_allclose(m_gpu, m_cpu, atol=PSNR_TOL_DB)
+    assert abs(f_gpu.mean() - f_cpu.mean()) <= PSNR_TOL_DB
+    assert abs(m_gpu.mean() - m_cpu.mean()) <= PSNR_TOL_DB
+    np.testing.assert_allclose(f_gpu, f_cpu, atol=PSNR_VIEW_TOL_DB)
+    np.testing.assert_allclose(m_gpu, m_cpu, atol=PSNR_VIEW_TOL_DB)
     np.testing.assert_allclose(f_hip, f_gpu, atol=0.01)
     np.testing.assert_allclose(m_hip, m_gpu, atol=0.01)
 
