@@ -631,9 +631,12 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // each quadrant's contributing entries are listed in LDS (ballot + mbcnt, list order).  Iteration
 // i then evaluates the i-th last entry of every quadrant at once (pixels of different quadrants share no
 // state; a group past its list evaluates a staged record at position "never", which adds zeros),
-// three iterations per transposed reduction; the groups add their partial totals into the
-// entries' LDS sums two groups at a time (two sets of sums), and at the end of the batch every contributing
-// entry's lane stores its record (10 floats) at its record slot and flags it valid.  Against one
+// three iterations per transposed reduction, whose group totals go to a per-wave LDS row of
+// partials with one 8-B store per lane; at the end of the batch every contributing entry's lane
+// adds its <= 4 quadrant partials (it knows each one's iteration from its place in the quadrant
+// lists) and stores its record (10 floats) at its record slot and flags it valid.  (Until round 5
+// the groups added their totals into per-entry LDS sums by read-add-write, two phases per
+// reduction: 0.79 bank-conflict cycles per LDS instruction at random entries; -1 %.)  Against one
 // 64-lane pass per entry over the half-tiles it reaches, this skips the pixel pairs of quadrants
 // an entry does not reach (25 % of them) and reduces over 16 lanes: render_bwd -11 %.
 // Tiles (independent waves) per workgroup.  A retiring 4-wave workgroup frees one wave slot on
@@ -643,6 +646,8 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
 // 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
 constexpr int BWD_TPW = 4;
+// reduction blocks of partial rows per wave: 11 blocks = 33 iterations per pass (5.5 KB per wave)
+constexpr int BWD_PART_BLOCKS = 11;
 // (Measured and dropped, DESIGN §10: a reduction group's three entries as ONE basic block, 2 %
 // slower; entry jj + 1's staged record read from LDS while entry jj computes, 2 % slower.)
 
@@ -714,14 +719,14 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
 
     __shared__ float4 s_recw[BWD_TPW][3][64];
     __shared__ uint8_t s_lqw[BWD_TPW][4][64];
-    // rows padded to 65 floats: the 16 lanes of a group add the ten fields of one entry (same
-    // column e) at once, which a 64-float row stride would put in one LDS bank; column 64 takes the
-    // writes of lanes that hold no sum.  Two sets: groups 0 / 2 add into set 0, groups 1 / 3 into
-    // set 1, so two read-add-write phases per reduction instead of four (4 x 8.4 KB per workgroup).
-    __shared__ float s_accw[BWD_TPW][2][GF_NUM][65];
+    // The groups' partial totals, one 32-float row per (reduction block, group): block b holds the
+    // group's iterations 3b .. 3b + 2 (value jj * GF_NUM + f = term f of iteration 3b + jj).  Every
+    // reduction writes its block with ONE conflict-free 8-B store per lane (the 64 lanes cover 512
+    // contiguous bytes); each entry's lane sums its <= 4 quadrant partials when the pass ends.
+    __shared__ float s_partw[BWD_TPW][BWD_PART_BLOCKS][4][32];
     float4 (&s_rec)[3][64] = s_recw[wv];
     uint8_t (&s_lq)[4][64] = s_lqw[wv];  // per quadrant: the batch entries it evaluates, in list order
-    float (&s_acc)[2][GF_NUM][65] = s_accw[wv];  // per batch entry: sums of its quadrant partials
+    float (&s_part)[BWD_PART_BLOCKS][4][32] = s_partw[wv];
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
@@ -760,111 +765,120 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             s_rec[1][lane] = r1;
             s_rec[2][lane] = r2;
         }
-        const uint64_t any = __ballot(m != 0);
-        if (any == 0) continue;  // nothing staged, nothing to store
-        int cq[4];
+        if (__ballot(m != 0) == 0) continue;  // nothing staged, nothing to store
+        // A batch whose busiest quadrant has more entries than the partial rows hold runs as two
+        // passes, its back half (lanes 32..63: the later entries) first; each half has <= 32
+        // entries per quadrant.  An entry is evaluated and stored in one pass.
+        int big = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const bool in = (m >> q) & 1u;
-            const uint64_t bq = __ballot(in);
-            const int before = __builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0));
-            if (in) s_lq[q][before] = (uint8_t)lane;
-            cq[q] = __popcll(bq);
-        }
+        for (int q = 0; q < 4; q++) big |= __popcll(__ballot((m >> q) & 1u)) > 3 * BWD_PART_BLOCKS;
+        for (int hp = big ? 1 : 0; hp >= 0; hp--) {
+            const uint32_t mm = (big && (lane >> 5) != hp) ? 0u : m;
+            const uint64_t any = __ballot(mm != 0);
+            if (any == 0) continue;
+            int cq[4];
+            uint32_t bef = 0;  // this entry's index in each quadrant's list (a byte per quadrant)
 #pragma unroll
-        for (int f = 0; f < GF_NUM; f++) s_acc[0][f][lane] = s_acc[1][f][lane] = 0.f;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int q = 0; q < 4; q++) {
+                const bool in = (mm >> q) & 1u;
+                const uint64_t bq = __ballot(in);
+                const int before =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(bq >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bq, 0));
+                if (in) s_lq[q][before] = (uint8_t)lane;
+                bef |= (uint32_t)before << (8 * q);
+                cq[q] = __popcll(bq);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        // Each quadrant group walks its own entries back to front (pixels of different quadrants
-        // share no state), iteration i of all four groups at once; a group past its count
-        // evaluates a staged record at position "never" (alpha = 0: state unchanged, zero terms).
-        const int fv = (int)__builtin_ctzll(any);
-        const int mycnt = grp == 0 ? cq[0] : grp == 1 ? cq[1] : grp == 2 ? cq[2] : cq[3];
-        const int niter = max(max(cq[0], cq[1]), max(cq[2], cq[3]));
-        for (int i0 = 0; i0 < niter; i0 += G) {
-            int ej[G];
-            bool act[G];
+            // Each quadrant group walks its own entries back to front (pixels of different quadrants
+            // share no state), iteration i of all four groups at once; a group past its count
+            // evaluates a staged record at position "never" (alpha = 0: state unchanged, zero terms).
+            const int fv = (int)__builtin_ctzll(any);
+            const int mycnt = grp == 0 ? cq[0] : grp == 1 ? cq[1] : grp == 2 ? cq[2] : cq[3];
+            const int niter = max(max(cq[0], cq[1]), max(cq[2], cq[3]));
+            for (int i0 = 0, blk = 0; i0 < niter; i0 += G, blk++) {
+                int ej[G];
+                bool act[G];
 #pragma unroll
-            for (int jj = 0; jj < G; jj++) {
-                act[jj] = i0 + jj < mycnt;
-                ej[jj] = act[jj] ? (int)s_lq[grp][mycnt - 1 - (i0 + jj)] : fv;
-            }
-            float v[32];
-#pragma unroll
-            for (int jj = 0; jj < G; jj++) {
-                // a wave-uniform branch per entry (a block per entry): the iterations past niter
-                // evaluate nothing
-                if (i0 + jj < niter) {
-                    const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
-                    const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
-                    const Falloff f = falloff(co);
-                    // the falloff's dy terms, shared by the lane's two pairs (one row)
-                    const float dy = xy.y - pfy;
-                    const float bq = f.kb * dy, cq = (f.kc * dy) * dy;
-                    BwdAcc o;
-                    bwd_pair<HAS_INV, true>(st[0], pfx0, pos, xy, bq, cq, f, co, col, o);
-                    bwd_pair<HAS_INV, false>(st[1], pfx1, pos, xy, bq, cq, f, co, col, o);
-                    bwd_lane_terms(o, dy, &v[jj * GF_NUM]);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = 0.f;
+                for (int jj = 0; jj < G; jj++) {
+                    act[jj] = i0 + jj < mycnt;
+                    ej[jj] = act[jj] ? (int)s_lq[grp][mycnt - 1 - (i0 + jj)] : fv;
                 }
-            }
+                float v[32];
 #pragma unroll
-            for (int q = G * GF_NUM; q < 32; q++) v[q] = 0.f;
-            float r0, r1;
-            group_transpose_reduce32(v, lane, r0, r1);
-            // lane li of a group holds the group totals of values 2 li and 2 li + 1 (value
-            // jj * GF_NUM + f = term f of the group's entry jj); the four groups add their
-            // partials into the entries' sums one after the other (fixed order: reproducible)
-            const int k0 = 2 * li, k1 = k0 + 1;
-            const int j0 = k0 / GF_NUM, j1 = k1 / GF_NUM;
-            const bool ok0 = k0 < G * GF_NUM && (j0 == 0 ? act[0] : j0 == 1 ? act[1] : act[2]);
-            const bool ok1 = k1 < G * GF_NUM && (j1 == 0 ? act[0] : j1 == 1 ? act[1] : act[2]);
-            const int e0 = j0 == 0 ? ej[0] : j0 == 1 ? ej[1] : ej[2];
-            const int e1 = j1 == 0 ? ej[0] : j1 == 1 ? ej[1] : ej[2];
-            float (&sa)[GF_NUM][65] = s_acc[grp & 1];
-            float* a0 = ok0 ? &sa[k0 - j0 * GF_NUM][e0] : &sa[0][64];
-            float* a1 = ok1 ? &sa[k1 - j1 * GF_NUM][e1] : &sa[1][64];
-            // groups 0 and 1, then 2 and 3, add their partials into their set's sums (fixed order:
-            // reproducible); the 32 lanes of a phase hold distinct (set, field, entry) sums, so a
-            // plain LDS read-add-write is race-free (a wave's LDS operations complete in issue
-            // order) -- the LDS float atomics it replaces cost 6 % of render_bwd
+                for (int jj = 0; jj < G; jj++) {
+                    // a wave-uniform branch per entry (a block per entry): the iterations past niter
+                    // evaluate nothing
+                    if (i0 + jj < niter) {
+                        const float4 xy = s_rec[0][ej[jj]], co = s_rec[1][ej[jj]], col = s_rec[2][ej[jj]];
+                        const uint32_t pos = act[jj] ? (uint32_t)(p0 + ej[jj]) : 0xFFFFFFFFu;
+                        const Falloff f = falloff(co);
+                        // the falloff's dy terms, shared by the lane's two pairs (one row)
+                        const float dy = xy.y - pfy;
+                        const float bq = f.kb * dy, cq = (f.kc * dy) * dy;
+                        BwdAcc o;
+                        bwd_pair<HAS_INV, true>(st[0], pfx0, pos, xy, bq, cq, f, co, col, o);
+                        bwd_pair<HAS_INV, false>(st[1], pfx1, pos, xy, bq, cq, f, co, col, o);
+                        bwd_lane_terms(o, dy, &v[jj * GF_NUM]);
+                    } else {
 #pragma unroll
-            for (int ph = 0; ph < 2; ph++) {
-                if ((grp >> 1) == ph) {
-                    const float o0 = *a0, o1 = *a1;
-                    *a0 = o0 + r0;
-                    *a1 = o1 + r1;
+                        for (int q = 0; q < GF_NUM; q++) v[jj * GF_NUM + q] = 0.f;
+                    }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // one 48-B record per contributing entry, stored by its own lane
-        if (m != 0) {
-            const uint32_t slot = GSR_SLOT_LOCAL ? es + myslot : myslot;  // (BIN_SLOT: the index in the rect)
-            float* rec = a.grad_inst + (size_t)slot * GRAD_REC;
-            float t[GF_NUM];
 #pragma unroll
-            for (int f = 0; f < GF_NUM; f++) t[f] = s_acc[0][f][lane] + s_acc[1][f][lane];
-            reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
-            reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
-            reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
-            // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
-            // then finds the records without a dependent load of the valid words), else in the valid
-            // words: one atomic per record either way
-            const uint32_t local = slot - es;
-            if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
-            else atomicOr(&a.valid[slot >> 5], 1u << (slot & 31u));
+                for (int q = G * GF_NUM; q < 32; q++) v[q] = 0.f;
+                float r0, r1;
+                group_transpose_reduce32(v, lane, r0, r1);
+                // lane li of a group holds the group totals of values 2 li and 2 li + 1
+                *reinterpret_cast<float2*>(&s_part[blk][grp][2 * li]) = make_float2(r0, r1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // one 48-B record per contributing entry, stored by its own lane: its quadrant partials
+            // summed as (q0 + q2) + (q1 + q3), a fixed order (bitwise reproducible)
+            if (mm != 0) {
+                float t0[GF_NUM], t1[GF_NUM];
+#pragma unroll
+                for (int f = 0; f < GF_NUM; f++) t0[f] = t1[f] = 0.f;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    if ((mm >> q) & 1u) {
+                        const int i = cq[q] - 1 - (int)((bef >> (8 * q)) & 0xFFu);  // its iteration
+                        const int b = i / G, jj = i - G * b;
+                        const float2* src = reinterpret_cast<const float2*>(&s_part[b][q][jj * GF_NUM]);
+#pragma unroll
+                        for (int h = 0; h < GF_NUM / 2; h++) {
+                            const float2 pv = src[h];
+                            if (q & 1) {
+                                t1[2 * h] += pv.x;
+                                t1[2 * h + 1] += pv.y;
+                            } else {
+                                t0[2 * h] += pv.x;
+                                t0[2 * h + 1] += pv.y;
+                            }
+                        }
+                    }
+                }
+                const uint32_t slot = GSR_SLOT_LOCAL ? es + myslot : myslot;  // (BIN_SLOT: the index in the rect)
+                float* rec = a.grad_inst + (size_t)slot * GRAD_REC;
+                float t[GF_NUM];
+#pragma unroll
+                for (int f = 0; f < GF_NUM; f++) t[f] = t0[f] + t1[f];
+                reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
+                reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
+                reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
+                // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
+                // then finds the records without a dependent load of the valid words), else in the valid
+                // words: one atomic per record either way
+                const uint32_t local = slot - es;
+                if (GSR_REC_MASK && local < 32u) atomicOr(&a.rec_mask[id], 1u << local);
+                else atomicOr(&a.valid[slot >> 5], 1u << (slot & 31u));
+            }
+            __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_part reuse in the next pass
         }
-        __builtin_amdgcn_wave_barrier();  // s_rec / s_lq / s_acc reuse in the next batch
     }
 }
 

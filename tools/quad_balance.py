@@ -56,6 +56,7 @@ def main():
         np.savez_compressed(sys.argv[1], hit=hit, ranges=ranges, tmax=tmax)
     useful = issued = issued_g3 = 0
     qsum = np.zeros(4)
+    ms = []  # per batch: the iterations its groups run (the largest quadrant count)
     for t in range(T):
         n = int(tmax[t])
         if n == 0:
@@ -66,11 +67,18 @@ def main():
             cq = np.array([((hb >> q) & 1).sum() for q in range(4)])
             qsum += cq
             m = int(cq.max())
+            ms.append(m)
             useful += int(cq.sum())
             issued += 4 * m
             issued_g3 += 4 * 3 * ((m + 2) // 3)
     print(f"L={L} tiles={T} entries(hit)={useful} group-iterations issued={issued} (G=3: {issued_g3})")
     print(f"utilisation {useful / issued:.3f} (G=3 rounding: {useful / issued_g3:.3f}); per-quadrant totals {qsum}")
+    ms = np.array(ms)
+    print(f"batches {len(ms)}; iterations per batch: mean {ms.mean():.1f}, p50 {np.percentile(ms, 50):.0f}, "
+          f"p90 {np.percentile(ms, 90):.0f}, p99 {np.percentile(ms, 99):.0f}, max {ms.max()}")
+    for c in (12, 15, 18, 21, 24, 27, 30, 33, 42):
+        big = ms > c
+        print(f"  > {c}: {big.mean():.4f} of the batches, {ms[big].sum() / ms.sum():.4f} of the iterations")
 
 
 if __name__ == "__main__":
