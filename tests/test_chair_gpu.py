@@ -43,7 +43,7 @@ def test_chair_distcuda2_bit_exact(chair):
 def test_chair_case(chair, case):
     import diff_gaussian_rasterization as dgr
     from test_gpu_parity import _img_state
-    f, _, cases = chair
+    f, base, cases = chair
     cam, deg, aa, bg, seed, scene = cases[case]
     H, W, P = cam.image_height, cam.image_width, scene["means3D"].shape[0]
     o, og = make_chair.run_case(scene, cam, deg, aa, bg, seed, nthreads=min(16, os.cpu_count() or 1))
@@ -92,8 +92,11 @@ def test_chair_case(chair, case):
         cam.tanfovy, gc, gi, sc["shs"], deg, cp, geom, L, binning, img, aa, False)
     torch.cuda.synchronize()
     g64 = o.backward(gc.cpu(), gi.cpu(), f64=True)  # the accuracy yardstick (check_rel_truth)
+    perturbed = scene is not base  # cases 3 / 4: rotations and anisotropic scales
     for n, t in zip(make_chair.GRAD_NAMES, out):
         hip, ref = t.cpu().numpy(), og[n].reshape(t.shape)
+        if perturbed and n in ("dL_drotations", "dL_dscales"):  # the cov3D -> (scale, rotation) chain is live
+            assert np.count_nonzero(ref) > 0.01 * ref.size and np.count_nonzero(hip) > 0.01 * hip.size, n
         # outliers may sit in the walk of any decision suspect (a decision taken the other way that moved
         # the colour by less than IMG_ATOL: common.DECISION_ATOL), not only of a flipped pixel
         common.check_grad_attributed(f"{tag} {n}", hip, ref, suspect_rows)
