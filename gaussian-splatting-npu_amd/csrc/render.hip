@@ -647,12 +647,18 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
 constexpr int BWD_TPW = 4;
 // reduction blocks of partial rows per wave: 11 blocks = 33 iterations per pass (5.5 KB per wave)
-constexpr int BWD_PART_BLOCKS = 11;
+#ifndef GSR_BWD_PART_BLOCKS
+#define GSR_BWD_PART_BLOCKS 11
+#endif
+constexpr int BWD_PART_BLOCKS = GSR_BWD_PART_BLOCKS;
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 4  // waves per SIMD (VGPR budget)
+#endif
 // (Measured and dropped, DESIGN §10: a reduction group's three entries as ONE basic block, 2 %
 // slower; entry jj + 1's staged record read from LDS while entry jj computes, 2 % slower.)
 
 template <bool HAS_INV>
-__global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_eu(4))) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
+__global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES))) render_bwd_kernel(const ViewBatch<RenderBwdArgs> B)
 {
 #pragma clang fp contract(fast)
     const RenderBwdArgs& a = B.v[blockIdx.y];  // a batch of views: one launch tail per batch
