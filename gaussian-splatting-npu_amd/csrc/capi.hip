@@ -85,6 +85,11 @@ int pinned(int slot, uint32_t** out)
 // the other view's long kernels instead of behind them.  Buffers stay stream-ordered for the caller:
 // everything the prefix writes is joined into its stream before the entry point returns.
 // ---------------------------------------------------------------------------
+// the fork / join events order streams of one device only: no system-scope fence (the host never
+// inspects them; what the host reads -- num_rendered -- the scan stores with system-scope atomics)
+#ifndef GSR_EVENT_FLAGS
+#define GSR_EVENT_FLAGS (hipEventDisableTiming | hipEventDisableSystemFence)
+#endif
 constexpr int PREFIX_STREAMS = 4;  // views whose binning prefixes run side by side (gsr_forward_views)
 struct PrefixStream {
     hipStream_t s[PREFIX_STREAMS] = {};
@@ -95,22 +100,28 @@ struct PrefixStream {
 };
 constexpr int MAX_DEVICES = 64;
 thread_local PrefixStream g_prefix[MAX_DEVICES];
-thread_local bool g_prefix_off = false;  // gsr_set_prefix_stream(0): everything on the caller's stream
+// gsr_set_prefix_stream: 0 = everything on the caller's stream; 1 = the prefix on its own
+// high-priority stream (forked from the caller's, joined before render_fwd) and its side work on
+// the auxiliary stream; 2 = the prefix on the caller's stream, its side work on the auxiliary stream
+#ifndef GSR_PREFIX_MODE_DEFAULT
+#define GSR_PREFIX_MODE_DEFAULT 1
+#endif
+thread_local int g_prefix_mode = GSR_PREFIX_MODE_DEFAULT;
 
 // n (<= PREFIX_STREAMS) prefix streams of the current device, each forked from `caller`; all of
 // them the caller's own stream when the prefix streams are off (or the device is out of range).
 int prefix_fork(hipStream_t caller, int n, hipStream_t* out)
 {
     for (int k = 0; k < n; k++) out[k] = caller;
-    if (g_prefix_off) return GSR_OK;
+    if (g_prefix_mode != 1) return GSR_OK;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail_hip(e, __LINE__);
     if (dev < 0 || dev >= MAX_DEVICES) return GSR_OK;
     PrefixStream& ps = g_prefix[dev];
     if (!ps.fork) {
-        if ((e = hipEventCreateWithFlags(&ps.fork, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
-        if ((e = hipEventCreateWithFlags(&ps.join, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.fork, GSR_EVENT_FLAGS)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.join, GSR_EVENT_FLAGS)) != hipSuccess) return fail_hip(e, __LINE__);
     }
     if ((e = hipEventRecord(ps.fork, caller)) != hipSuccess) return fail_hip(e, __LINE__);
     for (int k = 0; k < n; k++) {
@@ -139,7 +150,7 @@ int current_device()
 int aux_fork(hipStream_t s, hipStream_t* out)
 {
     *out = s;
-    if (g_prefix_off) return GSR_OK;
+    if (g_prefix_mode == 0) return GSR_OK;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return fail_hip(e, __LINE__);
@@ -150,8 +161,8 @@ int aux_fork(hipStream_t s, hipStream_t* out)
         if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) != hipSuccess) return fail_hip(e, __LINE__);
         if ((e = hipStreamCreateWithPriority(&ps.aux, hipStreamNonBlocking, greatest)) != hipSuccess)
             return fail_hip(e, __LINE__);
-        if ((e = hipEventCreateWithFlags(&ps.aux_in, hipEventDisableTiming)) != hipSuccess) return fail_hip(e, __LINE__);
-        if ((e = hipEventCreateWithFlags(&ps.aux_out, hipEventDisableTiming)) != hipSuccess)
+        if ((e = hipEventCreateWithFlags(&ps.aux_in, GSR_EVENT_FLAGS)) != hipSuccess) return fail_hip(e, __LINE__);
+        if ((e = hipEventCreateWithFlags(&ps.aux_out, GSR_EVENT_FLAGS)) != hipSuccess)
             return fail_hip(e, __LINE__);
     }
     if ((e = hipEventRecord(ps.aux_in, s)) != hipSuccess) return fail_hip(e, __LINE__);
@@ -250,7 +261,8 @@ const char* gsr_version(void) { return "gsr-hip 0.1 gfx950"; }
 
 int gsr_set_prefix_stream(int on)
 {
-    g_prefix_off = on == 0;
+    if (on < 0 || on > 2) return fail(GSR_ERR_INVALID, "prefix stream mode must be 0, 1 or 2");
+    g_prefix_mode = on;
     return GSR_OK;
 }
 

@@ -370,9 +370,12 @@ int gsr_adam_update_multi(int n_groups, float* const* params, const float* const
                           const float* lrs, const float* epss, const bool* visible, float b1,
                           float b2, int N, gsr_stream_t stream);
 
-/* The forward's binning prefix (preprocess .. tile order) runs on an internal stream of the
- * highest priority, forked from and joined back into the caller's stream (on = 1, the
- * default); on = 0 puts every launch on the caller's stream.  Per host thread. */
+/* Where the forward's binning prefix (preprocess .. tile order) runs.  on = 1: on an internal
+ * stream of the highest priority, forked from and joined back into the caller's stream, its side
+ * work (record-slot scan, tile histogram, forward tile order) on a second internal stream;
+ * on = 2: on the caller's stream, the side work on the internal one (no join before render_fwd);
+ * on = 0: every launch on the caller's stream.  Other values: GSR_ERR_INVALID.  Per host
+ * thread; the default is the library's build-time GSR_PREFIX_MODE_DEFAULT. */
 int gsr_set_prefix_stream(int on);
 
 /* Debug / parity helper: writes the sorted 64-bit tile|depth keys
