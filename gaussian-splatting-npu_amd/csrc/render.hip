@@ -651,6 +651,11 @@ constexpr int BWD_TPW = 4;
 #define GSR_BWD_PART_BLOCKS 11
 #endif
 constexpr int BWD_PART_BLOCKS = GSR_BWD_PART_BLOCKS;
+#ifndef GSR_BWD_PART_STRIDE
+#define GSR_BWD_PART_STRIDE 132
+#endif
+constexpr int BWD_PART_STRIDE = GSR_BWD_PART_STRIDE;  // floats per block of partial rows (>= 4 x 32, even)
+static_assert(BWD_PART_STRIDE >= 128 && BWD_PART_STRIDE % 2 == 0, "partial rows: 4 groups x 32 values, 8-B aligned");
 #ifndef GSR_BWD_WAVES
 #define GSR_BWD_WAVES 4  // waves per SIMD (VGPR budget)
 #endif
@@ -729,10 +734,14 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
     // group's iterations 3b .. 3b + 2 (value jj * GF_NUM + f = term f of iteration 3b + jj).  Every
     // reduction writes its block with ONE conflict-free 8-B store per lane (the 64 lanes cover 512
     // contiguous bytes); each entry's lane sums its <= 4 quadrant partials when the pass ends.
-    __shared__ float s_partw[BWD_TPW][BWD_PART_BLOCKS][4][32];
+    // (blocks BWD_PART_STRIDE = 132 floats apart, not 128: an entry's lane reads its partial from
+    // block b at a lane-dependent b, and with a 128-float stride (0 mod the 64 banks) the up to 33
+    // lanes reading one quadrant's partials fell into 3 banks -- 11-way conflicts; 132 spreads them
+    // to 2 LDS cycles, the minimum for 64 lanes x 8 B)
+    __shared__ __attribute__((aligned(16))) float s_partw[BWD_TPW][BWD_PART_BLOCKS * BWD_PART_STRIDE];
     float4 (&s_rec)[3][64] = s_recw[wv];
     uint8_t (&s_lq)[4][64] = s_lqw[wv];  // per quadrant: the batch entries it evaluates, in list order
-    float (&s_part)[BWD_PART_BLOCKS][4][32] = s_partw[wv];
+    float* s_part = s_partw[wv];  // block b, group g, value k at b * BWD_PART_STRIDE + 32 g + k
 
     // Only the quadrants in which an entry contributed to some pixel in the forward (render_fwd's
     // a.hit bits: alpha >= 1/255 and the pixel not yet saturated, the tests this loop repeats per
@@ -838,7 +847,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                 float r0, r1;
                 group_transpose_reduce32(v, lane, r0, r1);
                 // lane li of a group holds the group totals of values 2 li and 2 li + 1
-                *reinterpret_cast<float2*>(&s_part[blk][grp][2 * li]) = make_float2(r0, r1);
+                *reinterpret_cast<float2*>(&s_part[blk * BWD_PART_STRIDE + 32 * grp + 2 * li]) = make_float2(r0, r1);
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -854,7 +863,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                     if ((mm >> q) & 1u) {
                         const int i = cq[q] - 1 - (int)((bef >> (8 * q)) & 0xFFu);  // its iteration
                         const int b = i / G, jj = i - G * b;
-                        const float2* src = reinterpret_cast<const float2*>(&s_part[b][q][jj * GF_NUM]);
+                        const float2* src =
+                            reinterpret_cast<const float2*>(&s_part[b * BWD_PART_STRIDE + 32 * q + jj * GF_NUM]);
 #pragma unroll
                         for (int h = 0; h < GF_NUM / 2; h++) {
                             const float2 pv = src[h];
