@@ -59,6 +59,18 @@ def test_version_and_error_string(lib):
     assert isinstance(lib.gsr_last_error(), bytes)
 
 
+def test_prefix_stream_modes(lib):
+    """gsr_set_prefix_stream takes 0 (caller's stream), 1 (prefix stream + auxiliary stream) and 2
+    (prefix on the caller's stream, side work on the auxiliary one); anything else is refused
+    (no GPU is touched: the mode is host state)."""
+    for mode in (0, 2, 1):
+        assert lib.gsr_set_prefix_stream(mode) == 0
+    for bad in (-1, 3):
+        assert lib.gsr_set_prefix_stream(bad) != 0
+        assert b"prefix stream mode" in lib.gsr_last_error()
+    assert lib.gsr_set_prefix_stream(1) == 0
+
+
 def _layout(fn, *args, n=64):
     off = (ctypes.c_size_t * n)()
     k = fn(*args, off, n)
