@@ -68,7 +68,8 @@ def parse(argv=None):
     ap.add_argument("--antialiasing", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
-    ap.add_argument("--cpu-reps", type=int, default=3, help="CPU baseline runs (median reported)")
+    ap.add_argument("--cpu-reps", type=int, default=10,
+                    help="CPU baseline runs (median reported; ~1 s each at the default workload)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-aux", action="store_true", help="skip the §8f side measurements (distCUDA2)")
     ap.add_argument("--no-pmc", action="store_true",
