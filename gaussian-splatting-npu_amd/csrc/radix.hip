@@ -1327,6 +1327,10 @@ hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s
     }
 }
 
+#ifndef GSR_TILE_W1_DELTA
+#define GSR_TILE_W1_DELTA -1
+#endif
+
 size_t fused_pass1_scratch_bytes(int P)
 {
     const size_t chunks = ((size_t)(P > 0 ? P : 0) + FE_RANKS - 1) / FE_RANKS;
@@ -1337,7 +1341,11 @@ hipError_t tile_sort_fused_batch(const TileSortJob* jobs, int V, uint32_t gx, in
 {
     const int nbits = max((int)higher_msb((uint32_t)T), 1);
     const int npass = (nbits + 7) / 8;
-    const int w1 = nbits / npass + (nbits % npass ? 1 : 0);  // radix_sort_batch's balanced first width
+    // the first (fused) pass's digit width: one bit narrower than balanced when there are two passes
+    // (the fused pass costs more per digit bit than the plain second one: 6 + 7 bits at 1080p measured
+    // 480-487 us per 8-view tile sort against 490-493 for 7 + 6, and 8 + 5 567-579)
+    int w1 = nbits / npass + (nbits % npass ? 1 : 0);
+    if (npass == 2) w1 = min(max(w1 + GSR_TILE_W1_DELTA, nbits - 8), 8);
     return for_groups(V, [&](int v0, int nv) -> hipError_t {
         ViewBatch<FusedPassArgs> fb;
         ViewBatch<RowJob> rb;
