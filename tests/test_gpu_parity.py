@@ -259,8 +259,10 @@ def test_packed_rect_boundary_keys_bit_exact(H, W, P):
     (tile_hist + the tile-order prefix sums; the tile sort writes no tile ids); above it the depth
     sort gathers the u16x4 rect by id and the ranges come from tile_ranges over the sorted tile ids.
     255 and 256 tiles along either axis give keys, ids and ranges bit-identical to the oracle, and
-    every gradient matches it on both sides (render_bwd finds a record's mask bit from the
-    Gaussian's first record slot, emit_start, on both).  P not a multiple of 4 (3001, 3003, 1001,
+    every gradient matches it on both sides.  The record slots switch there too: up to 255 tiles the
+    tile sort carries no slot and render_bwd derives each instance's slot from the packed rect in the
+    render record (emit_start + its index in the rect); above, the tile sort writes the index in the
+    rect per instance (BIN_SLOT) and render_bwd reads it.  P not a multiple of 4 (3001, 3003, 1001,
     3) covers tile_hist's tail, the last P mod 4 rects it adds outside its 16-B loads."""
     dgr = _dgr()
     case = common.make_case(P=P, H=H, W=W)
