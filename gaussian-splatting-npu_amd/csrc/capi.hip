@@ -838,11 +838,12 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
                                              tan_fovy[v], prefiltered, antialiasing, radii ? radii[v] : nullptr, v,
                                              &pa[v], &h[v], &hdev[v]);
         if (rc) return rc;
-        // GeometryState's means2D, depths and rgb are read by nothing after the forward: the
-        // batched forward does not write them (24 B per visible Gaussian and view)
+        // GeometryState's means2D, depths, rgb and conic_opacity are read by nothing after the forward: the
+        // batched forward does not write them (40 B per visible Gaussian and view)
         pa[v].means2D = nullptr;
         pa[v].depths = nullptr;
         pa[v].rgb = nullptr;
+        pa[v].conic_opacity = nullptr;  // (preprocess_bwd recomputes it: 16 B per visible Gaussian and view)
     }
     // The binning prefix of all V views, batched: every stage is one launch over all views
     // (grid.y = view), on the caller's stream like the renders that follow (a separate prefix

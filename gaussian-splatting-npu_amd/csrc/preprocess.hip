@@ -196,7 +196,8 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     a.radii[idx] = (int)my_radius;
     if (a.means2D) reinterpret_cast<float2*>(a.means2D)[idx] = make_float2(pix_x, pix_y);
     const float opacity = opacity_in * h_convolution_scaling;
-    reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
+    if (a.conic_opacity)  // (the batched forward stores none: preprocess_bwd recomputes it)
+        reinterpret_cast<float4*>(a.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     a.tiles_touched[idx] = (rmaxy - rminy) * (rmaxx - rminx);
     if (a.rect4) a.rect4[idx] = rect_pack(rminx, rminy, rmaxx, rmaxy);
     else a.rect[idx] = make_uint2(rminx | (rminy << 16), rmaxx | (rmaxy << 16));

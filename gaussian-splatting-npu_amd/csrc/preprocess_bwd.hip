@@ -247,26 +247,19 @@ __device__ __forceinline__ void cov3d_of(const PreprocessBwdArgs& a, const BwdIn
 // computeCov2DCUDA (backward.cu:147-326), the projection part of preprocessCUDA
 // (backward.cu:423-440) and the set-up of computeColorFromSH's backward (backward.cu:28-49) for
 // one view: `gin` are the view's record sums, `co` its conic + rendered opacity.
+// The view's conic and (AA-scaled) opacity -- GeometryState's conic_opacity, which the batched
+// forward does not store -- are recomputed here from the 2D covariance this function recomputes
+// anyway, with the forward's own operations (preprocess.hip preprocess_one, -ffp-contract=off):
+// bit-identical to the stored values.
 __device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const ViewCam& vc, const float (&gin)[GF_NUM],
-                                          const float4 co, uint8_t clamped, const f3 mean, float opacity,
-                                          const float (&cov3D)[6], ViewGrad& o)
+                                          uint8_t clamped, const f3 mean, float opacity, const float (&cov3D)[6],
+                                          ViewGrad& o)
 {
     float* g = o.g;
 #pragma unroll
     for (int q = 0; q < GF_NUM; q++) g[q] = gin[q];
-    {
-        // per-Gaussian factors of the record sums (see GradField; backward.cu:619-636)
-        const float op = co.w;
-        const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
-        g[GF_MEAN2D_X] = (co.x * sx + co.y * sy) * (-op * (0.5f * a.W));
-        g[GF_MEAN2D_Y] = (co.y * sx + co.z * sy) * (-op * (0.5f * a.H));
-        g[GF_CONIC_A] *= -0.5f * op;
-        g[GF_CONIC_B] *= -0.5f * op;
-        g[GF_CONIC_C] *= -0.5f * op;
-    }
 
     // ---------------- computeCov2DCUDA (backward.cu:147-326) ----------------
-    const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
     const float* view = vc.view;
     f3 t = transformPoint4x3(mean, view);
     const float limx = 1.3f * vc.tan_fovx;
@@ -290,12 +283,14 @@ __device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const View
     float c_yy = cov2D.m[1][1];
     const float h_var = 0.3f;
     float d_inside_root = 0.f;
+    float op = opacity;  // the opacity the render blended (forward.cu:262-266)
     if (a.antialiasing) {
         const float det_cov = c_xx * c_yy - c_xy * c_xy;
         c_xx += h_var;
         c_yy += h_var;
         const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
         const float h_convolution_scaling = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
+        op = opacity * h_convolution_scaling;
         const float dL_dopacity_v = g[GF_OPACITY];
         const float d_h_convolution_scaling = dL_dopacity_v * opacity;
         o.dopacity = dL_dopacity_v * h_convolution_scaling;
@@ -306,6 +301,20 @@ __device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const View
         c_yy += h_var;
         o.dopacity = g[GF_OPACITY];
     }
+    const float denom = c_xx * c_yy - c_xy * c_xy;
+    {
+        // the conic (forward.cu:218-222 as preprocess_one computes it), then the per-Gaussian
+        // factors of the record sums (see GradField; backward.cu:619-636)
+        const float det_inv = 1.f / denom;
+        const float cx = c_yy * det_inv, cy = -c_xy * det_inv, cz = c_xx * det_inv;
+        const float sx = g[GF_MEAN2D_X], sy = g[GF_MEAN2D_Y];
+        g[GF_MEAN2D_X] = (cx * sx + cy * sy) * (-op * (0.5f * a.W));
+        g[GF_MEAN2D_Y] = (cy * sx + cz * sy) * (-op * (0.5f * a.H));
+        g[GF_CONIC_A] *= -0.5f * op;
+        g[GF_CONIC_B] *= -0.5f * op;
+        g[GF_CONIC_C] *= -0.5f * op;
+    }
+    const f3 dL_dconic = {g[GF_CONIC_A], g[GF_CONIC_B], g[GF_CONIC_C]};
     float dL_dc_xx = 0, dL_dc_xy = 0, dL_dc_yy = 0;
     if (a.antialiasing) {
         const float x = c_xx, y = c_yy, z = c_xy, w = h_var;
@@ -314,7 +323,6 @@ __device__ __forceinline__ void view_grad(const PreprocessBwdArgs& a, const View
         dL_dc_yy = w * (w * x + x * x + z * z) * denom_f;
         dL_dc_xy = -2.f * w * z * (w + x + y) * denom_f;
     }
-    const float denom = c_xx * c_yy - c_xy * c_xy;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     const float(*Tm)[3] = T.m;
     float* dcov = o.dcov;
@@ -515,7 +523,6 @@ __device__ __forceinline__ float group_sum(float x)
 // A lane's view inputs, loaded in the kernel's prologue (unconditionally, clamped), so that their
 // round trip overlaps the SH staging and the record gather is the only dependent one after it.
 struct ViewIn {
-    float4 co;
     uint8_t cl;
     uint32_t e0, n;  // record slots [e0, e0 + n)
     uint32_t mask;   // which of the first 32 hold a record
@@ -525,7 +532,6 @@ struct ViewIn {
 __device__ __forceinline__ void view_load(const PreprocessBwdViewsArgs& A, int idx, int v, ViewIn& vi)
 {
     const BwdView& bv = A.v[v < A.V ? v : 0];
-    vi.co = bv.conic_opacity[idx];
     vi.cl = bv.clamped[idx];
     vi.e0 = bv.emit_start[idx];
     vi.n = bv.tiles_touched[idx];
@@ -596,7 +602,7 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
     cov3d_of(a, in, cov3D);
     ViewGrad o;
     if (vis) {
-        view_grad(a, cam_of_lds(cam), gs, vi.co, vi.cl, in.mean, in.opacity, cov3D, o);
+        view_grad(a, cam_of_lds(cam), gs, vi.cl, in.mean, in.opacity, cov3D, o);
     } else {
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) o.g[q] = 0.f;
