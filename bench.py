@@ -576,8 +576,9 @@ def main(argv=None):
                 ab[k] *= vb
             # the batched preprocess reads the parameters once for its views
             params_b = P * 4 * (11 + 3 * M)
-            # (and writes no means2D / depth / rgb: 24 B per visible Gaussian and view, read by nothing)
-            ab["preprocess_fwd"] = params_b + vb * (ab["preprocess_fwd"] - params_b - P_vis * 24)
+            # (and writes no means2D / depth / rgb / conic_opacity: 40 B per visible Gaussian and view,
+            # read by nothing -- preprocess_bwd recomputes the conic)
+            ab["preprocess_fwd"] = params_b + vb * (ab["preprocess_fwd"] - params_b - P_vis * 40)
         # the dominant kernel: the largest share of the step (mean launch time x launches per step)
         dom = max(kern, key=lambda k: kern[k]["avg_ms"] * kern[k]["launches"])
         achieved = ab[dom] / (kern[dom]["avg_ms"] * 1e-3) / 1e9
