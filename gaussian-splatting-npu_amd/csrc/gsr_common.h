@@ -248,6 +248,12 @@ constexpr int TILE_DIFF_MAX_CELLS = 8704;
 #endif
 // BIN_SLOT holds each instance's index inside its Gaussian's tile rect (its record slot minus the
 // Gaussian's emit_start) instead of the absolute record slot
+// floats per per-instance gradient record (GRAD_INST): 10 used; 10 = 40 B packed (8-B accesses), 12 =
+// 48 B (16-B accesses).  The tile sort's ping-pong buffers (<= 32 B per instance) live in the region.
+#ifndef GSR_GRAD_REC
+#define GSR_GRAD_REC 10
+#endif
+static_assert(GSR_GRAD_REC == 10 || GSR_GRAD_REC == 12, "gradient record: 10 or 12 floats");
 #ifndef GSR_SLOT_LOCAL
 #define GSR_SLOT_LOCAL 1
 #endif
@@ -312,7 +318,8 @@ inline ImageLayout image_layout(int W, int H)
 inline BinLayout bin_layout(int L)
 {
     size_t n = (size_t)(L > 0 ? L : 0);
-    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 48 * n + 4096, radix_status_bytes(L, 4), 4 * ((n + 31) / 32), n};
+    size_t sizes[BIN_COUNT] = {4 * n, 4 * n, 4 * n, 4 * (size_t)GSR_GRAD_REC * n + 4096, radix_status_bytes(L, 4),
+                               4 * ((n + 31) / 32), n};
     BinLayout l;
     size_t o = 0;
     for (int i = 0; i < BIN_COUNT; i++) { l.off[i] = o; o = align_up(o + sizes[i], 256); }

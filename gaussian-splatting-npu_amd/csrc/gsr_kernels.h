@@ -80,7 +80,7 @@ struct RenderBwdArgs {
     uint32_t* rec_mask;         // GEOM_REC_MASK: bit (slot - emit_start[id]) set for records at local index < 32
 };
 
-// Layout of one per-instance gradient record (GRAD_REC floats, 48 B).  With u = G dL/dalpha
+// Layout of one per-instance gradient record (GRAD_REC floats: 40 B, or 48 B padded).  With u = G dL/dalpha
 // per pixel, the mean2D fields hold Sx = sum u dx, Sy = sum u dy and the conic fields
 // sum u dx^2, u dx dy, u dy^2 -- WITHOUT the per-Gaussian factors (backward.cu:619-636):
 // preprocess_bwd forms dL/dmean2D = (a Sx + b Sy, b Sx + c Sy) * (-opacity W/2, -opacity H/2)
@@ -89,7 +89,10 @@ enum GradField {
     GF_MEAN2D_X = 0, GF_MEAN2D_Y, GF_CONIC_A, GF_CONIC_B, GF_CONIC_C, GF_OPACITY, GF_COLOR_R, GF_COLOR_G,
     GF_COLOR_B, GF_INVDEPTH, GF_NUM
 };
-constexpr int GRAD_REC = 12;
+#ifndef GSR_GRAD_REC
+#define GSR_GRAD_REC 10  // (the same default as gsr_common.h, which sizes BIN_GRAD_INST with it)
+#endif
+constexpr int GRAD_REC = GSR_GRAD_REC;
 
 // In-place gradient accumulation (gsr_backward_dc_acc): bit set = that output array is added to.
 enum AccBits : uint32_t {

@@ -40,6 +40,41 @@ struct BwdIn {
 #endif
 constexpr int REC_BATCH = GSR_VIEW_REC_BATCH;
 
+// B records (slots sl[k], v[k]: present) loaded side by side, then added to g in slot order.
+template <int B>
+__device__ __forceinline__ void rec_batch(const bool (&v)[B], const uint32_t (&sl)[B], const float* grad_inst,
+                                          float (&g)[GF_NUM])
+{
+    float r[B][GF_NUM];
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+        if (v[k]) {
+            if constexpr (GRAD_REC % 4 == 0) {  // 16-B aligned records
+                const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
+                const float4 a0 = rec[0], a1 = rec[1], a2 = rec[2];
+                r[k][0] = a0.x; r[k][1] = a0.y; r[k][2] = a0.z; r[k][3] = a0.w;
+                r[k][4] = a1.x; r[k][5] = a1.y; r[k][6] = a1.z; r[k][7] = a1.w;
+                r[k][8] = a2.x; r[k][9] = a2.y;
+            } else {  // packed 40-B records
+                const float2* rec = reinterpret_cast<const float2*>(grad_inst + (size_t)sl[k] * GRAD_REC);
+#pragma unroll
+                for (int h = 0; h < GF_NUM / 2; h++) {
+                    const float2 x = rec[h];
+                    r[k][2 * h] = x.x;
+                    r[k][2 * h + 1] = x.y;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < B; k++) {
+        if (v[k]) {
+#pragma unroll
+            for (int q = 0; q < GF_NUM; q++) g[q] += r[k][q];
+        }
+    }
+}
+
 // Sum of one Gaussian's per-tile gradient records of one view.  Its records are contiguous
 // (slots [emit_start, + tiles_touched)); entries that contributed to no pixel were never written (their bit in the valid
 // mask is 0) and are not read (most slots: records are sparse).  The mask has one bit per slot
@@ -66,24 +101,7 @@ __device__ __forceinline__ void gather_range(uint32_t e0, uint32_t e1, const uin
                 sl[k] = w0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
                 bits &= bits - 1u;
             }
-            float4 r[B][3];
-#pragma unroll
-            for (int k = 0; k < B; k++) {
-                if (v[k]) {
-                    const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
-                    r[k][0] = rec[0];
-                    r[k][1] = rec[1];
-                    r[k][2] = rec[2];
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < B; k++) {
-                if (v[k]) {
-                    g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
-                    g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
-                    g[8] += r[k][2].x; g[9] += r[k][2].y;
-                }
-            }
+            rec_batch<B>(v, sl, grad_inst, g);
         }
     }
 }
@@ -105,24 +123,7 @@ __device__ __forceinline__ void gather_mask(uint32_t e0, uint32_t bits, const fl
             sl[k] = e0 + (v[k] ? (uint32_t)__builtin_ctz(bits) : 0u);
             bits &= bits - 1u;
         }
-        float4 r[B][3];
-#pragma unroll
-        for (int k = 0; k < B; k++) {
-            if (v[k]) {
-                const float4* rec = reinterpret_cast<const float4*>(grad_inst + (size_t)sl[k] * GRAD_REC);
-                r[k][0] = rec[0];
-                r[k][1] = rec[1];
-                r[k][2] = rec[2];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < B; k++) {
-            if (v[k]) {
-                g[0] += r[k][0].x; g[1] += r[k][0].y; g[2] += r[k][0].z; g[3] += r[k][0].w;
-                g[4] += r[k][1].x; g[5] += r[k][1].y; g[6] += r[k][1].z; g[7] += r[k][1].w;
-                g[8] += r[k][2].x; g[9] += r[k][2].y;
-            }
-        }
+        rec_batch<B>(v, sl, grad_inst, g);
     }
 }
 

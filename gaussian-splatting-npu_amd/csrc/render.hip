@@ -852,7 +852,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // one 48-B record per contributing entry, stored by its own lane: its quadrant partials
+            // one gradient record per contributing entry, stored by its own lane: its quadrant partials
             // summed as (q0 + q2) + (q1 + q3), a fixed order (bitwise reproducible)
             if (mm != 0) {
                 float t0[GF_NUM], t1[GF_NUM];
@@ -883,9 +883,14 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                 float t[GF_NUM];
 #pragma unroll
                 for (int f = 0; f < GF_NUM; f++) t[f] = t0[f] + t1[f];
-                reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
-                reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
-                reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
+                if constexpr (GRAD_REC % 4 == 0) {  // 16-B aligned records
+                    reinterpret_cast<float4*>(rec)[0] = make_float4(t[0], t[1], t[2], t[3]);
+                    reinterpret_cast<float4*>(rec)[1] = make_float4(t[4], t[5], t[6], t[7]);
+                    reinterpret_cast<float2*>(rec)[4] = make_float2(t[8], t[9]);
+                } else {  // packed 40-B records: 8-B aligned
+#pragma unroll
+                    for (int h = 0; h < GF_NUM / 2; h++) reinterpret_cast<float2*>(rec)[h] = make_float2(t[2 * h], t[2 * h + 1]);
+                }
                 // flagged in the Gaussian's own mask when it is one of its first 32 slots (preprocess_bwd
                 // then finds the records without a dependent load of the valid words), else in the valid
                 // words: one atomic per record either way
