@@ -639,13 +639,16 @@ __device__ __forceinline__ void bwd_lane_terms(const BwdAcc& o, float dy, float*
 // reduction: 0.79 bank-conflict cycles per LDS instruction at random entries; -1 %.)  Against one
 // 64-lane pass per entry over the half-tiles it reaches, this skips the pixel pairs of quadrants
 // an entry does not reach (25 % of them) and reduces over 16 lanes: render_bwd -11 %.
-// Tiles (independent waves) per workgroup.  A retiring 4-wave workgroup frees one wave slot on
-// each SIMD of its CU -- the footprint of a 256-thread binning-prefix workgroup of the next view
-// (depth sort, scans, tile sort), which then runs beside this launch instead of
-// waiting for its last wave; single-wave workgroups left no such hole (a freed slot was refilled
-// by the next tile first).  Same-box A/B, 8-view step: 1 -> 2 -> 4 -> 8 tiles: 2,258 / 2,285 /
-// 2,340 / 2,323 Mpix/s (render_bwd alone 374 / 375 / 377 / 420 us).
-constexpr int BWD_TPW = 4;
+// Tiles (independent waves) per workgroup.  Round 2 chose 4: a retiring 4-wave workgroup frees one
+// wave slot on each SIMD of its CU -- the footprint of a 256-thread binning-prefix workgroup of the
+// next view, which then ran beside this launch when views alternated over two streams (1 -> 2 -> 4
+// -> 8 tiles: 2,258 / 2,285 / 2,340 / 2,323 Mpix/s then).  Since the views are batched, the prefix
+// runs before the renders and nothing needs that hole: one tile per workgroup (the finest dispatch
+// granularity) measured render_bwd 1,910-1,915 -> 1,873-1,883 us per 8 views (round 5, 3 rounds).
+#ifndef GSR_BWD_TPW
+#define GSR_BWD_TPW 1
+#endif
+constexpr int BWD_TPW = GSR_BWD_TPW;
 // reduction blocks of partial rows per wave: 11 blocks = 33 iterations per pass (5.5 KB per wave)
 #ifndef GSR_BWD_PART_BLOCKS
 #define GSR_BWD_PART_BLOCKS 11
