@@ -257,7 +257,7 @@ extern "C" {
 
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
-const char* gsr_version(void) { return "gsr-hip 0.1 gfx950"; }
+const char* gsr_version(void) { return GSR_REF_ALPHA ? "gsr-hip 0.1 gfx950 ref-alpha (TEST BUILD)" : "gsr-hip 0.1 gfx950"; }
 
 int gsr_set_prefix_stream(int on)
 {

@@ -257,6 +257,14 @@ static_assert(GSR_GRAD_REC == 10 || GSR_GRAD_REC == 12, "gradient record: 10 or 
 #ifndef GSR_SLOT_LOCAL
 #define GSR_SLOT_LOCAL 1
 #endif
+// TEST-ONLY build (make refalpha -> refalpha/libgsr_hip_refalpha.so, never loaded by the package):
+// the render record carries the plain conic and the render kernels compute power and alpha in the
+// reference's operation order with the shared exp of gsr_ref_exp.h (forward.cu:353-363,
+// backward.cu:556-571), so that tests/test_ref_alpha_exact.py can hold the blend bit-exact against
+// the oracle.  The production build (0) evaluates exp2 of the log2(e)-prescaled falloff instead.
+#ifndef GSR_REF_ALPHA
+#define GSR_REF_ALPHA 0
+#endif
 // on grids of packed rects (rect_packable): no record slots at all -- render_bwd derives an instance's
 // index in its Gaussian's rect from the packed rect preprocess stores in the render record's free word
 // (SPLAT word 3) and the tile, and the tile sort moves 4 B per instance instead of 8

@@ -214,12 +214,18 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, int idx,
     // The record carries the conic pre-scaled into the log2-domain falloff the render kernels
     // evaluate (render.hip Falloff: p2 = ka dx^2 + kb dx dy + kc dy^2 = log2(e) * power), and
     // cullK in the same scale (q' = -(ka dx^2 + kb dx dy + kc dy^2) <= log2(e)/2 * K).
-    constexpr float LOG2E = 1.4426950408889634f;
+    [[maybe_unused]] constexpr float LOG2E = 1.4426950408889634f;
+#if !GSR_REF_ALPHA
     if (cullK >= 0.f && cullK < 1.0e37f) cullK = cullK * (0.5f * LOG2E);
+#endif
     float4* sp = a.splat + 3 * (size_t)idx;
     // (word 3: the packed tile rect, from which render_bwd derives an instance's record slot)
     sp[0] = make_float4(pix_x, pix_y, cullK, a.rect4 ? __uint_as_float(rect_pack(rminx, rminy, rmaxx, rmaxy)) : 0.0f);
+#if GSR_REF_ALPHA  // (test build: the plain conic, cullK in units of d^T conic d)
+    sp[1] = make_float4(conic_x, conic_y, conic_z, opacity);
+#else
     sp[1] = make_float4((-0.5f * LOG2E) * conic_x, (-LOG2E) * conic_y, (-0.5f * LOG2E) * conic_z, opacity);
+#endif
     sp[2] = make_float4(rgb.x, rgb.y, rgb.z, 1.0f / p_view.z);
 }
 

@@ -30,6 +30,10 @@
 // backward.cu:593-635).
 #include "gsr_common.h"
 #include "gsr_kernels.h"
+#if GSR_REF_ALPHA
+#define GSR_REF_EXP_QUAL static __device__ __forceinline__
+#include "gsr_ref_exp.h"
+#endif
 
 namespace gsr {
 
@@ -78,7 +82,11 @@ __device__ __forceinline__ uint32_t quad_mask(const float4 r0, const float4 k, u
     if (K > 1.0e37f) return 0xFu;  // degenerate conic: never cull
     if (K < 0.f) return 0u;
     const float dx0 = (float)(tx * GSR_BLOCK_X) - r0.x, dy0 = (float)(ty * GSR_BLOCK_Y) - r0.y;
+#if GSR_REF_ALPHA  // (test build: the record holds the plain conic and K)
+    const float qa = k.x, qb = k.y, qc = k.z;
+#else
     const float qa = -k.x, qb = -0.5f * k.y, qc = -k.z;
+#endif
     uint32_t m = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -116,6 +124,17 @@ __device__ __forceinline__ v2f falloff_p2(const Falloff f, v2f dx, float dy)
     const float cq = (f.kc * dy) * dy;
     return fma2(fma2((v2f)(f.ka), dx, (v2f)(bq)), dx, (v2f)(cq));
 }
+
+#if GSR_REF_ALPHA
+// TEST BUILD ONLY (GSR_REF_ALPHA): the reference's falloff, forward.cu:353-354 / backward.cu:556-557,
+// in its operation order without contraction, on the record's plain conic (co.xyz), and its alpha
+// with the shared exp (gsr_ref_exp.h) -- what oracle/gsr_oracle.c computes with shared_exp set.
+__device__ __forceinline__ float ref_power(const float4 co, float dx, float dy)
+{
+#pragma clang fp contract(off)
+    return -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+}
+#endif
 
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 {
@@ -309,7 +328,11 @@ __device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
 {
+#if GSR_REF_ALPHA  // (test build: every blend operation in the reference's order, forward.cu:353-380)
+#pragma clang fp contract(off)
+#else
 #pragma clang fp contract(fast)
+#endif
     const RenderFwdArgs& a = B.v[blockIdx.y];
     const uint32_t tile = a.tile_order[blockIdx.x];
     const uint32_t tx = tile % a.grid_x, ty = tile / a.grid_x;
@@ -384,8 +407,13 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             // entry that would take T below 1e-4 finishes the pixel without blending
             // (forward.cu:356-376); ae = the alpha actually blended (0 or a).
             auto blend = [&](int j, const float4 xy, const float4 co, const float4 col) {
+#if GSR_REF_ALPHA
+                const float p2 = ref_power(co, xy.x - pfx, xy.y - pfy);  // power (test build)
+                const float alpha = fminf(0.99f, co.w * gsr_ref_expf(p2));
+#else
                 const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
                 const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
+#endif
                 const float a = (p2 > 0.0f ? 0.0f : alpha) * live;
                 const bool contrib = a >= 1.0f / 255.0f;
                 const float test_T = T * (1 - a);
@@ -402,11 +430,18 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                         : "scc");
                     hitbits |= t;
                 }
+#if GSR_REF_ALPHA  // features * alpha * T, left to right (forward.cu:373-375)
+                C0 += col.x * ae * T;
+                C1 += col.y * ae * T;
+                C2 += col.z * ae * T;
+                ID += col.w * ae * T;
+#else
                 const float aT = ae * T;  // 0 leaves the sums unchanged
                 C0 += col.x * aT;
                 C1 += col.y * aT;
                 C2 += col.z * aT;
                 ID += col.w * aT;
+#endif
                 T = blended ? test_T : T;
                 last_contributor = blended ? (uint32_t)(base + j + 1) : last_contributor;
             };
@@ -554,12 +589,20 @@ struct BwdAcc {
 // b Sx + c Sy) times -opacity * W/2 resp. H/2) and sum u*dx*dx, u*dx*dy, u*dy*dy (conic, times
 // -opacity/2).  FIRST: the sums are assigned, not accumulated (no zero-initialisation).
 template <bool HAS_INV, bool FIRST>
-__device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, const float4 xy, float bq, float cq,
+__device__ __forceinline__ void bwd_pair(BwdPair& s, v2f pfx, uint32_t pos, const float4 xy, float dy, float bq, float cq,
                                          const Falloff f, const float4 co, const float4 col, BwdAcc& o)
 {
     const v2f dx = (v2f)(xy.x) - pfx;
+#if GSR_REF_ALPHA  // (test build: power and G = exp(power) as backward.cu:556-568; bq, cq unused)
+    (void)bq;
+    (void)cq;
+    const v2f p2 = {ref_power(co, dx.x, dy), ref_power(co, dx.y, dy)};
+    const v2f G = {gsr_ref_expf(p2.x), gsr_ref_expf(p2.y)};
+#else
+    (void)dy;
     const v2f p2 = fma2(fma2((v2f)(f.ka), dx, (v2f)(bq)), dx, (v2f)(cq));
     const v2f G = {__builtin_amdgcn_exp2f(p2.x), __builtin_amdgcn_exp2f(p2.y)};
+#endif
     const v2f al = G * co.w;
     const bool c0 = pos < s.lc0 && !(p2.x > 0.0f) && !(al.x < 1.0f / 255.0f);
     const bool c1 = pos < s.lc1 && !(p2.y > 0.0f) && !(al.y < 1.0f / 255.0f);
@@ -837,8 +880,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
                         const float dy = xy.y - pfy;
                         const float bq = f.kb * dy, cq = (f.kc * dy) * dy;
                         BwdAcc o;
-                        bwd_pair<HAS_INV, true>(st[0], pfx0, pos, xy, bq, cq, f, co, col, o);
-                        bwd_pair<HAS_INV, false>(st[1], pfx1, pos, xy, bq, cq, f, co, col, o);
+                        bwd_pair<HAS_INV, true>(st[0], pfx0, pos, xy, dy, bq, cq, f, co, col, o);
+                        bwd_pair<HAS_INV, false>(st[1], pfx1, pos, xy, dy, bq, cq, f, co, col, o);
                         bwd_lane_terms(o, dy, &v[jj * GF_NUM]);
                     } else {
 #pragma unroll

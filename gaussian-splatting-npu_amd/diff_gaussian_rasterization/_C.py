@@ -18,12 +18,14 @@ LIB_PATH = os.path.join(_HERE, "libgsr_hip.so")
 _vp, _i, _f, _b, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_bool, ctypes.c_size_t
 
 
-def _load():
-    if not os.path.exists(LIB_PATH):
+def _load(path=LIB_PATH):
+    """The C ABI of the HIP library at `path` with its ctypes signatures.  The package loads only
+    LIB_PATH; tests/test_ref_alpha_exact.py passes its test-only GSR_REF_ALPHA build here."""
+    if not os.path.exists(path):
         raise ImportError(
-            f"diff_gaussian_rasterization: native library {LIB_PATH} is missing; build it with "
+            f"diff_gaussian_rasterization: native library {path} is missing; build it with "
             "`make -C gaussian-splatting-npu_amd` (or __graft_entry__.build()). There is no CPU fallback.")
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     lib.gsr_last_error.restype = ctypes.c_char_p
     lib.gsr_version.restype = ctypes.c_char_p
     for n in ("gsr_geometry_buffer_size", "gsr_binning_buffer_size"):

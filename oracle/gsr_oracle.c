@@ -54,6 +54,15 @@ typedef struct { float x, y, z, w; } f4;
 typedef struct { float m[3][3]; } mat3;
 
 static inline float fminf_(float a, float b) { return fminf(a, b); }
+
+/* exp() of the blend (forward.cu:363, backward.cu:568): the host libm's expf by default; with
+ * gsr_oracle_set_shared_exp(1) the test-only gsr_ref_expf that the GSR_REF_ALPHA build of the HIP
+ * render kernels evaluates too (gsr_ref_exp.h), so that the two compare bit for bit. */
+#include "../gaussian-splatting-npu_amd/csrc/gsr_ref_exp.h"
+static int g_shared_exp = 0;
+void gsr_oracle_set_shared_exp(int on) { g_shared_exp = on; }
+float gsr_oracle_ref_expf(float x) { return gsr_ref_expf(x); } /* (for tests/test_oracle.py) */
+static inline float blend_expf(float x) { return g_shared_exp ? gsr_ref_expf(x) : expf(x); }
 static inline float fmaxf_(float a, float b) { return fmaxf(a, b); }
 
 /* glm type_mat3x3.inl operator*(mat3, mat3) */
@@ -416,7 +425,7 @@ static void render_tile(const oracle_state* st, uint32_t tx, uint32_t ty, const 
                 const float* co = st->conic_opacity + 4 * (size_t)id;
                 float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                 if (power > 0.0f) continue;
-                float alpha = fminf_(0.99f, co[3] * expf(power));
+                float alpha = fminf_(0.99f, co[3] * blend_expf(power));
                 if (alpha < 1.0f / 255.0f) continue;
                 float test_T = T * (1 - alpha);
                 if (test_T < 0.0001f) break; /* done = true */
@@ -469,7 +478,7 @@ int gsr_oracle_near_threshold(void* p, float rel, uint8_t* out, uint8_t* out_gau
                     const float terms = 0.5f * (fabsf(co[0]) * dx * dx + fabsf(co[2]) * dy * dy) + fabsf(co[1] * dx * dy);
                     if (fabsf(power) <= rel * terms) near = 1;
                     if (power <= 0.0f) {
-                        const float alpha = fminf_(0.99f, co[3] * expf(power));
+                        const float alpha = fminf_(0.99f, co[3] * blend_expf(power));
                         if (fabsf(alpha - 1.0f / 255.0f) <= rel * (1.0f / 255.0f)) near = 1;
                         if (alpha >= 1.0f / 255.0f) {
                             const float test_T = Tr * (1 - alpha);
@@ -696,7 +705,7 @@ static void render_bwd_tile(const oracle_state* st, uint32_t tx, uint32_t ty, co
                 const float* co = st->conic_opacity + 4 * (size_t)gid;
                 const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                 if (power > 0.0f) continue;
-                const float G = expf(power);
+                const float G = blend_expf(power);
                 const float alpha = fminf_(0.99f, co[3] * G);
                 if (alpha < 1.0f / 255.0f) continue;
                 T = T / (1.f - alpha);
@@ -789,7 +798,7 @@ static void render_bwd_tile_f64(const oracle_state* st, uint32_t tx, uint32_t ty
                 const float dxf = st->means2D[2 * gid] - pfx, dyf = st->means2D[2 * gid + 1] - pfy;
                 const float power = -0.5f * (co[0] * dxf * dxf + co[2] * dyf * dyf) - co[1] * dxf * dyf;
                 if (power > 0.0f) continue;
-                const float alpha_f = fminf_(0.99f, co[3] * expf(power));
+                const float alpha_f = fminf_(0.99f, co[3] * blend_expf(power));
                 if (alpha_f < 1.0f / 255.0f) continue;
                 const double dx = dxf, dy = dyf;
                 const double pw = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;

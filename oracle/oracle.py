@@ -57,8 +57,13 @@ class OracleRaster:
 
     def __init__(self, means3D, opacities, bg, viewmatrix, projmatrix, campos, tanfovx, tanfovy, H, W,
                  shs=None, sh_degree=0, colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
-                 scale_modifier=1.0, prefiltered=False, antialiasing=False, nthreads=1):
+                 scale_modifier=1.0, prefiltered=False, antialiasing=False, nthreads=1, shared_exp=False):
+        """shared_exp: the blend's exp() is gsr_ref_expf (gsr_ref_exp.h) instead of the host libm's
+        expf, in the forward and in every later backward / near_threshold of this object -- the
+        function the GSR_REF_ALPHA test build of the HIP render kernels evaluates (bit-exact parity
+        of the blend, tests/test_ref_alpha_exact.py)."""
         L = lib()
+        self.shared_exp = bool(shared_exp)
         self.args = dict(means3D=_np(means3D), opacities=_np(opacities), bg=_np(bg), view=_np(viewmatrix),
                          proj=_np(projmatrix), campos=_np(campos), shs=_np(shs), colors=_np(colors_precomp),
                          scales=_np(scales), rots=_np(rotations), cov3D=_np(cov3D_precomp))
@@ -73,6 +78,7 @@ class OracleRaster:
         self.invdepth = np.zeros((1, H, W), np.float32)
         self.radii = np.zeros((P,), np.int32)
         nr = ctypes.c_int(0)
+        L.gsr_oracle_set_shared_exp(ctypes.c_int(int(self.shared_exp)))
         self.h = L.gsr_oracle_forward(
             ctypes.c_int(P), ctypes.c_int(sh_degree), ctypes.c_int(self.M), _p(a["bg"]), ctypes.c_int(W),
             ctypes.c_int(H), _p(a["means3D"]), _p(a["shs"]), _p(a["colors"]), _p(a["opacities"]),
@@ -80,6 +86,7 @@ class OracleRaster:
             _p(a["proj"]), _p(a["campos"]), ctypes.c_float(tanfovx), ctypes.c_float(tanfovy),
             ctypes.c_int(int(prefiltered)), ctypes.c_int(int(antialiasing)), _p(self.color), _p(self.invdepth),
             _p(self.radii), ctypes.c_int(nthreads), ctypes.byref(nr))
+        L.gsr_oracle_set_shared_exp(ctypes.c_int(0))
         if not self.h:
             raise RuntimeError(L.gsr_oracle_last_error().decode())
         self.num_rendered = nr.value
@@ -118,6 +125,7 @@ class OracleRaster:
         di = _np(dL_dinvdepth)
         lib().gsr_oracle_set_bwd_f64(ctypes.c_int(int(bool(f64))))
         lib().gsr_oracle_set_bwd_tile_sums(ctypes.c_int(int(bool(tile_sums))))
+        lib().gsr_oracle_set_shared_exp(ctypes.c_int(int(self.shared_exp)))
         rc = lib().gsr_oracle_backward(
             ctypes.c_void_p(self.h), _p(a["bg"]), _p(a["means3D"]), _p(a["shs"]), _p(a["colors"]),
             _p(a["opacities"]), _p(a["scales"]), ctypes.c_float(self.scale_modifier), _p(a["rots"]),
@@ -128,6 +136,7 @@ class OracleRaster:
             ctypes.c_int(self.nthreads))
         lib().gsr_oracle_set_bwd_f64(ctypes.c_int(0))
         lib().gsr_oracle_set_bwd_tile_sums(ctypes.c_int(0))
+        lib().gsr_oracle_set_shared_exp(ctypes.c_int(0))
         if rc != 0:
             raise RuntimeError("oracle backward failed")
         return g
@@ -140,8 +149,10 @@ class OracleRaster:
         out = np.zeros((self.H, self.W), np.uint8)
         g = np.zeros((max(self.P, 1),), np.uint8)
         if out.size:
+            lib().gsr_oracle_set_shared_exp(ctypes.c_int(int(self.shared_exp)))
             lib().gsr_oracle_near_threshold(ctypes.c_void_p(self.h), ctypes.c_float(rel),
                                             out.ctypes.data_as(ctypes.c_void_p), g.ctypes.data_as(ctypes.c_void_p))
+            lib().gsr_oracle_set_shared_exp(ctypes.c_int(0))
         return (out.astype(bool), g[:self.P].astype(bool)) if gaussians else out.astype(bool)
 
     def __del__(self):

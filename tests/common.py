@@ -124,7 +124,9 @@ REL_FLOOR = 1e-3
 REL_P999 = 1e-3
 REL_OUT = 1e-2
 REL_OUT_FRAC = 1e-4
-REL_LEFT_OUT_FRAC = 0.2  # check_rel: at most this share of the rows may be left out as decision suspects
+# check_rel: at most this share of the rows may be left out as decision suspects (0.1; round 5 raised the
+# global cap to 0.2 for one case -- chair case 4 -- which now passes its own cap, test_chair_gpu.py)
+REL_LEFT_OUT_FRAC = 0.1
 
 
 def rel_stats(hip, ref, floor=REL_FLOOR):
@@ -141,7 +143,7 @@ def rel_stats(hip, ref, floor=REL_FLOOR):
             "max": float(r.max()), "n_over_1e-3": int((r > 1e-3).sum()), "n_over_REL_OUT": int((r > REL_OUT).sum())}
 
 
-def check_rel(name, hip, ref, affected=None, truth_stats=None):
+def check_rel(name, hip, ref, affected=None, truth_stats=None, max_left_out_frac=REL_LEFT_OUT_FRAC):
     """Asserts the per-element relative-error bounds above over the rows (Gaussians) outside
     `affected` (the walks of decision-suspect pixels: their rows are bounded by
     check_grad_attributed); returns (and logs) the statistics.  truth_stats: the oracle's own
@@ -159,8 +161,8 @@ def check_rel(name, hip, ref, affected=None, truth_stats=None):
     PARITY_LOG.append({"name": name + " rel", "rows_left_out": left_out, "p999_bound": bound, **st})
     # the rows left out (decision suspects' walks) stay a small share of the Gaussians (measured: at most
     # 11.4 % on the chair fixture's perturbed case 4, whose 100k Gaussians are densely packed behind
-    # few pixels -- 15 suspect pixels; 0.05 % at config 3's scale)
-    assert left_out <= REL_LEFT_OUT_FRAC * max(len(keep) if affected is not None else 0, 1), \
+    # few pixels -- 15 suspect pixels -- which passes its own cap; 0.05 % at config 3's scale)
+    assert left_out <= max_left_out_frac * max(len(keep) if affected is not None else 0, 1), \
         f"{name}: {left_out} rows left out of the per-element check"
     assert st["p999"] <= bound, f"{name}: 99.9th percentile relative error {st['p999']:.3e} > {bound:.3e} ({st})"
     assert st["n_over_REL_OUT"] <= max(2, REL_OUT_FRAC * st["considered"]), f"{name}: {st}"
@@ -211,10 +213,14 @@ def allclose_rel(a, b, rtol=GRAD_RTOL, atol=GRAD_ATOL):
 # of a flipped pixel's tile are the only ones whose gradients a flip can move.  Every gradient
 # element beyond GRAD_RTOL of max|ref| (or beyond REL_OUT relative to itself) must belong to such
 # a Gaussian; outside that set the plain tolerance holds, inside it GRAD_RTOL_ATTRIBUTED.
-# (2e-3 through round 4; raised in round 5 after a 2.005e-3 attributed row in a 3,001-Gaussian,
-# 4080 x 256 case of test_packed_rect_boundary_keys_bit_exact: where a Gaussian covers few pixels,
-# one flipped pixel's term is a larger share of its gradient.  The count of such rows is capped below.)
-GRAD_RTOL_ATTRIBUTED = 5e-3
+# (Round 5 raised it to 5e-3 after a 2.005e-3 attributed row in a 3,001-Gaussian, 4080 x 256 case of
+# test_packed_rect_boundary_keys_bit_exact: where a Gaussian covers few pixels, one flipped pixel's term
+# is a larger share of its gradient.  Round 6 restored 2e-3 here; that test passes its own
+# GRAD_RTOL_ATTRIBUTED_SMALL_FOOTPRINT.  The count of such rows is capped below.  That the flips are
+# the only source is shown by tests/test_ref_alpha_exact.py: with the blend in the reference's
+# operation order there are no flipped pixels and no row beyond GRAD_RTOL.)
+GRAD_RTOL_ATTRIBUTED = 2e-3
+GRAD_RTOL_ATTRIBUTED_SMALL_FOOTPRINT = 5e-3
 # and only a few of the attributed Gaussians may actually be off beyond GRAD_RTOL: at most
 # max(ATTR_ROWS_MIN, ATTR_ROWS_FRAC x the walks' Gaussians) rows (measured through round 4: at most
 # 16 rows of 17,250 for the 8-view sum, a ratio of at most 0.0018 per view), so a real regression

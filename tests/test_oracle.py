@@ -302,3 +302,44 @@ def test_cpu_abi_matches_oracle():
     for k in ("dL_dmean2D", "dL_dopacity", "dL_dcolors", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
               "dL_drotations"):
         np.testing.assert_array_equal(g[k], og[k].reshape(g[k].shape), err_msg=k)
+
+
+def test_shared_exp_accuracy():
+    """gsr_ref_expf (gaussian-splatting-npu_amd/csrc/gsr_ref_exp.h, the exp() the GSR_REF_ALPHA test
+    build of the render kernels and the oracle's shared_exp mode both evaluate) is within 1.5 ulp of
+    exp over the range the blend uses, 0 below it."""
+    import ctypes
+    lib = oracle.lib()
+    f = lib.gsr_oracle_ref_expf
+    f.restype, f.argtypes = ctypes.c_float, [ctypes.c_float]
+    xs = np.concatenate([np.linspace(-103, 88, 20001, dtype=np.float32),
+                         -np.logspace(-8, 2, 2000).astype(np.float32), np.float32([0.0, -0.0])])
+    ys = np.array([f(float(x)) for x in xs], np.float32)
+    t = np.exp(xs.astype(np.float64))
+    m = t > 1.2e-38
+    ulp = np.abs(ys[m].astype(np.float64) - t[m]) / np.spacing(t[m].astype(np.float32)).astype(np.float64)
+    assert ulp.max() <= 1.5, ulp.max()
+    assert f(0.0) == 1.0 and f(-200.0) == 0.0 and f(float("nan")) == 0.0
+
+
+def test_shared_exp_oracle_differs_only_at_thresholds():
+    """The oracle with the shared exp (OracleRaster(shared_exp=True), the test_ref_alpha_exact
+    comparison's checker) against its libm-exp self on config 1: identical binning, images within
+    the tolerances of a 1-ulp exp difference."""
+    case = common.make_case()
+    a, ga = common.run_oracle(case)
+    sc, cam = case["scene"], case["cam"]
+    b = oracle.OracleRaster(sc["means3D"], sc["opacities"], case["bg"], cam.world_view_transform,
+                            cam.full_proj_transform, cam.camera_center, cam.tanfovx, cam.tanfovy, case["H"],
+                            case["W"], shs=sc["shs"], sh_degree=3, scales=sc["scales"], rotations=sc["rotations"],
+                            shared_exp=True)
+    gb = b.backward(case["grad_color"], case["grad_invdepth"])
+    np.testing.assert_array_equal(a.get("keys"), b.get("keys"))
+    np.testing.assert_array_equal(a.radii, b.radii)
+    common.check_render("oracle shared exp vs libm", {"color": b.color, "invdepth": b.invdepth,
+                                                      "final_T": b.get("final_T"), "n_contrib": b.get("n_contrib")},
+                        {"color": a.color, "invdepth": a.invdepth, "final_T": a.get("final_T"),
+                         "n_contrib": a.get("n_contrib")})
+    assert not np.array_equal(a.color, b.color)  # the switch is live
+    ok, rel = common.allclose_rel(gb["dL_dmeans3D"], ga["dL_dmeans3D"])
+    assert ok, rel

@@ -1,0 +1,167 @@
+"""The blend held bit-exact against the oracle (VERDICT r05 "next" #1; needs an MI355X: -m gpu).
+
+The production render kernels evaluate alpha as exp2 of a log2(e)-prescaled falloff (render.hip
+Falloff) -- not the reference's operation order (forward.cu:353-363, backward.cu:556-571) -- so an
+alpha within an ulp of 1/255 or of the T < 1e-4 stop can be decided differently from the oracle,
+and the production parity tests (test_gpu_parity, test_config2_parity, test_chair_gpu) carry
+tolerances for those flipped pixels.  This file proves that those flips are the ONLY difference:
+
+* it loads the test-only GSR_REF_ALPHA build of the same kernels
+  (gaussian-splatting-npu_amd/refalpha/libgsr_hip_refalpha.so, `make refalpha`, or the path in
+  $GSR_REF_ALPHA_LIB; the package never loads it), whose render_fwd / render_bwd compute power and
+  alpha in the reference's order with contraction off and the exp() of csrc/gsr_ref_exp.h;
+* it runs the oracle with that same exp (OracleRaster(shared_exp=True): one routine, written
+  once, compiled into both);
+* and asserts, on config 1's fixture inputs (every input mode, antialiasing on/off, the
+  reference's PLY hand cases), config 2 (1M Gaussians, 1080p) and the five chair cases:
+  - num_rendered, radii, the sorted keys / values / ranges bit-exact (as everywhere);
+  - colour, inverse depth, final_T and n_contrib BIT-EXACT: zero flipped pixels, no tolerance;
+  - every backward output within GRAD_RTOL = 1e-4 of its max|ref| (+1e-6) for EVERY Gaussian --
+    no attributed rows, no rows left out -- and the per-element relative bounds of
+    common.check_rel over all rows.  The gradients are not bit-exact by design: render_bwd sums
+    each Gaussian's per-pixel terms on chip in a fixed order where the reference adds them with
+    float atomics in no fixed order (backward.cu:593-635), and rebuilds T with v_rcp_f32.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import common
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda:0") if torch.cuda.is_available() else None
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF_LIB = os.environ.get("GSR_REF_ALPHA_LIB",
+                         os.path.join(ROOT, "gaussian-splatting-npu_amd", "refalpha", "libgsr_hip_refalpha.so"))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+NAMES = ["dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+         "dL_drotations"]
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def ref_lib():
+    """Swaps the test build in as _C's library for this module (every _C op calls through _C.lib)."""
+    import diff_gaussian_rasterization as dgr
+    lib = dgr._C._load(REF_LIB)
+    assert b"ref-alpha" in lib.gsr_version(), lib.gsr_version()
+    saved = dgr._C.lib
+    dgr._C.lib = lib
+    try:
+        yield lib
+    finally:
+        dgr._C.lib = saved
+
+
+def _t(x):
+    return torch.Tensor([]) if x is None else torch.as_tensor(np.ascontiguousarray(x, np.float32)).to(DEV)
+
+
+def run_exact(tag, H, W, inp, cam, sh_degree, antialiasing, bg, scale_modifier, grad_color, grad_invdepth,
+              truth=True):
+    """inp: means3D, opacities and one of shs / colors_precomp and of (scales, rotations) /
+    cov3D_precomp as numpy arrays (None = absent); cam: (viewmatrix, projmatrix, campos, tanfovx,
+    tanfovy).  The exact-blend assertions of the module docstring; returns the parity-log entries."""
+    import diff_gaussian_rasterization as dgr
+    import oracle
+    from test_gpu_parity import _img_state
+    view, proj, campos, tfx, tfy = cam
+    o = oracle.OracleRaster(inp["means3D"], inp["opacities"], bg, view, proj, campos, tfx, tfy, H, W,
+                            shs=inp.get("shs"), sh_degree=sh_degree, colors_precomp=inp.get("colors_precomp"),
+                            scales=inp.get("scales"), rotations=inp.get("rotations"),
+                            cov3D_precomp=inp.get("cov3D_precomp"), scale_modifier=scale_modifier,
+                            antialiasing=antialiasing, nthreads=THREADS, shared_exp=True)
+    og = o.backward(grad_color, grad_invdepth)
+    P = np.asarray(inp["means3D"]).shape[0]
+    g = {k: _t(inp.get(k)) for k in ("means3D", "opacities", "shs", "colors_precomp", "scales", "rotations",
+                                      "cov3D_precomp")}
+    bg_d, vm, pm, cp = _t(bg), _t(view), _t(proj), _t(campos)
+    L, color, radii, geom, binning, img, inv = dgr._C.rasterize_gaussians(
+        bg_d, g["means3D"], g["colors_precomp"], g["opacities"], g["scales"], g["rotations"], scale_modifier,
+        g["cov3D_precomp"], vm, pm, tfx, tfy, H, W, g["shs"], sh_degree, cp, False, antialiasing, False)
+    torch.cuda.synchronize()
+    assert L == o.num_rendered, f"{tag}: num_rendered {L} vs {o.num_rendered}"
+    np.testing.assert_array_equal(radii.cpu().numpy(), o.radii)
+    keys, vals, ranges = dgr._C.sorted_keys(geom, binning, img, P, L, W, H)
+    np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"))
+    np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"))
+    np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"))
+    del keys, vals
+    fT, nc = _img_state(img, W, H)
+    hip_r = {"color": color.cpu().numpy(), "invdepth": inv.cpu().numpy(), "final_T": fT, "n_contrib": nc}
+    ora_r = {"color": o.color, "invdepth": o.invdepth, "final_T": o.get("final_T"), "n_contrib": o.get("n_contrib")}
+    # through check_render for the log (0 flipped pixels expected), then bit for bit
+    st = common.check_render(tag + " [ref-alpha]", hip_r, ora_r)
+    for k in ("color", "invdepth", "final_T", "n_contrib"):
+        a, b = np.ascontiguousarray(hip_r[k]), np.ascontiguousarray(ora_r[k])
+        diff = int((a.reshape(-1).view(np.uint32) != b.reshape(-1).view(np.uint32)).sum())
+        assert diff == 0, f"{tag}: {k} differs from the oracle in {diff} values ({st})"
+    assert st["flipped"] == 0 and st["decision_suspects"] == 0, st
+
+    out = dgr._C.rasterize_gaussians_backward(
+        bg_d, g["means3D"], radii, g["colors_precomp"], g["opacities"], g["scales"], g["rotations"], scale_modifier,
+        g["cov3D_precomp"], vm, pm, tfx, tfy, _t(grad_color), _t(grad_invdepth), g["shs"], sh_degree, cp, geom, L,
+        binning, img, antialiasing, False)
+    torch.cuda.synchronize()
+    g64 = o.backward(grad_color, grad_invdepth, f64=True) if truth else None
+    for n, t in zip(NAMES, out):
+        if t.numel() == 0:
+            continue
+        hip, ref = t.cpu().numpy(), og[n].reshape(t.shape)
+        ok, rel = common.allclose_rel(hip, ref)  # GRAD_RTOL 1e-4 of max|ref| + 1e-6, every element
+        none = np.zeros(P, bool)
+        ast = common.check_grad_attributed(f"{tag} [ref-alpha] {n}", hip, ref, none)  # logs; no row may be over
+        assert ok and ast["rows_over"] == 0, f"{tag}: {n} max err {rel:.3e} of max|ref| ({ast})"
+        so = None
+        if truth:
+            so = common.check_rel_truth(f"{tag} [ref-alpha] {n}", hip, ref, g64[n].reshape(t.shape))[1]
+        common.check_rel(f"{tag} [ref-alpha] {n}", hip, ref, None, so)  # no rows left out
+    return st
+
+
+def _golden_files():
+    return sorted(os.path.join(GOLDEN, f) for f in os.listdir(GOLDEN) if f.endswith(".npz")) \
+        if os.path.isdir(GOLDEN) else []
+
+
+@pytest.mark.parametrize("path", _golden_files(), ids=lambda p: p.rsplit("/", 1)[-1])
+def test_ref_alpha_config1_fixture_inputs(ref_lib, path):
+    """Config 1 (1k Gaussians, 256x256, every input mode, aa on/off) and the PLY hand cases, on the
+    committed fixtures' inputs (the fixtures' stored outputs are the libm-exp oracle's: not used)."""
+    z = np.load(path, allow_pickle=False)
+    inp = {k: (z[k] if z[k].size else None) for k in ("means3D", "opacities", "shs", "colors_precomp", "scales",
+                                                      "rotations", "cov3D_precomp")}
+    cam = (z["viewmatrix"], z["projmatrix"], z["campos"], float(z["tanfovx"]), float(z["tanfovy"]))
+    run_exact(path.rsplit("/", 1)[-1], int(z["H"]), int(z["W"]), inp, cam, int(z["sh_degree"]),
+              bool(z["antialiasing"]), z["bg"], float(z["scale_modifier"]), z["grad_color"], z["grad_invdepth"])
+
+
+@pytest.mark.parametrize("antialiasing", [False, True])
+def test_ref_alpha_config2(ref_lib, antialiasing):
+    """Config 2 at full size: 1M Gaussians, SH degree 3, 1920x1080 ring view 0."""
+    case = common.make_case(P=1_000_000, H=1080, W=1920)
+    sc, c = case["scene"], case["cam"]
+    inp = {k: sc[k].numpy() for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    cam = (c.world_view_transform.numpy(), c.full_proj_transform.numpy(), c.camera_center.numpy(), c.tanfovx,
+           c.tanfovy)
+    run_exact(f"config2 aa={antialiasing}", 1080, 1920, inp, cam, 3, antialiasing, case["bg"].numpy(), 1.0,
+              case["grad_color"].numpy(), case["grad_invdepth"].numpy())
+
+
+@pytest.mark.parametrize("case", [0, 1, 2, 3, 4])
+def test_ref_alpha_chair(ref_lib, case):
+    """The NeRF-synthetic chair fixture's five cases (real geometry; cases 3/4 with rotations and
+    anisotropic scales)."""
+    import synthetic
+    from test_chair import load_chair
+    f, base, cases = load_chair()
+    cam, deg, aa, bg, seed, scene = cases[case]
+    H, W = cam.image_height, cam.image_width
+    inp = {k: scene[k].numpy() for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    gc, gi = synthetic.make_grads(H, W, seed=seed)
+    camt = (cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), cam.camera_center.numpy(),
+            cam.tanfovx, cam.tanfovy)
+    run_exact(f"chair case {case}", H, W, inp, camt, deg, aa, np.asarray(bg, np.float32), 1.0, gc.numpy(), gi.numpy())
