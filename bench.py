@@ -67,7 +67,8 @@ def parse(argv=None):
                     help="> 0: weak scaling, this many views per rank at every N (overrides --views-total)")
     ap.add_argument("--antialiasing", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpu count)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = every usable host core (affinity mask, bounded by a cgroup CPU quota)")
     ap.add_argument("--cpu-reps", type=int, default=10,
                     help="CPU baseline runs (median reported; ~1 s each at the default workload)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -130,8 +131,10 @@ def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1, diff_cells=0):
         "scan": P * 8,                                          # depth-ordered tile counts in, offsets out
         # ids, offsets, rects, record starts in; (tile, (record slot, id)) per instance + valid bits out
         "emit_instances": P * 20 + L * 12 + L // 8,
-        # (tile, slot, id) in, (slot, id) out -- (tile, slot, id) out without the difference array
-        "tile_sort": L * (20 if diff_cells else 24),
+        # with the difference array (slotless, emission fused into pass 1): depth-ordered ids, offsets and
+        # packed rects in per Gaussian, the 4-B id word out (pass 1), in and out (pass 2); without it,
+        # (tile, slot, id) in and out
+        "tile_sort": P * 12 + L * 12 if diff_cells else L * 24,
         # tile_hist: packed rects in, 16 workgroup arrays added; else a pass over the sorted tile ids
         "tile_ranges": P * 4 + 16 * 4 * diff_cells if diff_cells else L * 4 + T * 8,
         # the mean of its two launches per view: the forward's (ranges in, launch order out -- with the
@@ -139,9 +142,11 @@ def algorithmic_bytes(P, M, L, N, T, P_vis, views_per_bwd=1, diff_cells=0):
         # (per-tile work in, launch order out)
         "tile_order": ((4 * diff_cells + 12 * T if diff_cells else 12 * T) + 8 * T) // 2,
         "render_fwd": L * 44 + N * 24 + T * 8,                  # id + 40 B record per instance; 24 B/pixel out
-        "render_bwd": L * 44 + N * 24 + T * 8,                  # id + record per instance; 24 B/pixel in
-        # params + radii + 48 B/G render grads in, parameter gradients out
-        "preprocess_bwd": P * params + views_per_bwd * (P * 4 + P_vis * 48) + P * (40 + 12 * M),
+        # id + record per instance, 24 B/pixel in; the 40-B gradient record (GSR_GRAD_REC 10 floats) out
+        # per visible Gaussian (SURVEY §8d's per-Gaussian record, written once here, read once below)
+        "render_bwd": L * 44 + N * 24 + T * 8 + P_vis * 40,
+        # params + radii + the 40-B render gradient records in, parameter gradients out
+        "preprocess_bwd": P * params + views_per_bwd * (P * 4 + P_vis * 40) + P * (40 + 12 * M),
     }
 
 
@@ -293,6 +298,19 @@ def launch_ranks(args, argv, timeout=3000):
             os.unlink(pmc_file)
 
 
+def rank_views(args, rank, views_world):
+    """(scaling, n_ring, this rank's ring views, views per step over all ranks): weak scaling
+    (--views-per-rank K) gives every rank K distinct cameras of a ring of max(8, K x world) views;
+    strong scaling deals the fixed --views-total batch round-robin."""
+    from diff_gaussian_rasterization import multiview
+    if args.views_per_rank > 0:
+        n_ring = max(N_RING, args.views_per_rank * views_world)
+        views = multiview.views_for_rank(rank, views_world, args.views_per_rank, n_views=n_ring)
+        return "weak", n_ring, views, views_world * len(views)
+    n_ring = max(N_RING, args.views_total)
+    return "strong", n_ring, multiview.views_of_batch(rank, views_world, args.views_total), args.views_total
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
@@ -303,9 +321,12 @@ def main(argv=None):
         if env_world is not None and int(env_world) != args.gpus:
             print(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}", file=sys.stderr)
             sys.exit(2)
-    if args.rank_probe:
-        print(json.dumps({"rank": int(os.environ.get("RANK", "0")), "world": int(os.environ.get("WORLD_SIZE", "1")),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "argv": argv}), flush=True)
+    if args.rank_probe:  # (no GPU call: the views come from host arithmetic only)
+        r, w = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+        scaling, n_ring, views, views_step = rank_views(args, r, w)
+        print(json.dumps({"rank": r, "world": w, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "argv": argv,
+                          "scaling": scaling, "n_ring": n_ring, "views": views, "views_step": views_step}),
+              flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -346,14 +367,10 @@ def main(argv=None):
     scene = synthetic.make_scene(P, seed=0)
     params = {k: v.to(dev).requires_grad_(True) for k, v in scene.items()}
     M = params["shs"].shape[1]
-    if args.views_per_rank > 0:  # weak scaling: K views per rank, distinct cameras over all ranks
-        mode, scaling = "weak", "weak"
-        n_ring = max(N_RING, args.views_per_rank * views_world)
-        views = multiview.views_for_rank(rank, views_world, args.views_per_rank, n_views=n_ring)
-    else:  # strong scaling: a fixed batch of views per step, dealt round-robin
-        mode, scaling = "strong", "strong"
-        n_ring = max(N_RING, args.views_total)
-        views = multiview.views_of_batch(rank, views_world, args.views_total)
+    # weak scaling: K views per rank, distinct cameras over all ranks; strong: a fixed batch of views
+    # per step, dealt round-robin
+    mode, n_ring, views, _ = rank_views(args, rank, views_world)
+    scaling = mode
     views_step = world * len(views) if mode == "weak" else args.views_total
     cams, grads = [], []
     for v in views:
@@ -719,7 +736,7 @@ def aux_knn(points, args, reps=5):
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             n = 20000
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads = cpu_threads(args)
             sample = points[:n].cpu().numpy()
             t = time.perf_counter()
             oracle.knn_dist2(sample, nthreads=threads)
@@ -937,7 +954,7 @@ def aux_ssim(H, W, dev, args, reps=20):
         try:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import ssim_oracle
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads = cpu_threads(args)
             torch.set_num_threads(threads)
             ac, bc, uc = a.cpu(), b.cpu(), up.cpu()
             t = time.perf_counter()
@@ -950,6 +967,42 @@ def aux_ssim(H, W, dev, args, reps=20):
     return out
 
 
+def host_cpus():
+    """The host cores this process may use, and how that was found (the CPU baseline
+    runs on all host cores of the GPU box, with the count and CPU model reported).  The affinity
+    mask bounds it; a cgroup CPU quota (cpu.max: quota / period) bounds it further -- on a shared
+    box the mask may list the whole machine while the quota grants a share of it, and threads
+    beyond the quota only time-slice."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    n = min(aff, quota) if quota else aff
+    return n, {"nproc_affinity": aff, "cgroup_quota_cpus": quota, "os_cpu_count": os.cpu_count(), "cpu_model": model}
+
+
+def cpu_threads(args):
+    """--cpu-threads, or every usable host core (host_cpus)."""
+    return args.cpu_threads or host_cpus()[0]
+
+
 def cpu_baseline(args, scene, s, grad):
     """The CPU restatement behind the product's own C ABI (oracle/libgsr_cpu.so: gsr_forward with
     resize callbacks, then gsr_backward on the state buffers -- the host calling sequence of the
@@ -958,7 +1011,7 @@ def cpu_baseline(args, scene, s, grad):
     try:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_abi
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = cpu_threads(args)
         gc, gi = grad
         gc, gi = gc.cpu(), gi.cpu()
         cpu = cpu_abi.CpuRasterizer(nthreads=threads)
@@ -972,7 +1025,7 @@ def cpu_baseline(args, scene, s, grad):
             times.append(time.perf_counter() - t)
         dt = statistics.median(times)
         return {"value": round(s.image_height * s.image_width / dt / 1e6, 3), "unit": "Mpix/s", "cores": threads,
-                "kind": "port", "seconds": round(dt, 3), "runs_s": [round(x, 3) for x in times],
+                "kind": "port", **host_cpus()[1], "seconds": round(dt, 3), "runs_s": [round(x, 3) for x in times],
                 "sample": f"one full fwd+bwd of one bench view ({args.P} Gaussians, {s.image_width}x"
                           f"{s.image_height}) by the C/OpenMP restatement through gsr_forward/gsr_backward "
                           f"(oracle/libgsr_cpu.so), median of {len(times)} runs"}

@@ -28,9 +28,13 @@ namespace {
 thread_local std::string g_err;
 thread_local uint32_t* g_pinned = nullptr;
 constexpr uint32_t L_PENDING = 0xFFFFFFFFu;  // h[2] before the scan stores num_rendered (< 2^31)
-// forward_geometry_wait: the depth keys' range was too wide for the three-pass depth sort (h[1]); the
-// forward is re-run with four passes (set_depth_wide) -- internal, never returned to a caller
+// forward_geometry_wait: the depth keys' range was too wide for the three-pass depth sort (h[1]); that
+// call's depth sort and tile-count scan are re-run with four passes (depth_sort_rerun_wide) --
+// internal, never returned to a caller
 constexpr int GSR_RERUN_WIDE = -100;
+// depth-sort passes of this thread's last forward (per view: 3, or 4 after a re-run of its depth
+// sort; gsr_debug_last_depth_passes)
+thread_local int t_last_depth_passes[16] = {};
 
 int fail(int code, const char* msg)
 {
@@ -426,7 +430,8 @@ static OrderJob diff_order_job(char* ib, int width, int height, uint32_t gx, uin
 
 // After preprocess: the record-slot scan, the depth sort and the tile-count scan of one view.
 static int forward_geometry_sort(const PreprocessArgs& a, char* gb, char* ib, int width, int height, int P,
-                                 uint32_t* h_dev, hipStream_t s, bool debug, bool use_aux = true)
+                                 uint32_t* h_dev, hipStream_t s, bool debug, bool use_aux, SortJob* dsort_out,
+                                 ScanJob* off_out)
 {
     const GeomLayout g = geom_layout(P);
     // 1b. each Gaussian's first gradient-record slot: index-order exclusive scan of the tile counts
@@ -471,12 +476,14 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, char* ib, in
                      a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                      a.rect4};
         j.host_wide = h_dev + 1;
+        *dsort_out = j;
         e = radix_sort_batch(&j, 1, DEPTH_BITS, s);
     }
     if (debug && e == hipSuccess) e = hipStreamSynchronize(s);
 
     // 3. instance offsets in depth order (cub::DeviceScan::InclusiveSum, rasterizer_impl.cu:280)
     uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
+    *off_out = {offsets, offsets, P, a.scan_status, h_dev + 2};
     if (e == hipSuccess) {
         ProfScope ps_(PK_SCAN, s);
         e = launch_inclusive_scan(offsets, nullptr, offsets, P, a.scan_status, h_dev + 2, s);
@@ -498,8 +505,8 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
                                    float scale_modifier, const float* rotations, const float* cov3D_precomp,
                                    const float* viewmatrix, const float* projmatrix, const float* cam_pos,
                                    float tan_fovx, float tan_fovy, bool prefiltered, bool antialiasing, int* radii,
-                                   bool debug, gsr_stream_t stream, uint32_t** h_out, int slot = 0,
-                                   bool use_aux = true)
+                                   bool debug, gsr_stream_t stream, uint32_t** h_out, SortJob* dsort_out,
+                                   ScanJob* off_out, int slot = 0, bool use_aux = true)
 {
     hipStream_t s = (hipStream_t)stream;
     PreprocessArgs a;
@@ -515,7 +522,8 @@ static int forward_geometry_launch(char* geometry_buffer, char* image_buffer, in
         HIP_TRY(launch_preprocess(a, s));
     }
     DEBUG_SYNC(s);
-    return forward_geometry_sort(a, geometry_buffer, image_buffer, width, height, P, h_dev, s, debug, use_aux);
+    return forward_geometry_sort(a, geometry_buffer, image_buffer, width, height, P, h_dev, s, debug, use_aux,
+                                 dsort_out, off_out);
 }
 
 static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rendered)
@@ -536,14 +544,38 @@ static int forward_geometry_wait(uint32_t* h, gsr_stream_t stream, int* num_rend
     if (__atomic_load_n(&h[2], __ATOMIC_ACQUIRE) == L_PENDING) return fail(GSR_ERR_HIP, "scan did not publish num_rendered");
     if (h[0] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (__atomic_load_n(&h[1], __ATOMIC_ACQUIRE)) {  // (stored before the scan ran: visible with L)
-        set_depth_wide(true);
-        return GSR_RERUN_WIDE;
-    }
+    if (__atomic_load_n(&h[1], __ATOMIC_ACQUIRE)) return GSR_RERUN_WIDE;  // (stored before the scan ran: visible with L)
     if (h[2] > 0x7fffffffu) return fail(GSR_ERR_INVALID, "num_rendered overflows int");
     *num_rendered = (int)h[2];
     return GSR_OK;
 }
+
+// A view whose visible depth keys spanned too wide a range for the three-pass depth sort
+// (forward_geometry_wait returned GSR_RERUN_WIDE): its depth sort runs again in four 8-bit passes and
+// the tile-count scan re-publishes num_rendered (its status words cleared first), for THIS call only
+// -- the next forward starts with three passes again (the reference's sort keeps no state,
+// rasterizer_impl.cu:306-311).  Preprocess, the record-slot scan, the rects' difference array and the
+// forward tile order do not depend on the depth order and stand.  (What follows the scan -- the tile
+// sort's first-pass histograms -- is the caller's to enqueue again.)  h: the views' pinned words, whose
+// scans have published (no kernel still writes them).
+static int depth_sort_rerun_wide(SortJob* dsort, const ScanJob* off, uint32_t* const* h, int V, hipStream_t s)
+{
+    for (int v = 0; v < V; v++) {
+        h[v][1] = 0;
+        __atomic_store_n(&h[v][2], L_PENDING, __ATOMIC_RELEASE);
+        dsort[v].host_wide = nullptr;  // (four passes: no range to report)
+        HIP_TRY(hipMemsetAsync(off[v].status, 0, sizeof(uint64_t) * (size_t)scan_status_words(off[v].n), s));
+    }
+    {
+        ProfScope ps_(PK_DEPTH_SORT, s);
+        HIP_TRY(radix_sort_batch(dsort, V, DEPTH_BITS, s, 0, SORT_DEPTH, /*four_pass=*/true));
+    }
+    ProfScope ps_(PK_SCAN, s);
+    HIP_TRY(launch_scan_batch(off, V, false, s));
+    return GSR_OK;
+}
+
+int gsr_debug_last_depth_passes(int view) { return view >= 0 && view < 16 ? t_last_depth_passes[view] : 0; }
 
 int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
                          const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
@@ -559,18 +591,21 @@ int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, in
     hipStream_t ps = nullptr;
     int rc = prefix_begin((hipStream_t)stream, &ps);
     if (rc) return rc;
+    SortJob dsort;
+    ScanJob off;
     rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
                                  colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
                                  viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                 radii, debug, ps, &h);
+                                 radii, debug, ps, &h, &dsort, &off);
     if (rc) return rc;
     rc = forward_geometry_wait(h, ps, num_rendered);
+    t_last_depth_passes[0] = depth_force_wide() ? 4 : 3;
+    if (rc == GSR_RERUN_WIDE) {  // this call only: the depth sort in four passes
+        rc = depth_sort_rerun_wide(&dsort, &off, &h, 1, ps);
+        if (!rc) rc = forward_geometry_wait(h, ps, num_rendered);
+        t_last_depth_passes[0] = 4;
+    }
     const int rj = prefix_end((hipStream_t)stream, ps);
-    if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
-        return gsr_forward_geometry_dc(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
-                                       colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
-                                       viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                       radii, debug, stream, num_rendered);
     return rc ? rc : rj;
 }
 
@@ -757,38 +792,40 @@ int gsr_forward_prealloc_dc(char* geometry_buffer, char* image_buffer, char* bin
     hipStream_t ps = nullptr;
     int rc = prefix_begin((hipStream_t)stream, &ps);
     if (rc) return rc;
+    SortJob dsort;
+    ScanJob off;
     rc = forward_geometry_launch(geometry_buffer, image_buffer, P, D, M, width, height, means3D, dc, shs,
                                  colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
                                  viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                 radii, debug, ps, &h);
+                                 radii, debug, ps, &h, &dsort, &off);
     if (rc) return rc;
-    {
-        // the tile sort's first-pass histograms need only the depth-ordered rects and offsets (not L
-        // or the binning buffer): enqueued before the read-back, they run while the host waits
+    // the tile sort's first-pass histograms need only the depth-ordered rects and offsets (not L or
+    // the binning buffer): enqueued before the read-back, they run while the host waits
+    auto count_pass = [&]() -> int {
         const uint32_t gx = (uint32_t)((width + GSR_BLOCK_X - 1) / GSR_BLOCK_X);
         const int T = (int)(gx * (uint32_t)((height + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y));
         const TileSortJob cj = fused_tile_sort_job(geometry_buffer, nullptr, image_buffer, P, 0, width, height);
-        hipError_t e;
-        {
-            ProfScope ps_(PK_TILE_SORT, ps);
-            e = tile_sort_fused_batch(&cj, 1, gx, T, ps, FUSED_COUNT);
-        }
-        if (e != hipSuccess) {
-            prefix_end((hipStream_t)stream, ps);
-            return fail_hip(e, __LINE__);
-        }
+        ProfScope ps_(PK_TILE_SORT, ps);
+        const hipError_t e = tile_sort_fused_batch(&cj, 1, gx, T, ps, FUSED_COUNT);
+        return e == hipSuccess ? GSR_OK : fail_hip(e, __LINE__);
+    };
+    rc = count_pass();
+    if (rc) {
+        prefix_end((hipStream_t)stream, ps);
+        return rc;
     }
     int L = 0;
     rc = forward_geometry_wait(h, ps, &L);
+    t_last_depth_passes[0] = depth_force_wide() ? 4 : 3;
+    if (rc == GSR_RERUN_WIDE) {  // this call only: the depth sort in four passes, then its histograms again
+        rc = depth_sort_rerun_wide(&dsort, &off, &h, 1, ps);
+        if (!rc) rc = count_pass();
+        if (!rc) rc = forward_geometry_wait(h, ps, &L);
+        t_last_depth_passes[0] = 4;
+    }
     *num_rendered = L;
     if (rc) {
         prefix_end((hipStream_t)stream, ps);
-        if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
-            return gsr_forward_prealloc_dc(geometry_buffer, image_buffer, binning_buffer, binning_capacity, P, D, M,
-                                           background, width, height, means3D, dc, shs, colors_precomp, opacities,
-                                           scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
-                                           cam_pos, tan_fovx, tan_fovy, prefiltered, antialiasing, out_color, depth,
-                                           radii, debug, stream, num_rendered, rendered);
         return rc;
     }
     if (!binning_buffer || gsr_binning_buffer_size(L) > binning_capacity)  // caller allocates
@@ -910,29 +947,53 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         ProfScope ps_(PK_SCAN, ps);
         HIP_TRY(launch_scan_batch(off, V, false, ps));
     }
-    {
-        // the first tile-sort pass's histograms need only the depth-ordered rects and offsets: the
-        // GPU computes them while the host waits for L below
+    // the first tile-sort pass's histograms need only the depth-ordered rects and offsets: the GPU
+    // computes them while the host waits for L below
+    auto count_pass = [&](const int* which, int n) -> hipError_t {
         TileSortJob cj[MAX_VIEWS];
-        for (int v = 0; v < V; v++) cj[v] = fused_tile_sort_job(geometry_buffers[v], nullptr, image_buffers[v], P, 0, width, height);
+        for (int i = 0; i < n; i++)
+            cj[i] = fused_tile_sort_job(geometry_buffers[which[i]], nullptr, image_buffers[which[i]], P, 0, width, height);
         ProfScope ps_(PK_TILE_SORT, ps);
-        HIP_TRY(tile_sort_fused_batch(cj, V, gx, T, ps, FUSED_COUNT));
+        return tile_sort_fused_batch(cj, n, gx, T, ps, FUSED_COUNT);
+    };
+    {
+        int all[MAX_VIEWS];
+        for (int v = 0; v < V; v++) all[v] = v;
+        HIP_TRY(count_pass(all, V));
     }
     DEBUG_SYNC(ps);
-    // the one host hand-off: every view's num_rendered (rasterizer_impl.cu:283-284)
+    // the one host hand-off: every view's num_rendered (rasterizer_impl.cu:283-284); a view whose depth
+    // range was too wide for three passes re-runs its depth sort in four (this call only)
     int L[MAX_VIEWS];
+    int wide[MAX_VIEWS], nw = 0;
     for (int v = 0; v < V && !rc; v++) {
         rc = forward_geometry_wait(h[v], ps, &L[v]);
-        num_rendered[v] = L[v];
+        t_last_depth_passes[v] = depth_force_wide() ? 4 : 3;
+        if (rc == GSR_RERUN_WIDE) {
+            wide[nw++] = v;
+            rc = GSR_OK;
+        }
     }
+    if (!rc && nw) {
+        SortJob wj[MAX_VIEWS];
+        ScanJob wo[MAX_VIEWS];
+        uint32_t* wh[MAX_VIEWS];
+        for (int i = 0; i < nw; i++) {
+            wj[i] = dsort[wide[i]];
+            wo[i] = off[wide[i]];
+            wh[i] = h[wide[i]];
+            t_last_depth_passes[wide[i]] = 4;
+        }
+        rc = depth_sort_rerun_wide(wj, wo, wh, nw, ps);
+        if (!rc) {
+            const hipError_t e = count_pass(wide, nw);
+            if (e != hipSuccess) rc = fail_hip(e, __LINE__);
+        }
+        for (int i = 0; i < nw && !rc; i++) rc = forward_geometry_wait(h[wide[i]], ps, &L[wide[i]]);
+    }
+    for (int v = 0; v < V; v++) num_rendered[v] = rc ? 0 : L[v];
     if (rc) {
         prefix_end(caller, ps);
-        if (rc == GSR_RERUN_WIDE)  // once: the depth sort now runs four passes
-            return gsr_forward_views(V, P, D, M, background, width, height, means3D, dc, shs, colors_precomp,
-                                     opacities, scales, scale_modifier, rotations, cov3D_precomp, viewmatrices,
-                                     projmatrices, campos, tan_fovx, tan_fovy, prefiltered, antialiasing,
-                                     geometry_buffers, image_buffers, binning_buffers, binning_capacity, out_colors,
-                                     out_invdepths, radii, debug, stream, num_rendered, rendered);
         return rc;
     }
     // views whose binning buffer holds them: emission fused into the tile sort, tile ranges and
@@ -1500,11 +1561,11 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
     return GSR_OK;
 }
 
-int gsr_debug_depth_wide(void) { return depth_wide() ? 1 : 0; }
+int gsr_debug_depth_wide(void) { return depth_force_wide() ? 1 : 0; }
 
 int gsr_debug_set_depth_wide(int on)
 {
-    set_depth_wide(on != 0);
+    set_depth_force_wide(on != 0);
     return GSR_OK;
 }
 
@@ -1526,16 +1587,13 @@ int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* w
     uint32_t* v1 = reinterpret_cast<uint32_t*>(workspace + 3 * q);
     // the forward's call (forward_geometry_sort) without the rect gather
     HIP_TRY(radix_sort(n, DEPTH_BITS, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr, workspace + 4 * q, s));
-    if (!depth_wide()) {  // three passes: the range word says whether they sufficed (else four, as the forward)
+    if (!depth_force_wide()) {  // three passes: the range word says whether they sufficed (else four, as the forward)
         uint32_t rw[2] = {0u, 1u};
         HIP_TRY(hipMemcpyAsync(rw, workspace + 4 * q + radix_range_offset(n), 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
         if (!rw[1]) {
-            set_depth_wide(true);
-            const hipError_t e = radix_sort(n, DEPTH_BITS, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr,
-                                            workspace + 4 * q, s);
-            set_depth_wide(false);
-            HIP_TRY(e);
+            const SortJob j = {n, keys, nullptr, k0, v0, k1, v1, out_ids, nullptr, nullptr, workspace + 4 * q};
+            HIP_TRY(radix_sort_batch(&j, 1, DEPTH_BITS, s, 0, SORT_DEPTH, /*four_pass=*/true));
         }
     }
     return GSR_OK;

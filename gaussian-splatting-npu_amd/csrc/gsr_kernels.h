@@ -229,18 +229,21 @@ struct SortJob {  // radix_sort's arguments for one view
     // the three-pass depth sort: a pinned host word set to 1 when the keys' range was too wide for it
     uint32_t* host_wide = nullptr;
 };
-// After a depth sort reported a range too wide for three 9-bit passes (SortJob::host_wide): every
-// later depth sort runs four 8-bit passes (process-wide).
-void set_depth_wide(bool on);
-bool depth_wide();
+// After a depth sort reported a range too wide for three 9-bit passes (SortJob::host_wide), the
+// forward re-runs that sort with four_pass (radix_sort_batch), for that call only.  Test hook: force
+// four passes for every depth sort of the calling host thread.
+void set_depth_force_wide(bool on);
+bool depth_force_wide();
 // byte offset, inside a sort's scratch (radix_status_bytes(n)), of its {base, fits} range word
 size_t radix_range_offset(int n);
 // which sort a radix pass serves (selects the kernels' name tag only: profiles attribute dispatches)
 enum SortKind { SORT_DEPTH = 0, SORT_TILE = 1, SORT_CELLS = 2 };
 // V independent stable sorts over the same bit width (key bits [shift0, shift0 + nbits)), pass by
 // pass in shared launches.
+// four_pass: the depth sort (32-bit keys, shift0 0) in four 8-bit passes instead of three 9-bit ones
+// (keys whose range is too wide for the relative third pass).
 hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0 = 0,
-                            SortKind kind = SORT_DEPTH);
+                            SortKind kind = SORT_DEPTH, bool four_pass = false);
 
 // Emission fused into the tile sort (gsr_forward_views): the instances are generated from the
 // depth-ordered rects inside the first radix pass's count and scatter kernels instead of being

@@ -80,8 +80,9 @@ static inline unsigned scatter_grid(int maxc) { return GSR_XCD_CHUNKS ? (unsigne
 // sort exactly whenever the keys other than 0xFFFFFFFF span at most 511 values of k >> 18 (visible
 // depths within a factor of ~2^16: 0.2 ... 13,000).  Pass 1 gathers the range (per-chunk min / max,
 // reduced by an extra workgroup of its scan into RangeWord).  A wider range is reported to the host
-// (SortJob::host_wide, a pinned word it reads with num_rendered): the forward then runs again with
-// the four-pass 8-bit sort (set_depth_wide), and keeps it from then on.
+// (SortJob::host_wide, a pinned word it reads with num_rendered): that call's depth sort then runs
+// again in four 8-bit passes (radix_sort_batch four_pass; capi.hip depth_sort_rerun_wide) -- per call,
+// no state is kept.
 // mode: DIG_RAW (k >> shift) & mask; DIG_REL (the relative digit above when the range fits, else raw).
 enum DigitMode { DIG_RAW = 0, DIG_REL = 1 };
 struct RangeWord { uint32_t base, fits; };  // min >> rel_shift of the keys other than 0xFFFFFFFF; range fits
@@ -1185,21 +1186,23 @@ size_t radix_range_offset(int n)
 // One radix pass of a sort: digit width, key shift, DigitMode.
 struct PassSpec { int w, shift, mode; };
 // The full 32-bit key sorts (the depth sort) in three 9-bit passes, the third relative to the keys'
-// minimum (DigitMode); after a range that did not fit (set_depth_wide), four 8-bit passes.
+// minimum (DigitMode); after a range that did not fit (four_pass), four 8-bit passes.
 constexpr int DEPTH3_PASSES = 3;
 constexpr PassSpec DEPTH3[DEPTH3_PASSES] = {{9, 0, DIG_RAW}, {9, 9, DIG_RAW}, {9, 18, DIG_REL}};
 #ifndef GSR_DEPTH3
 #define GSR_DEPTH3 1
 #endif
-static bool g_depth_wide = !GSR_DEPTH3;
-void set_depth_wide(bool on) { g_depth_wide = on || !GSR_DEPTH3; }
-bool depth_wide() { return g_depth_wide; }
+// test hook (gsr_debug_set_depth_wide): this host thread's depth sorts run four passes
+static thread_local bool t_force_wide = false;
+void set_depth_force_wide(bool on) { t_force_wide = on; }
+bool depth_force_wide() { return t_force_wide || !GSR_DEPTH3; }
 
 template <typename KIND>
-static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0)
+static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0, bool four_pass)
 {
     if (nbits < 1) nbits = 1;
-    const bool depth3 = !g_depth_wide && nbits == 32 && shift0 == 0 && std::is_same<KIND, DepthSort>::value;
+    const bool depth3 = !four_pass && !depth_force_wide() && nbits == 32 && shift0 == 0 &&
+                        std::is_same<KIND, DepthSort>::value;
     const int npass = depth3 ? DEPTH3_PASSES : (nbits + 7) / 8;
     return for_groups(V, [&](int v0, int nv) -> hipError_t {
         int maxc = 0;
@@ -1318,12 +1321,13 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
     });
 }
 
-hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0, SortKind kind)
+hipError_t radix_sort_batch(const SortJob* jobs, int V, int nbits, hipStream_t s, int shift0, SortKind kind,
+                            bool four_pass)
 {
     switch (kind) {
-    case SORT_TILE: return radix_sort_batch_k<TileSort>(jobs, V, nbits, s, shift0);
-    case SORT_CELLS: return radix_sort_batch_k<CellSort>(jobs, V, nbits, s, shift0);
-    default: return radix_sort_batch_k<DepthSort>(jobs, V, nbits, s, shift0);
+    case SORT_TILE: return radix_sort_batch_k<TileSort>(jobs, V, nbits, s, shift0, four_pass);
+    case SORT_CELLS: return radix_sort_batch_k<CellSort>(jobs, V, nbits, s, shift0, four_pass);
+    default: return radix_sort_batch_k<DepthSort>(jobs, V, nbits, s, shift0, four_pass);
     }
 }
 

@@ -714,6 +714,8 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
 #pragma clang fp contract(fast)
     const RenderBwdArgs& a = B.v[blockIdx.y];  // a batch of views: one launch tail per batch
     constexpr int G = 3;  // entries per group and transposed reduction (3 x 10 gradient terms <= 32 values)
+    // a pass evaluates <= 32 entries per quadrant (the two-pass split below): they must fit the rows
+    static_assert(G * BWD_PART_BLOCKS >= 32, "partial rows: a half batch's 32 entries per quadrant");
     const int wv = BWD_TPW == 1 ? 0 : (int)(threadIdx.x >> 6);
     const int ti = (int)blockIdx.x * BWD_TPW + wv;
     if (ti >= a.T) return;  // waves are independent: no workgroup barrier below
@@ -832,7 +834,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         // entries per quadrant.  An entry is evaluated and stored in one pass.
         int big = 0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) big |= __popcll(__ballot((m >> q) & 1u)) > 3 * BWD_PART_BLOCKS;
+        for (int q = 0; q < 4; q++) big |= __popcll(__ballot((m >> q) & 1u)) > G * BWD_PART_BLOCKS;
         for (int hp = big ? 1 : 0; hp >= 0; hp--) {
             const uint32_t mm = (big && (lane >> 5) != hp) ? 0u : m;
             const uint64_t any = __ballot(mm != 0);

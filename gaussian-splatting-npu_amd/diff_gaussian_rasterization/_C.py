@@ -71,6 +71,8 @@ def _load(path=LIB_PATH):
     if hasattr(lib, "gsr_debug_set_depth_wide"):  # (test hooks; absent from libraries built before them)
         lib.gsr_debug_depth_wide.argtypes = []
         lib.gsr_debug_set_depth_wide.argtypes = [_i]
+    if hasattr(lib, "gsr_debug_last_depth_passes"):
+        lib.gsr_debug_last_depth_passes.argtypes = [_i]
     for n in ("gsr_geometry_layout", "gsr_binning_layout"):
         getattr(lib, n).argtypes = [_i, ctypes.POINTER(_sz), _i]
     lib.gsr_image_layout.argtypes = [_i, _i, ctypes.POINTER(_sz), _i]
@@ -708,14 +710,20 @@ def depth_sort(keys):
 
 
 def depth_wide():
-    """True once a forward saw visible depths too widely spread for the three-pass depth sort: every
-    later depth sort of the process runs four 8-bit passes (test hook)."""
+    """Test hook: True while this host thread's depth sorts are forced to four 8-bit passes
+    (set_depth_wide).  Forwards never set it: a too-wide depth range re-runs that call's sort only."""
     return bool(lib.gsr_debug_depth_wide())
 
 
 def set_depth_wide(on):
-    """Test hook: force (True) or release (False) the four-pass depth sort."""
+    """Test hook: force (True) or release (False) the four-pass depth sort for this host thread."""
     _check(lib.gsr_debug_set_depth_wide(1 if on else 0))
+
+
+def last_depth_passes(view=0):
+    """Test hook: the passes of the final depth sort of view `view` in this thread's last forward (3,
+    or 4 when its visible depth range was too wide for three and the sort was re-run)."""
+    return int(lib.gsr_debug_last_depth_passes(int(view)))
 
 
 def fusedssim(C1, C2, img1, img2):

@@ -528,7 +528,11 @@ class DataParallelTrainer:
         rows of each gradient and of the visibility counts go to an asynchronous all_reduce(SUM) at
         once; then, range by range, the optimizer waits for that range's collectives only and runs
         SparseGaussianAdam on its rows -- range k's update runs while range k+1 is still being
-        reduced.  Bit-identical to reduce() + optimizer_step(): the same sums, a row-wise update.
+        reduced.  With 2 ranks this is bit-identical to reduce() + optimizer_step() (a + b commutes;
+        tests/test_dp_train.py).  With more ranks a ring all-reduce adds each element's terms in an
+        order that depends on how the buffer is split across the ring, so reducing range by range can
+        round differently from one flat reduction: the result is then identical on every rank (the
+        replicas stay in sync) but not bit-identical to the unpipelined path -- not pinned by a test.
         (Iterations that densify or reset opacities keep the unpipelined order: the reference
         densifies between the reduction and the step.)"""
         P = self.P

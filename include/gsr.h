@@ -394,12 +394,17 @@ int gsr_debug_sorted_keys(const char* geometry_buffer, const char* binning_buffe
 size_t gsr_debug_depth_sort_workspace_size(int n);
 int gsr_debug_depth_sort(const uint32_t* keys, int n, uint32_t* out_ids, char* workspace, gsr_stream_t stream);
 
-/* The depth sort runs three 9-bit passes, the third relative to the smallest visible key; a forward
- * whose visible depth keys span too wide a range for that (depths beyond a factor of ~2^16) is re-run
- * with four 8-bit passes, which every later forward of the process then keeps.  Test hooks: read /
- * set that mode (1 = four passes). */
+/* The depth sort runs three 9-bit passes, the third relative to the smallest visible key; in a forward
+ * whose visible depth keys span too wide a range for that (depths beyond a factor of ~2^16) that
+ * view's depth sort and tile-count scan run again in four 8-bit passes -- for that call only, no
+ * state is kept (the reference's sort is stateless, rasterizer_impl.cu:306-311).
+ * Test hooks: gsr_debug_set_depth_wide(1) forces four passes for every depth sort of the calling host
+ * thread (0 releases it; gsr_debug_depth_wide reads it); gsr_debug_last_depth_passes(v) = the passes
+ * the final depth sort of view v of this thread's last forward ran (3, or 4 after a re-run or when
+ * forced; 0 before any forward). */
 int gsr_debug_depth_wide(void);
 int gsr_debug_set_depth_wide(int on);
+int gsr_debug_last_depth_passes(int view);
 
 /* Byte offsets of the arrays inside each opaque state buffer (n entries
  * written, count of arrays returned; entry [count] is the total size).  For
