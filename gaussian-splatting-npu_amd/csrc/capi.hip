@@ -577,6 +577,8 @@ static int depth_sort_rerun_wide(SortJob* dsort, const ScanJob* off, uint32_t* c
 
 int gsr_debug_last_depth_passes(int view) { return view >= 0 && view < 16 ? t_last_depth_passes[view] : 0; }
 
+int gsr_debug_grad_record_floats(void) { return GRAD_REC; }
+
 int gsr_forward_geometry_dc(char* geometry_buffer, char* image_buffer, int P, int D, int M, int width, int height,
                          const float* means3D, const float* dc, const float* shs, const float* colors_precomp,
                          const float* opacities, const float* scales, float scale_modifier,

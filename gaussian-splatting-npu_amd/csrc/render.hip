@@ -38,6 +38,12 @@
 namespace gsr {
 
 constexpr int BATCH = 256;
+#ifndef GSR_DIAG_BWD_NOSTORE
+#define GSR_DIAG_BWD_NOSTORE 0
+#endif
+#ifndef GSR_FWD_HITLANE
+#define GSR_FWD_HITLANE 1
+#endif
 
 // Pixel of thread `tid` in tile (tx, ty): wave w covers the 8x8 quadrant (w & 1, w >> 1).
 __device__ __forceinline__ void quad_pixel(uint32_t tx, uint32_t ty, int tid, uint32_t& px, uint32_t& py)
@@ -392,7 +398,13 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             const int jr = r * 64 + lane;
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
+#if GSR_FWD_HITLANE
+            // lane jl of hitv: nonzero iff some pixel of the wave blended entry (r, jl) -- one v_writelane
+            // per entry instead of a scalar select and or; the round's bits are one ballot at its end
+            uint32_t hitv = 0;
+#else
             uint64_t hitbits = 0;  // wave-uniform
+#endif
             // two entries per iteration with ping-pong record registers (no rotation copies).  take():
             // the lowest set bit (s_ff1, -1 once none is left) and its clear (one s_bitset0; with
             // none left it clears bit 63 of a zero mask), as the batch position r * 64 + bit
@@ -421,6 +433,14 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 live = stop ? 0.0f : live;
                 const float ae = stop ? 0.0f : (contrib ? a : 0.0f);
                 const bool blended = ae > 0.0f;
+#if GSR_FWD_HITLANE
+                {
+                    const uint64_t bal = __ballot(blended);
+                    asm volatile("v_writelane_b32 %0, %1, %2"
+                                 : "+v"(hitv)
+                                 : "s"((uint32_t)bal | (uint32_t)(bal >> 32)), "{m0}"(j - r * 64));
+                }
+#else
                 {  // hitbits |= (any lane blended) ? bit j : 0 -- as one 64-bit scalar select (the
                    // compiler splits it into two 32-bit ones: one scalar instruction more per entry)
                     uint64_t t;
@@ -430,6 +450,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                         : "scc");
                     hitbits |= t;
                 }
+#endif
 #if GSR_REF_ALPHA  // features * alpha * T, left to right (forward.cu:373-375)
                 C0 += col.x * ae * T;
                 C1 += col.y * ae * T;
@@ -464,6 +485,9 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 blend(jb, bxy, bco, bcol);
                 if (--left == 0 || __all(live == 0.0f)) break;
             }
+#if GSR_FWD_HITLANE
+            const uint64_t hitbits = __ballot(hitv != 0u);
+#endif
             if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
         }
     }
@@ -902,7 +926,7 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // one gradient record per contributing entry, stored by its own lane: its quadrant partials
             // summed as (q0 + q2) + (q1 + q3), a fixed order (bitwise reproducible)
-            if (mm != 0) {
+            if (mm != 0 && !GSR_DIAG_BWD_NOSTORE) {  // (DIAG: timing-only A/B build without the record stores)
                 float t0[GF_NUM], t1[GF_NUM];
 #pragma unroll
                 for (int f = 0; f < GF_NUM; f++) t0[f] = t1[f] = 0.f;

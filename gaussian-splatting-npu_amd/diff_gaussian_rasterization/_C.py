@@ -720,6 +720,11 @@ def set_depth_wide(on):
     _check(lib.gsr_debug_set_depth_wide(1 if on else 0))
 
 
+def grad_record_floats():
+    """Floats per per-instance gradient record (GSR_GRAD_REC of the library build; diagnostics)."""
+    return int(lib.gsr_debug_grad_record_floats())
+
+
 def last_depth_passes(view=0):
     """Test hook: the passes of the final depth sort of view `view` in this thread's last forward (3,
     or 4 when its visible depth range was too wide for three and the sort was re-run)."""

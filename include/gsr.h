@@ -406,6 +406,10 @@ int gsr_debug_depth_wide(void);
 int gsr_debug_set_depth_wide(int on);
 int gsr_debug_last_depth_passes(int view);
 
+/* Floats per per-instance gradient record in the binning buffer's GRAD_INST region (the build's
+ * GSR_GRAD_REC: 10 = 40 B), for diagnostics that decode the records. */
+int gsr_debug_grad_record_floats(void);
+
 /* Byte offsets of the arrays inside each opaque state buffer (n entries
  * written, count of arrays returned; entry [count] is the total size).  For
  * parity tests and debugging only; the layout is private to this library. */

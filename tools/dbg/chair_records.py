@@ -21,8 +21,8 @@ def main():
     case = int(sys.argv[1])
     ids = np.array([int(x) for x in sys.argv[2:]], np.int64)
     dev = torch.device("cuda:0")
-    f, scene, cases = load_chair()
-    cam, deg, aa, bg, seed = cases[case]
+    f, _, cases = load_chair()
+    cam, deg, aa, bg, seed, scene = cases[case]
     H, W, P = cam.image_height, cam.image_width, scene["means3D"].shape[0]
     sc = {k: v.to(dev).contiguous() for k, v in scene.items()}
     bg_t = torch.tensor(bg, dtype=torch.float32, device=dev)
@@ -46,7 +46,8 @@ def main():
     emit = garr(11, np.uint32, (P,))
     tt = garr(6, np.uint32, (P,))
     recs, slots = [], []
-    grad = bb[bl[3]:bl[3] + 48 * L].view(np.float32).reshape(L, 12)
+    rec = dgr._C.grad_record_floats()  # the build's record size (10 floats = 40 B)
+    grad = bb[bl[3]:bl[3] + 4 * rec * L].view(np.float32).reshape(L, rec)
     for g in ids:
         s = np.arange(emit[g], emit[g] + tt[g], dtype=np.int64)
         slots.append(s)

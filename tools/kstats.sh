@@ -1,9 +1,10 @@
 #!/bin/bash
-# rocprofv3 --kernel-trace --stats of a short default bench run for every ab/*.so (one run each);
+# rocprofv3 --kernel-trace --stats of a short bench run for every ab/*.so (one run each; $2: extra bench
+# flags, e.g. "--views-total 1 --per-view --no-deferred" for the single view);
 # prints the radix / render kernels' average durations per library.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${1:-r05ks}
+TAG=${1:-ks}
 EXTRA=${2:-}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"

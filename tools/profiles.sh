@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-5 evidence: PMC passes over the 8-view step and the single view (tools/pmc_views.sh), then
+# Round-end evidence: PMC passes over the 8-view step and the single view (tools/pmc_views.sh), then
 # rocprofv3 --kernel-trace --stats (CSV) of the default bench step and of the single-view bench.
 # Each GPU step under its own limit; stop at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${1:-r05prof}
+TAG=${1:-prof}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
