@@ -402,6 +402,9 @@ static int forward_geometry_args(char* geometry_buffer, char* image_buffer, int 
         a.rect = nullptr;
     }
     a.rec_mask = at<uint32_t>(gb, g.off[GEOM_REC_MASK]);
+    // the depth sort's chunk-group counts, zeroed by preprocess (SortJob::gsum_zeroed)
+    a.dsort_gsum = at<uint32_t>(gb, g.off[GEOM_RADIX_SCRATCH] + radix_gsum_offset(P));
+    a.dsort_gsum_words = (int)(radix_gsum_bytes(P) / 4);
     a.tile_diff = nullptr;
     a.tile_diff_words = 0;
     if (use_tile_diff(a.grid_x, a.grid_y)) {  // the tile ranges from the rects' difference array
@@ -476,6 +479,7 @@ static int forward_geometry_sort(const PreprocessArgs& a, char* gb, char* ib, in
                      a.rect, at<uint2>(gb, g.off[GEOM_SORTED_RECT]), at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]),
                      a.rect4};
         j.host_wide = h_dev + 1;
+        j.gsum_zeroed = true;  // (preprocess)
         *dsort_out = j;
         e = radix_sort_batch(&j, 1, DEPTH_BITS, s);
     }
@@ -913,6 +917,7 @@ int gsr_forward_views(int V, int P, int D, int M, const float* background, int w
         uint32_t* offsets = at<uint32_t>(gb, g.off[GEOM_POINT_OFFSETS]);
         off[v] = {offsets, offsets, P, a.scan_status, hdev[v] + 2};  // L -> the view's pinned word
         dsort[v].host_wide = hdev[v] + 1;
+        dsort[v].gsum_zeroed = true;  // (preprocess)
     }
     // the record-slot scans (read only by the fused tile sort) on the auxiliary stream, beside the
     // depth sorts

@@ -41,6 +41,8 @@ struct PreprocessArgs {
     int* tile_diff;   // IMG_TILE_DIFF, zeroed here (tile_hist adds into it), or null
     int tile_diff_words;
     uint32_t* rec_mask;  // GEOM_REC_MASK, zeroed here (render_bwd sets it)
+    uint32_t* dsort_gsum;  // the depth sort's chunk-group digit counts (radix_gsum_*), zeroed here, or null
+    int dsort_gsum_words;
 };
 
 struct RenderFwdArgs {
@@ -228,7 +230,14 @@ struct SortJob {  // radix_sort's arguments for one view
     const uint32_t* soa_y = nullptr;
     // the three-pass depth sort: a pinned host word set to 1 when the keys' range was too wide for it
     uint32_t* host_wide = nullptr;
+    // the three-pass depth sort's chunk-group counts (radix_gsum_offset/bytes inside `scratch`) are
+    // already zero (preprocess clears them); otherwise the sort clears them itself
+    bool gsum_zeroed = false;
 };
+// The chunk-group digit counts of the three-pass depth sort inside its scratch: byte offset and size
+// (zero-initialised by the caller, see SortJob::gsum_zeroed).
+size_t radix_gsum_offset(int n);
+size_t radix_gsum_bytes(int n);
 // After a depth sort reported a range too wide for three 9-bit passes (SortJob::host_wide), the
 // forward re-runs that sort with four_pass (radix_sort_batch), for that call only.  Test hook: force
 // four passes for every depth sort of the calling host thread.

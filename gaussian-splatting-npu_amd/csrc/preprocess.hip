@@ -261,6 +261,9 @@ __global__ void __launch_bounds__(PF_TPB) preprocess_fwd_kernel(const Preprocess
     for (int v = 0; v < V; v++)  // tile_hist adds into it after this kernel (grid-stride: P may be small)
         if (A.a[v].tile_diff)
             for (int c = idx; c < A.a[v].tile_diff_words; c += (int)gridDim.x * PF_TPB) A.a[v].tile_diff[c] = 0;
+    for (int v = 0; v < V; v++)  // the depth sort's count kernels add into them after this kernel
+        if (A.a[v].dsort_gsum)
+            for (int c = idx; c < A.a[v].dsort_gsum_words; c += (int)gridDim.x * PF_TPB) A.a[v].dsort_gsum[c] = 0u;
     // the Gaussian's own inputs first: their loads are in flight during the SH staging
     GaussIn gi;
     if (idx < a.P) gi = load_gauss(a, idx);

@@ -36,6 +36,16 @@ constexpr int RS_ITEMS_SHORT = 8;               // short sorts (the depth sort; 
 constexpr int RS_SHORT_MAX = 1 << 21;           // n up to which a sort counts as short
 constexpr int RS_MAXBINS = 256;
 constexpr int RS_SCRATCH_BINS = 512;            // count-matrix rows reserved per sort (9-bit depth digits)
+// GSR_DEPTH_GSUM: the three-pass depth sort launches no column scan.  Each count workgroup also adds
+// its digit counts into its chunk group's row (GS_CHUNKS chunks per group, atomic adds of integers:
+// exact in any order), and each scatter workgroup derives its own digit offsets from the group rows
+// and the chunk rows of its group in its prologue (<= 31 loads per digit at P = 1M) -- 3 launches per
+// depth sort fewer (the single view's train.py path runs its depth sort alone on the GPU: each launch
+// is latency, ~7 us).  The pass-3 key range is reduced by workgroup 0 of the pass-2 count kernel.
+#ifndef GSR_DEPTH_GSUM
+#define GSR_DEPTH_GSUM 1
+#endif
+constexpr int GS_CHUNKS = 16;
 
 // Kernel-name tags: which sort a radix pass belongs to (the depth sort, the tile sort's later
 // passes, distCUDA2's cell sort) -- the kernels are identical, the names let a profile (rocprofv3
@@ -122,7 +132,60 @@ struct CountJob {
     uint32_t* cmin;            // non-null: per-chunk min / max of the keys other than 0xFFFFFFFF
     uint32_t* cmax;
     bool cmaj;                 // chunk-major count matrix (cm_index)
+    // GSR_DEPTH_GSUM: non-null: each chunk's digit counts are also added into
+    // gsum[(chunk / GS_CHUNKS) * nb + d] (zero on entry)
+    uint32_t* gsum = nullptr;
+    // non-null: workgroup 0 reduces the per-chunk key min / max of an earlier pass (rcmin / rcmax,
+    // rnchunks chunks) into *range_out (the relative pass's RangeWord; reduce_range)
+    RangeWord* range_out = nullptr;
+    const uint32_t* rcmin = nullptr;
+    const uint32_t* rcmax = nullptr;
+    int rnchunks = 0, rel_shift = 0, rel_bits = 0;
+    uint32_t* host_wide = nullptr;
 };
+// The keys' range from per-chunk min / max (nchunks of them) -> *out (base, fits) for a relative pass
+// on bits [rel_shift, rel_shift + rel_bits); a range that does not fit is flagged in *host_wide.  Every
+// thread of the workgroup (NT threads) calls it.
+template <int NT>
+__device__ void reduce_range_nt(const uint32_t* cmin, const uint32_t* cmax, int nchunks, RangeWord* out, int rel_shift,
+                                int rel_bits, uint32_t* host_wide)
+{
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t s_rr[2][NW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (int c = tid; c < nchunks; c += NT) {
+        mn = min(mn, cmin[c]);
+        mx = max(mx, cmax[c]);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    }
+    if (lane == 0) {
+        s_rr[0][w] = mn;
+        s_rr[1][w] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        for (int q = 1; q < NW; q++) {
+            mn = min(mn, s_rr[0][q]);
+            mx = max(mx, s_rr[1][q]);
+        }
+        RangeWord r;
+        if (mn > mx) {  // nothing but 0xFFFFFFFF
+            r.base = 0u;
+            r.fits = 1u;
+        } else {
+            r.base = mn >> rel_shift;
+            // the largest relative digit stays below 2^rel_bits - 1, the digit of 0xFFFFFFFF
+            r.fits = ((mx >> rel_shift) - r.base) <= (1u << rel_bits) - 2u ? 1u : 0u;
+        }
+        *out = r;
+        if (!r.fits && host_wide) __hip_atomic_store(host_wide, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 template <int ITEMS, typename KIND, int MAXB, int NT = RS_THREADS>
 __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJob> B, int shift, int nbits)
 {
@@ -211,7 +274,10 @@ __global__ void __launch_bounds__(NT) radix_count_kernel(const ViewBatch<CountJo
 #pragma unroll
         for (int q = 0; q < NW; q++) c += h[q][d];
         J.counts[cm_index(d, chunk, nb, J.nchunks, J.cmaj)] = c;
+        if (J.gsum && c) atomicAdd(&J.gsum[(size_t)(chunk / GS_CHUNKS) * nb + d], c);
     }
+    if (J.range_out && chunk == 0) reduce_range_nt<NT>(J.rcmin, J.rcmax, J.rnchunks, J.range_out, J.rel_shift, J.rel_bits,
+                                                       J.host_wide);
     if (J.cmin && tid == 0) {
         uint32_t mn = s_mm[0][0], mx = s_mm[1][0];
         for (int q = 1; q < NW; q++) {
@@ -469,6 +535,9 @@ struct SortPassArgs {
     int mode;                // DigitMode
     const RangeWord* range;
     bool cmaj;               // chunk-major count matrix (cm_index)
+    // GSR_DEPTH_GSUM: non-null: row_prefix holds the raw chunk-major counts (no column scan ran) and
+    // gsum their per-group sums; the digit offsets are derived from both here
+    const uint32_t* gsum = nullptr;
 };
 
 // Exclusive scan of one value per thread over the 256-thread block: wave scans by shuffles, then
@@ -523,12 +592,44 @@ __global__ void __launch_bounds__(NT) radix_scatter_kernel(const ViewBatch<SortP
     // digit offsets: exclusive scan of the totals, plus this chunk's row prefix (thread t owns digits
     // [t DPT, t DPT + DPT))
     uint32_t tot[DPT], rowp[DPT], tsum = 0;
+    if (a.gsum) {  // digit d: its total = the sum of the group rows; this chunk's offset = the groups
+                   // before its own + the chunks of its group before it (chunk-major raw counts)
+        const uint32_t ng = ((uint32_t)a.nchunks + GS_CHUNKS - 1) / GS_CHUNKS, cg = chunk / GS_CHUNKS;
 #pragma unroll
-    for (int i = 0; i < DPT; i++) {
-        const uint32_t d = (uint32_t)(tid * DPT + i);
-        tot[i] = d < (uint32_t)NB ? a.totals[d] : 0u;
-        rowp[i] = d < (uint32_t)NB ? a.row_prefix[cm_index(d, chunk, NB, a.nchunks, a.cmaj)] : 0u;
-        tsum += tot[i];
+        for (int i = 0; i < DPT; i++) {
+            const uint32_t d = (uint32_t)(tid * DPT + i);
+            uint32_t t = 0, pre = 0;
+            if (d < (uint32_t)NB) {  // every load of a block issued before the first add (clamped)
+                for (uint32_t g0 = 0; g0 < ng; g0 += GS_CHUNKS) {
+                    uint32_t x[GS_CHUNKS];
+#pragma unroll
+                    for (int u = 0; u < GS_CHUNKS; u++) x[u] = a.gsum[(size_t)min(g0 + u, ng - 1) * NB + d];
+#pragma unroll
+                    for (int u = 0; u < GS_CHUNKS; u++) {
+                        const uint32_t g = g0 + u, v = g < ng ? x[u] : 0u;
+                        t += v;
+                        pre += g < cg ? v : 0u;
+                    }
+                }
+                const uint32_t c0 = cg * GS_CHUNKS, nprev = chunk - c0;  // < GS_CHUNKS
+                uint32_t y[GS_CHUNKS - 1];
+#pragma unroll
+                for (int u = 0; u < GS_CHUNKS - 1; u++) y[u] = a.row_prefix[(size_t)(c0 + min((uint32_t)u, chunk - c0)) * NB + d];
+#pragma unroll
+                for (int u = 0; u < GS_CHUNKS - 1; u++) pre += (uint32_t)u < nprev ? y[u] : 0u;
+            }
+            tot[i] = t;
+            rowp[i] = pre;
+            tsum += t;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < DPT; i++) {
+            const uint32_t d = (uint32_t)(tid * DPT + i);
+            tot[i] = d < (uint32_t)NB ? a.totals[d] : 0u;
+            rowp[i] = d < (uint32_t)NB ? a.row_prefix[cm_index(d, chunk, NB, a.nchunks, a.cmaj)] : 0u;
+            tsum += tot[i];
+        }
     }
     uint32_t gbase[DPT];
     {
@@ -1119,10 +1220,17 @@ static inline size_t rs_chunks(int n)
 // then the per-chunk key min / max and the RangeWord of a three-pass depth sort.
 static inline size_t rs_count_bytes(int n) { return align_up(rs_chunks(n) * RS_SCRATCH_BINS * 4 + 256, 256); }
 static inline size_t rs_totals_bytes() { return align_up(RS_SCRATCH_BINS * 4, 256); }
+// ... then the chunk-group digit counts of the three passes of a depth sort (GSR_DEPTH_GSUM)
+static inline size_t rs_gsum_stride(int n)
+{
+    return align_up((rs_chunks(n) + GS_CHUNKS - 1) / GS_CHUNKS * RS_SCRATCH_BINS * 4, 256);
+}
+size_t radix_gsum_offset(int n) { return rs_count_bytes(n) + rs_totals_bytes() + align_up(2 * rs_chunks(n) * 4 + 64, 256); }
+size_t radix_gsum_bytes(int n) { return 3 * rs_gsum_stride(n); }  // (DEPTH3_PASSES)
 size_t radix_status_bytes(int n, int npass)
 {
     (void)npass;
-    return rs_count_bytes(n) + rs_totals_bytes() + align_up(2 * rs_chunks(n) * 4 + 64, 256);
+    return radix_gsum_offset(n) + radix_gsum_bytes(n);
 }
 static_assert(RS_THREADS * RS_ITEMS == 2048 && RS_THREADS * RS_ITEMS_SHORT == 2048 && RS_MAXBINS == 256,
               "2,048-key chunks");
@@ -1158,6 +1266,10 @@ static inline RangeWord* sort_range(const SortJob& j)
 {
     return reinterpret_cast<RangeWord*>(sort_minmax(j) + 2 * ((rs_chunks(j.n) + 1) & ~(size_t)1));
 }
+static inline uint32_t* sort_gsum(const SortJob& j, int pass)
+{
+    return reinterpret_cast<uint32_t*>(j.scratch + radix_gsum_offset(j.n) + (size_t)pass * rs_gsum_stride(j.n));
+}
 
 // (2) for a pass of nbins digits over (up to) maxc chunks: the per-digit exclusive scans over the
 // chunks and the digit totals (+ the range workgroup)
@@ -1187,7 +1299,7 @@ size_t radix_range_offset(int n)
 struct PassSpec { int w, shift, mode; };
 // The full 32-bit key sorts (the depth sort) in three 9-bit passes, the third relative to the keys'
 // minimum (DigitMode); after a range that did not fit (four_pass), four 8-bit passes.
-constexpr int DEPTH3_PASSES = 3;
+constexpr int DEPTH3_PASSES = 3;  // (radix_gsum_bytes: one group matrix per pass)
 constexpr PassSpec DEPTH3[DEPTH3_PASSES] = {{9, 0, DIG_RAW}, {9, 9, DIG_RAW}, {9, 18, DIG_REL}};
 #ifndef GSR_DEPTH3
 #define GSR_DEPTH3 1
@@ -1204,7 +1316,16 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
     const bool depth3 = !four_pass && !depth_force_wide() && nbits == 32 && shift0 == 0 &&
                         std::is_same<KIND, DepthSort>::value;
     const int npass = depth3 ? DEPTH3_PASSES : (nbits + 7) / 8;
+    const bool gsum = depth3 && GSR_DEPTH_GSUM;  // no column-scan launches (see GS_CHUNKS)
     return for_groups(V, [&](int v0, int nv) -> hipError_t {
+        if (gsum)
+            for (int v = 0; v < nv; v++) {
+                const SortJob& j = jobs[v0 + v];
+                if (!j.gsum_zeroed && j.n > 0) {
+                    const hipError_t e = hipMemsetAsync(sort_gsum(j, 0), 0, radix_gsum_bytes(j.n), s);
+                    if (e != hipSuccess) return e;
+                }
+            }
         int maxc = 0;
         bool pair = false;
         for (int v = 0; v < nv; v++) {
@@ -1251,7 +1372,19 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 cb.v[v].hi_words = j.key_hi_shift ? j.soa_y : nullptr;
                 cb.v[v].mode = mode;
                 cb.v[v].range = sort_range(j);
-                cb.v[v].cmaj = chunk_major(maxc_p);
+                cb.v[v].cmaj = gsum || chunk_major(maxc_p);
+                if (gsum) {
+                    cb.v[v].gsum = sort_gsum(j, p);
+                    if (p == 1) {  // the pass-3 key range, from pass 1's per-chunk min / max
+                        cb.v[v].range_out = sort_range(j);
+                        cb.v[v].rcmin = sort_minmax(j);
+                        cb.v[v].rcmax = sort_minmax(j) + nchunks;
+                        cb.v[v].rnchunks = nchunks;  // (every pass of a depth sort: the same 4,096-key chunks)
+                        cb.v[v].rel_shift = DEPTH3[2].shift;
+                        cb.v[v].rel_bits = DEPTH3[2].w;
+                        cb.v[v].host_wide = j.host_wide;
+                    }
+                }
                 rb.v[v] = {sort_counts(j), nchunks, sort_totals(j)};
                 if (depth3 && p == 0) {  // the keys' range, for the relative pass
                     cb.v[v].cmin = sort_minmax(j);
@@ -1286,7 +1419,8 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
                 a.vals_in_y = (p == 0 && j.soa_x) ? j.soa_y : nullptr;
                 a.mode = mode;
                 a.range = sort_range(j);
-                a.cmaj = chunk_major(maxc_p);
+                a.cmaj = gsum || chunk_major(maxc_p);
+                a.gsum = gsum ? sort_gsum(j, p) : nullptr;
                 kin[v] = a.keys_out;
                 vin[v] = a.vals_out;
             }
@@ -1297,7 +1431,7 @@ static hipError_t radix_sort_batch_k(const SortJob* jobs, int V, int nbits, hipS
             else
                 hipLaunchKernelGGL((radix_count_kernel<RS_ITEMS, KIND, RS_MAXBINS>), g, b, 0, s, cb, shift, w);
             for (int v = 0; v < nv; v++) rb.v[v].nbins = 1 << w;
-            launch_scan_rows<KIND>(rb, nv, 1 << w, maxc_p, depth3 && p == 0, s);
+            if (!gsum) launch_scan_rows<KIND>(rb, nv, 1 << w, maxc_p, depth3 && p == 0, s);
             if (wide) {
                 if (pair)
                     hipLaunchKernelGGL((radix_scatter_kernel<RS_ITEMS, true, KIND, 9, RS_THREADS_WIDE>), gs, bw, 0, s, sb);
