@@ -38,11 +38,6 @@
 namespace gsr {
 
 constexpr int BATCH = 256;
-// render_fwd's blend as compares into scalar masks (GSR_FWD_MASKS, see the blend below)
-#ifndef GSR_FWD_MASKS
-#define GSR_FWD_MASKS 1
-#endif
-constexpr bool FWD_MASKS = GSR_FWD_MASKS && !GSR_REF_ALPHA;
 
 // Pixel of thread `tid` in tile (tx, ty): wave w covers the 8x8 quadrant (w & 1, w >> 1).
 __device__ __forceinline__ void quad_pixel(uint32_t tx, uint32_t ty, int tid, uint32_t& px, uint32_t& py)
@@ -360,9 +355,6 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
     __shared__ uint64_t s_hitw[4][BATCH / 64];
 
     float live = inside ? 1.0f : 0.0f;  // 0 once the pixel is finished (or outside the image)
-    // (GSR_FWD_MASKS: -inf once the pixel is finished or outside the image, else 0)
-    float thr = inside ? 0.0f : -__builtin_inff();
-    auto finished = [&]() -> bool { return FWD_MASKS ? thr < 0.0f : live == 0.0f; };
     float T = 1.0f;
     float C0 = 0.f, C1 = 0.f, C2 = 0.f, ID = 0.f;
     uint32_t last_contributor = 0;
@@ -371,7 +363,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
     uint32_t next_id = todo > 0 ? a.point_list[range.x + min(tid, todo - 1)] : 0u;
     int flushed = 0;  // entries [0, flushed) have their contribution bits in a.hit
     for (int base = 0; base < todo; base += BATCH) {
-        if (__syncthreads_and(finished())) break;
+        if (__syncthreads_and(live == 0.0f)) break;
         if (base > 0) {  // the previous batch's contribution bits (every wave has finished it)
             a.hit[range.x + base - BATCH + tid] = (uint8_t)hit_bits(s_hitw, tid);
             flushed = base;
@@ -396,7 +388,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
         // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
         // per 64 entries, then a scalar bit scan; each record is read one entry ahead of use.
         for (int r = 0; r < BATCH / 64; r++) {
-            if (__all(finished())) break;
+            if (__all(live == 0.0f)) break;
             const int jr = r * 64 + lane;
             uint64_t rem = __ballot(jr < n && ((s_mask[jr] >> wid) & 1));
             if (rem == 0) continue;
@@ -414,45 +406,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             // issue port in this loop).  a = 0 for a finished pixel (live = 0) or power > 0; an
             // entry that would take T below 1e-4 finishes the pixel without blending
             // (forward.cu:356-376); ae = the alpha actually blended (0 or a).
-            // GSR_FWD_MASKS: the same decisions as compares into scalar masks (v_cmp + s_and / s_andn2)
-            // instead of selects on the alpha value -- 26 VALU per entry instead of 30 (the VALU is the
-            // busier port: trading the per-entry scalar hit-bit update for a VALU lane write measured
-            // render_fwd +3 %).  A finished pixel has thr = -inf (no entry passes !(p2 > thr)); the
-            // alpha is never masked: (1 - alpha), test_T and alpha T are used only under the masks.
-            //   contrib = power <= 0 (forward.cu:355-356) and alpha >= 1/255 (:364)
-            //   stop    = contrib and T (1 - alpha) < 1e-4 (:368-371)
-            //   blended = contrib and not stop
-            auto blend_masked = [&](int j, const float4 xy, const float4 co, const float4 col) {
-                const float p2 = falloff_p2(falloff(co), xy.x - pfx, xy.y - pfy);
-                const float alpha = fminf(0.99f, __builtin_amdgcn_exp2f(p2) * co.w);
-                const bool in_front = !(p2 > thr), visible = alpha >= 1.0f / 255.0f;
-                const bool contrib = in_front & visible;
-                const float test_T = T * (1.0f - alpha);
-                const bool low = test_T < 0.0001f;
-                const bool stop = contrib & low;
-                const bool blended = contrib & !low;
-                thr = stop ? -__builtin_inff() : thr;
-                {  // hitbits |= (any lane blended) ? bit j : 0 (as in blend below); the wave's blended
-                   // mask from the compares' own masks (a ballot of the combined bool would be
-                   // re-materialised through a VGPR)
-                    const uint64_t mb = __ballot(in_front) & __ballot(visible) & ~__ballot(low);
-                    uint64_t t;
-                    asm("s_cmp_lg_u64 %1, 0\n\ts_cselect_b64 %0, %2, 0" : "=s"(t) : "s"(mb), "s"(1ull << (j & 63)) : "scc");
-                    hitbits |= t;
-                }
-                const float aT = blended ? alpha * T : 0.0f;  // 0 leaves the sums unchanged
-                C0 += col.x * aT;
-                C1 += col.y * aT;
-                C2 += col.z * aT;
-                ID += col.w * aT;
-                T = blended ? test_T : T;
-                last_contributor = blended ? (uint32_t)(base + j + 1) : last_contributor;
-            };
             auto blend = [&](int j, const float4 xy, const float4 co, const float4 col) {
-                if constexpr (FWD_MASKS) {
-                    blend_masked(j, xy, co, col);
-                    return;
-                }
 #if GSR_REF_ALPHA
                 const float p2 = ref_power(co, xy.x - pfx, xy.y - pfy);  // power (test build)
                 const float alpha = fminf(0.99f, co.w * gsr_ref_expf(p2));
@@ -508,7 +462,7 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 aco = s_rec[BATCH + j];
                 acol = s_rec[2 * BATCH + j];
                 blend(jb, bxy, bco, bcol);
-                if (--left == 0 || __all(finished())) break;
+                if (--left == 0 || __all(live == 0.0f)) break;
             }
             if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
         }
