@@ -325,7 +325,10 @@ __device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64
 // One launch renders a batch of views (grid.y = view): the views' tiles are dispatched one view
 // after the other, so a view's long tiles start while the previous view's short tail still runs --
 // one launch tail per batch instead of one per view.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
+#ifndef GSR_FWD_WAVES
+#define GSR_FWD_WAVES 8  // waves per SIMD (VGPR budget)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES)))
 render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
 {
 #if GSR_REF_ALPHA  // (test build: every blend operation in the reference's order, forward.cu:353-380)
