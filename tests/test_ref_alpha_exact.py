@@ -165,3 +165,79 @@ def test_ref_alpha_chair(ref_lib, case):
     camt = (cam.world_view_transform.numpy(), cam.full_proj_transform.numpy(), cam.camera_center.numpy(),
             cam.tanfovx, cam.tanfovy)
     run_exact(f"chair case {case}", H, W, inp, camt, deg, aa, np.asarray(bg, np.float32), 1.0, gc.numpy(), gi.numpy())
+
+
+def test_ref_alpha_bench_step(ref_lib):
+    """The benchmarked step itself (bench.py's default: ONE MultiViewRasterizer call over config 4's
+    8 ring views of the config-2 scene at 1080p, the batched forward and the one batched preprocess
+    backward) in the test build: every view's colour / invdepth / final_T / n_contrib bit-identical to
+    the shared-exp oracle on that view, num_rendered / radii / keys / values / ranges bit-exact, each
+    view's dL/dmean2D and the 8-view sums of the parameter gradients within GRAD_RTOL of their max with
+    no row beyond it and none left out (antialiasing off)."""
+    import diff_gaussian_rasterization as dgr
+    import oracle
+    import synthetic
+    from test_gpu_parity import _img_state
+    P, H, W, V = 1_000_000, 1080, 1920, 8
+    scene = synthetic.make_scene(P, seed=0)
+    bg = torch.zeros(3)
+    cams = [synthetic.Camera(W, H, view=v, n_views=8) for v in range(V)]
+    grads = [synthetic.make_grads(H, W, seed=1 + v) for v in range(V)]
+    settings = [dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy, bg=bg.to(DEV), scale_modifier=1.0,
+        viewmatrix=c.world_view_transform.to(DEV), projmatrix=c.full_proj_transform.to(DEV), sh_degree=3,
+        campos=c.camera_center.to(DEV), prefiltered=False, debug=False, antialiasing=False) for c in cams]
+    params = {k: v.to(DEV).requires_grad_(True) for k, v in scene.items()}
+    means2D = torch.zeros((V, P, 3), device=DEV, requires_grad=True)
+    color, radii, inv = dgr.MultiViewRasterizer(settings)(
+        means3D=params["means3D"], means2D=means2D, shs=params["shs"], opacities=params["opacities"],
+        scales=params["scales"], rotations=params["rotations"])
+    node = color.grad_fn
+    Ls = list(node.num_rendered)
+    bufs = node.saved_tensors[9:]
+    geoms, bins, imgs = bufs[0::3], bufs[1::3], bufs[2::3]
+    torch.autograd.backward([color, inv], [torch.stack([g[0] for g in grads]).to(DEV),
+                                           torch.stack([g[1] for g in grads]).to(DEV)])
+    torch.cuda.synchronize()
+    keys_p = {"means3D": "dL_dmeans3D", "shs": "dL_dsh", "opacities": "dL_dopacity", "scales": "dL_dscales",
+              "rotations": "dL_drotations"}
+    none = np.zeros(P, bool)
+    ref_sum = None
+    for v in range(V):
+        o = oracle.OracleRaster(scene["means3D"], scene["opacities"], bg, cams[v].world_view_transform,
+                                cams[v].full_proj_transform, cams[v].camera_center, cams[v].tanfovx, cams[v].tanfovy,
+                                H, W, shs=scene["shs"], sh_degree=3, scales=scene["scales"],
+                                rotations=scene["rotations"], nthreads=THREADS, shared_exp=True)
+        tag = f"bench step view {v} [ref-alpha]"
+        assert Ls[v] == o.num_rendered, tag
+        np.testing.assert_array_equal(radii[v].cpu().numpy(), o.radii, err_msg=tag)
+        keys, vals, ranges = dgr._C.sorted_keys(geoms[v], bins[v], imgs[v], P, Ls[v], W, H)
+        np.testing.assert_array_equal(keys.cpu().numpy().view(np.uint64), o.get("keys"), err_msg=tag)
+        np.testing.assert_array_equal(vals.cpu().numpy().view(np.uint32), o.get("vals"), err_msg=tag)
+        np.testing.assert_array_equal(ranges.cpu().numpy().view(np.uint32), o.get("ranges"), err_msg=tag)
+        del keys, vals, ranges
+        fT, nc = _img_state(imgs[v], W, H)
+        hip_r = {"color": color[v].detach().cpu().numpy(), "invdepth": inv[v].detach().cpu().numpy(), "final_T": fT,
+                 "n_contrib": nc}
+        ora_r = {"color": o.color, "invdepth": o.invdepth, "final_T": o.get("final_T"), "n_contrib": o.get("n_contrib")}
+        st = common.check_render(tag, hip_r, ora_r)
+        for k in ("color", "invdepth", "final_T", "n_contrib"):
+            a, b = np.ascontiguousarray(hip_r[k]), np.ascontiguousarray(ora_r[k])
+            diff = int((a.reshape(-1).view(np.uint32) != b.reshape(-1).view(np.uint32)).sum())
+            assert diff == 0, f"{tag}: {k} differs in {diff} values ({st})"
+        og = o.backward(grads[v][0], grads[v][1])
+        del o
+        m2 = means2D.grad[v].cpu().numpy()
+        ok, rel = common.allclose_rel(m2, og["dL_dmean2D"])
+        common.check_grad_attributed(f"{tag} dL_dmean2D", m2, og["dL_dmean2D"], none)
+        assert ok, f"{tag}: dL/dmean2D {rel:.3e}"
+        og = {k: og[k].astype(np.float64) for k in keys_p.values()}
+        ref_sum = og if ref_sum is None else {k: ref_sum[k] + og[k] for k in ref_sum}
+    for k, ok_ in keys_p.items():
+        a = params[k].grad.cpu().numpy()
+        ref = ref_sum[ok_].reshape(a.shape)
+        name = f"bench step sum of 8 views {ok_} [ref-alpha]"
+        ok, rel = common.allclose_rel(a, ref)
+        common.check_grad_attributed(name, a, ref, none)
+        common.check_rel(name, a, ref, None)
+        assert ok, f"{name}: {rel:.3e}"
