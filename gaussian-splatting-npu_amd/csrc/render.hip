@@ -328,6 +328,16 @@ __device__ __forceinline__ uint32_t hit_bits(const uint64_t (*s_hitw)[BATCH / 64
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 8  // waves per SIMD (VGPR budget)
 #endif
+#ifndef GSR_FWD_STATS
+#define GSR_FWD_STATS 0  // diagnostic build: per (tile, batch, wave) entries walked, view 0 only
+#endif
+#if GSR_FWD_STATS
+__device__ uint32_t* g_fwd_stats;  // [tile][32 batches][4 waves]
+extern "C" int gsr_debug_fwd_stats(void* p)
+{
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_stats), &p, sizeof(p));
+}
+#endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES)))
 render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
 {
@@ -388,6 +398,9 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
         // follow in program order
         if (lane < BATCH / 64) s_hitw[wid][lane] = 0ull;
         const int n = min(BATCH, todo - base);
+#if GSR_FWD_STATS
+        uint32_t walked = 0;
+#endif
         // Walk the entries whose mask has this wave's quadrant bit, in list order: one ballot
         // per 64 entries, then a scalar bit scan; each record is read one entry ahead of use.
         for (int r = 0; r < BATCH / 64; r++) {
@@ -453,6 +466,9 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
             // The all-finished exit is tested every second entry (blending into finished pixels
             // is a no-op), at the end of each two-entry turn.
             int left = __popcll(rem);
+#if GSR_FWD_STATS
+            const int left0 = left;
+#endif
             int j = take();
             float4 axy = s_rec[j], aco = s_rec[BATCH + j], acol = s_rec[2 * BATCH + j];
             while (true) {
@@ -468,7 +484,13 @@ render_fwd_kernel(const ViewBatch<RenderFwdArgs> B)
                 if (--left == 0 || __all(live == 0.0f)) break;
             }
             if (lane == 0 && hitbits) s_hitw[wid][r] = hitbits;
+#if GSR_FWD_STATS
+            walked += (uint32_t)(left0 - left);
+#endif
         }
+#if GSR_FWD_STATS
+        if (blockIdx.y == 0 && lane == 0 && base / BATCH < 32) g_fwd_stats[(tile * 32 + base / BATCH) * 4 + wid] = walked + 1;
+#endif
     }
 
     __shared__ uint32_t s_lc[4];
