@@ -52,6 +52,15 @@ def main():
     print(f"utilisation, waves in lock step per batch: {lock:.3f}")
     print(f"utilisation, each wave alone over its tile: {alone:.3f}")
     print(f"walked (wave-entries) total {w.sum()}, lock-step slots {4 * bmax.sum()}, alone slots {4 * tot.max(axis=1).sum()}")
+    # slot time a wave holds after its last batch with work (what exiting at a batch boundary frees)
+    act = w > 0
+    last = np.where(act.any(axis=1), 31 - np.argmax(act[:, ::-1, :], axis=1), -1)  # (T, 4)
+    bidx = np.arange(32)[None, :, None]
+    after = (bidx > last[:, None, :]) & done.any(axis=2)[:, :, None]
+    freed = (after * bmax[:, :, None]).sum()
+    idle = 4 * bmax.sum() - w.sum()
+    print(f"idle slot time {idle} ({idle / (4 * bmax.sum()):.3f}); after a wave's last active batch {freed} "
+          f"({freed / (4 * bmax.sum()):.3f})")
     # tiles' walk relative to the tile with most
     ws = tot.max(axis=1)
     print("busiest-wave walk per tile: p50 %d p90 %d p99 %d max %d" % tuple(np.percentile(ws, [50, 90, 99, 100])))
