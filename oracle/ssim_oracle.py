@@ -68,4 +68,4 @@ def ssim_and_grad(img1, img2, dtype=torch.float64, upstream=None):
     m = ssim_map(a, img2, dtype)
     loss = m.mean() if upstream is None else (m * _t(upstream, dtype)).sum()
     loss.backward()
-    return float(m.mean()), a.grad.numpy()
+    return float(m.detach().mean()), a.grad.numpy()
