@@ -33,6 +33,7 @@ for st in "$@"; do
           [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     testsel:*) run pytest_sel 600 python -u -m pytest ${st#testsel:} -m gpu -x -v --timeout 300 --timeout-method thread
           cp -f gpurun_out/parity_stats.json "$OUT/" 2>/dev/null ;;
+    smoke) run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python -u bench.py
            cp -f gpurun_out/pmc_step.json gpurun_out/pmc_single.json "$OUT/" 2>/dev/null ;;
     benchq) run benchq 300 python -u bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-aux --no-pmc --no-single-view ;;
