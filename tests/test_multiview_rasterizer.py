@@ -216,6 +216,9 @@ def test_deferred_backward_after_context_exit():
         assert ok, f"d{k}: late deferred vs plain rel {rel:.3e}"
 
 
+# (the views alternate between two streams on purpose, so autograd notes that a leaf's gradient
+# arrives from another stream than the leaf's own)
+@pytest.mark.filterwarnings("ignore:The AccumulateGrad node's stream does not match")
 def test_deferred_backward_activations_streams_accumulation():
     """The train.py shape: activations between the parameters and the rasterizer (exp, sigmoid,
     normalize), views alternating between two streams, and a second batch adding into the .grad of

@@ -78,7 +78,7 @@ def test_hip_matches_oracle(shape, seed, padding):
         m = m[..., 5:-5, 5:-5]
     ref = m.mean()
     ref.backward()
-    assert abs(float(v) - float(ref)) < 2e-6
+    assert abs(float(v.detach()) - float(ref.detach())) < 2e-6
     g, r = x.grad.cpu().numpy(), a64.grad.numpy()
     assert np.abs(g - r).max() <= 1e-4 * np.abs(r).max() + 1e-12
 
