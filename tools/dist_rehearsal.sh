@@ -8,7 +8,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/${1:-dist}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+# BENCH_EXTRA: more bench.py flags (e.g. "--views-per-rank 4" for the weak-scaling mode)
 GSR_DIST_BACKEND=gloo timeout -k 10 600 python bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline \
-    > "$OUT/bench2.log" 2>&1
+    ${BENCH_EXTRA:-} > "$OUT/bench2.log" 2>&1
 rc=$?; grep '^{' "$OUT/bench2.log" > "$OUT/bench2.json"; cut -c1-400 "$OUT/bench2.json"
 [ $rc -ne 0 ] && tail -30 "$OUT/bench2.log"; exit $rc
