@@ -571,6 +571,20 @@ __device__ __forceinline__ ViewCam cam_of_lds(const float* c)
     return {c, c + 16, c + 32, c[35], c[36], c[37], c[38]};
 }
 
+// visible <=> radius > 0 (backward.cu:163,420) <=> a tile count > 0: preprocess culls a Gaussian whose
+// rect is empty and writes radius 0 and no tiles for every culled one (4 B per view less to read)
+// (the single-view launch keeps the reference's test on the caller's radii)
+__device__ __forceinline__ bool view_visible_in(const PreprocessBwdViewsArgs& A, bool live, int v, const ViewIn& vi)
+{
+    return live && v < A.V && (A.a.radii ? vi.drawn : vi.n > 0);
+}
+
+template <int LPG>
+__device__ __forceinline__ void bwd_views_group_gs(const PreprocessBwdViewsArgs& A, int idx, bool live, int v,
+                                                   const BwdIn& in, const ViewIn& vi, const float (&gs)[GF_NUM],
+                                                   const float* cam, const float* c0, const float* cr, float* d0,
+                                                   float* dr, int kw, bool acc_dc, bool acc_sh);
+
 // One lane's share of a Gaussian of the batch.  c0: SH coefficient 0 (3 floats), cr: coefficient
 // k >= 1 at cr[3 (k - 1)]; d0 / dr the same for dL/dsh (may alias c0 / cr: every lane of the group
 // reads coefficient k before its sum is written), kw the number of coefficients to write (zeros from
@@ -582,16 +596,9 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
                                                 const float* c0, const float* cr, float* d0, float* dr, int kw,
                                                 bool acc_dc, bool acc_sh)
 {
-    const PreprocessBwdArgs& a = A.a;
-    const size_t i = (size_t)idx;
-    const bool has_view = live && v < A.V;
     const BwdView& bv = A.v[v < A.V ? v : 0];
-    // visible <=> radius > 0 (backward.cu:163,420) <=> a tile count > 0: preprocess culls a Gaussian whose
-    // rect is empty and writes radius 0 and no tiles for every culled one (4 B per view less to read)
-    // (the single-view launch keeps the reference's test on the caller's radii)
-    const bool vis = has_view && (a.radii ? vi.drawn : vi.n > 0);
     float gs[GF_NUM];
-    if (vis) {
+    if (view_visible_in(A, live, v, vi)) {
         // one lane per Gaussian: 8 records in flight (145 VGPRs; the SH staging caps it at 3 waves/SIMD
         // anyway): 145 -> 141 us per 1080p view
         gather_any<LPG == 1 ? 2 * REC_BATCH : REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
@@ -599,6 +606,21 @@ __device__ __forceinline__ void bwd_views_group(const PreprocessBwdViewsArgs& A,
 #pragma unroll
         for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
     }
+    bwd_views_group_gs<LPG>(A, idx, live, v, in, vi, gs, cam, c0, cr, d0, dr, kw, acc_dc, acc_sh);
+}
+
+// gs: the lane's view records, summed (zeros for an invisible view)
+template <int LPG>
+__device__ __forceinline__ void bwd_views_group_gs(const PreprocessBwdViewsArgs& A, int idx, bool live, int v,
+                                                   const BwdIn& in, const ViewIn& vi, const float (&gs)[GF_NUM],
+                                                   const float* cam, const float* c0, const float* cr, float* d0,
+                                                   float* dr, int kw, bool acc_dc, bool acc_sh)
+{
+    const PreprocessBwdArgs& a = A.a;
+    const size_t i = (size_t)idx;
+    const bool has_view = live && v < A.V;
+    const BwdView& bv = A.v[v < A.V ? v : 0];
+    const bool vis = view_visible_in(A, live, v, vi);
     float cov3D[6];
     cov3d_of(a, in, cov3D);
     ViewGrad o;
@@ -796,6 +818,91 @@ __global__ void __launch_bounds__(256) preprocess_bwd_views_kernel(const Preproc
     });
 }
 
+// The same work as preprocess_bwd_views_kernel<LPG, true> for the interleaved SH layout, with
+// GSR_PBWD_PIPE chunks of G Gaussians per workgroup in straight-line code: every chunk's view
+// inputs (record range and mask) are loaded up front, so a later chunk's record gathers are issued
+// together with its parameter and SH loads -- one memory round trip before its compute instead of two.
+// (As a loop over chunks the compiler keeps ~60 more VGPRs live: 2 waves/SIMD instead of 4.)
+#ifndef GSR_PBWD_PIPE
+#define GSR_PBWD_PIPE 2  // chunks per workgroup, lane groups (the batch launches; 0: one chunk, the plain kernel)
+#endif
+#ifndef GSR_PBWD_PIPE1
+#define GSR_PBWD_PIPE1 0  // the same for the single view's one lane per Gaussian
+#endif
+#ifndef GSR_PBWD_PIPE2
+#define GSR_PBWD_PIPE2 0  // the same for two lanes per Gaussian (batches of 1-2 views)
+#endif
+template <int LPG>
+__device__ __forceinline__ void pbwd_chunk(const PreprocessBwdViewsArgs& A, float* s_sh, const float* cam, int chunk,
+                                           const ViewIn& vi)
+{
+    constexpr int G = 256 / LPG;
+    constexpr int PER = (G * 12 + 255) / 256;  // SH float4 loads per thread and chunk
+    const PreprocessBwdArgs& a = A.a;
+    const int gl = (int)threadIdx.x / LPG, v = (int)threadIdx.x % LPG;
+    const int base = A.g_begin + chunk * G;
+    const bool live = base + gl < A.g_end;
+    const int idx = min(base + gl, A.g_end - 1);  // clamped: all lanes take part in the reductions
+    const int n = min(G, A.g_end - base);
+    BwdIn in;
+    bwd_gather(a, idx, in);
+    const float4* src = reinterpret_cast<const float4*>(a.shs + (size_t)base * 48);
+    float4 sv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        const int f = (int)threadIdx.x + u * 256;
+        if (f < n * 12) sv[u] = src[f];
+    }
+    float gs[GF_NUM];
+    if (view_visible_in(A, live, v, vi)) {
+        const BwdView& bv = A.v[v < A.V ? v : 0];
+        gather_any<REC_BATCH>(vi.e0, vi.n, vi.mask, bv.valid, bv.grad_inst, gs);
+    } else {
+#pragma unroll
+        for (int q = 0; q < GF_NUM; q++) gs[q] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+        const int f = (int)threadIdx.x + u * 256;
+        if (f < n * 12) {
+            const int g = f / 12, j = f - g * 12;
+            float* d = &s_sh[g * SH_STRIDE + 4 * j];
+            d[0] = sv[u].x; d[1] = sv[u].y; d[2] = sv[u].z; d[3] = sv[u].w;
+        }
+    }
+    __syncthreads();
+    float* row = s_sh + gl * SH_STRIDE;
+    bwd_views_group_gs<LPG>(A, idx, live, v, in, vi, gs, cam, row, row + 3, row, row + 3, 16, false, false);
+    __syncthreads();
+    store_f4(reinterpret_cast<float4*>(a.dL_dsh + (size_t)base * 48), n * 12, a.acc & ACC_SH, [&](int f) {
+        const int g = f / 12, j = f - g * 12;
+        const float* q = &s_sh[g * SH_STRIDE + 4 * j];
+        return make_float4(q[0], q[1], q[2], q[3]);
+    });
+}
+
+template <int LPG, int NCH>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LPG == 1 ? 3 : 1)))
+preprocess_bwd_views_pipe_kernel(const PreprocessBwdViewsArgs A, int nchunks)
+{
+    constexpr int G = 256 / LPG;
+    extern __shared__ __attribute__((aligned(16))) float s_sh[];
+    const int gl = (int)threadIdx.x / LPG, v = (int)threadIdx.x % LPG;
+    __shared__ float s_cam[MAX_VIEWS][CAM_FLOATS];
+    const int c0 = (int)blockIdx.x * NCH;
+    ViewIn vi[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) view_load(A, min(A.g_begin + min(c0 + k, nchunks - 1) * G + gl, A.g_end - 1), v, vi[k]);
+    cams_to_lds(A, s_cam);  // (read after the first chunk's barrier)
+    const float* cam = s_cam[v < A.V ? v : 0];
+#pragma unroll
+    for (int k = 0; k < NCH; k++) {
+        if (c0 + k >= nchunks) break;  // (uniform)
+        if (k > 0) __syncthreads();  // the rows are restaged
+        pbwd_chunk<LPG>(A, s_sh, cam, c0 + k, vi[k]);
+    }
+}
+
 static bool staged_layout(const PreprocessBwdArgs& a)
 {
     const bool interleaved = a.shs && a.dL_dsh && a.M == 16 && ((uintptr_t)a.shs % 16) == 0 &&
@@ -808,6 +915,15 @@ static hipError_t launch_views(const PreprocessBwdViewsArgs& A, hipStream_t s)
 {
     constexpr int G = 256 / LPG;
     const dim3 grid((A.g_end - A.g_begin + G - 1) / G), block(256);
+    constexpr int NCH = LPG >= 4 ? GSR_PBWD_PIPE : LPG == 2 ? GSR_PBWD_PIPE2 : GSR_PBWD_PIPE1;
+    if constexpr (NCH > 0) {
+        if (staged_layout(A.a) && !A.a.dc) {
+            const int nchunks = (int)grid.x, blocks = (nchunks + NCH - 1) / NCH;
+            hipLaunchKernelGGL((preprocess_bwd_views_pipe_kernel<LPG, NCH>), dim3(blocks), block, staged_lds_bytes(G), s,
+                               A, nchunks);
+            return hipGetLastError();
+        }
+    }
     if (staged_layout(A.a))
         hipLaunchKernelGGL((preprocess_bwd_views_kernel<LPG, true>), grid, block, staged_lds_bytes(G), s, A);
     else
