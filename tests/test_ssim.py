@@ -117,7 +117,7 @@ def test_dr_aa_ops_and_train_loss():
     a64 = a.double().requires_grad_(True)
     ref = 0.8 * (a64 - b.double()).abs().mean() + 0.2 * (1.0 - so.ssim_map(a64, b).mean())
     ref.backward()
-    assert abs(float(loss) - float(ref)) < 2e-6
+    assert abs(float(loss.detach()) - float(ref.detach())) < 2e-6
     assert np.abs(img.grad.cpu().numpy() - a64.grad.numpy()).max() <= 1e-4 * np.abs(a64.grad.numpy()).max()
 
 
