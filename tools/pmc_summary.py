@@ -23,6 +23,7 @@ SHORT = {"preprocess_fwd_kernel": "preprocess_fwd", "preprocess_views_kernel": "
          "emit_instances_kernel": "emit_instances", "tile_ranges_kernel": "tile_ranges", "tile_hist_kernel": "tile_ranges",
          "tile_order_kernel": "tile_order", "render_fwd_kernel": "render_fwd", "render_bwd_kernel": "render_bwd",
          "preprocess_bwd_kernel": "preprocess_bwd", "preprocess_bwd_views_kernel": "preprocess_bwd",
+         "preprocess_bwd_views_pipe_kernel": "preprocess_bwd",
          # the radix passes carry their sort's name tag (radix.hip): depth sort, tile sort (+ its fused
          # first pass), distCUDA2's cell sort
          "DepthSort": "depth_sort", "TileSort": "tile_sort", "fused_pass1_": "tile_sort", "CellSort": "distCUDA2",
