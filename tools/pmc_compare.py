@@ -2,7 +2,12 @@
 as "vs_previous": the counters VERDICT asks to track (waits, LDS bank conflicts, write requests,
 HBM bytes, SALU/VALU).  Usage: pmc_compare.py OLD.json NEW.json OUT.json OLD_TAG NEW_TAG"""
 import json
+import os
+import re
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import short_name  # noqa: E402
 
 KEYS = ["SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS", "TCC_EA0_WRREQ_sum",
         "TCC_EA0_WRREQ_64B_sum", "TCC_EA0_RDREQ_sum", "FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_SALU", "SQ_INSTS_VALU",
@@ -14,6 +19,13 @@ def main(old, new, out, old_tag, new_tag):
     cmp = {}
     for name, kb in b["kernels"].items():
         ka = a["kernels"].get(name)
+        if ka is None:  # a kernel renamed between the rounds: the same operation and first template argument
+            targ = re.search(r"<(\d+)", name)
+            cand = [k for k in a["kernels"] if short_name(k) == short_name(name) and short_name(k) is not None and
+                    (targ is None or re.search(r"<(\d+)", k) and re.search(r"<(\d+)", k).group(1) == targ.group(1))]
+            if len(cand) == 1:
+                ka = a["kernels"][cand[0]]
+                cmp.setdefault("_renamed", {})[name] = cand[0]
         pb = {c: kb[c] for c in KEYS if c in kb}
         row = {new_tag: pb, "dispatches": {new_tag: kb.get("dispatches")}}
         if ka is not None:
