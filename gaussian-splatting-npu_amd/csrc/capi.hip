@@ -1090,6 +1090,7 @@ int gsr_backward_dc_acc(int P, int D, int M, int R, const float* background, int
     RenderBwdArgs r;
     r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    r.tile_work = at<uint32_t>(ib, im.off[IMG_TILE_WORK]);
     r.point_list = R > 0 ? at<uint32_t>(bb, b.off[BIN_POINT_LIST]) : nullptr;
     r.W = width; r.H = height; r.grid_x = gx;
     r.T = (int)(gx * gy);
@@ -1188,6 +1189,7 @@ static RenderBwdArgs render_bwd_args(int P, int R, const float* background, int 
     RenderBwdArgs r;
     r.ranges = at<uint2>(ib, im.off[IMG_RANGES]);
     r.tile_order = at<uint32_t>(ib, im.off[IMG_TILE_ORDER]);
+    r.tile_work = at<uint32_t>(ib, im.off[IMG_TILE_WORK]);
     r.point_list = at<uint32_t>(bb, b.off[BIN_POINT_LIST]);
     r.W = width; r.H = height; r.grid_x = gx;
     r.T = (int)(gx * gy);

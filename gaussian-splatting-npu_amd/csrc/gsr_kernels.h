@@ -64,6 +64,7 @@ struct RenderFwdArgs {
 struct RenderBwdArgs {
     const uint2* ranges;
     const uint32_t* tile_order;  // IMG_TILE_ORDER (re-ordered from IMG_TILE_WORK for the backward)
+    const uint32_t* tile_work;   // IMG_TILE_WORK (render_fwd): the tile's largest n_contrib
     const uint32_t* point_list;
     int W, H;
     uint32_t grid_x;

@@ -798,8 +798,9 @@ __global__ void __launch_bounds__(64 * BWD_TPW) __attribute__((amdgpu_waves_per_
         s.lc0 = lc[2 * h];
         s.lc1 = lc[2 * h + 1];
     }
-    const uint32_t tmax =
-        (uint32_t)__builtin_amdgcn_readfirstlane((int)wave_max_u32(max(max(lc[0], lc[1]), max(lc[2], lc[3]))));
+    // the tile's largest n_contrib, as render_fwd stored it (the max of lc over the tile's pixels): a
+    // scalar load beside the range's, so the first batch's list loads do not wait for the pixel state
+    const uint32_t tmax = a.tile_work[tile];
 
     __shared__ float4 s_recw[BWD_TPW][3][64];
     __shared__ uint8_t s_lqw[BWD_TPW][4][64];
