@@ -335,3 +335,34 @@ def test_backward_bitwise_reproducible():
     for r in runs[1:]:
         for k in runs[0]:
             assert torch.equal(r[k], runs[0][k]), f"d{k} differs between identical backwards"
+
+
+@pytest.mark.parametrize("nv,p", [(8, 990), (3, 4000), (10, 1500)])
+def test_two_chunk_preprocess_backward_matches_one_chunk_kernel(nv, p):
+    """The batched preprocess backward runs as the two-chunk kernel for interleaved SH rows
+    (preprocess_bwd_views_pipe_kernel: 3+ views) and as the one-chunk kernel for the separate-DC
+    layout: the same arithmetic on the same values, so every gradient is bitwise identical between
+    the two layouts -- with an odd number of chunks (a workgroup with one chunk) and 4 / 8 / 16 lanes
+    per Gaussian."""
+    import diff_gaussian_rasterization as dgr
+    case = common.make_case(P=p, H=H, W=W, bg=(0.1, 0.2, 0.3))
+    bg = case["bg"].to(DEV)
+    cams = [synthetic.Camera(W, H, view=v, n_views=nv) for v in range(nv)]
+    settings = [_settings(c, False, bg) for c in cams]
+    grads = [synthetic.make_grads(H, W, seed=80 + v) for v in range(nv)]
+    gc = torch.stack([g[0] for g in grads]).to(DEV)
+    gi = torch.stack([g[1] for g in grads]).to(DEV)
+    out = {}
+    for mode in ("sh_scales", "dc"):
+        t = _leaves(case, mode)
+        means2D = torch.zeros((nv, p, 3), device=DEV, requires_grad=True)
+        c, r, i = dgr.MultiViewRasterizer(settings)(means2D=means2D, **t)
+        torch.autograd.backward([c, i], [gc, gi])
+        torch.cuda.synchronize()
+        g = {k: v.grad for k, v in t.items()}
+        if mode == "dc":
+            g["shs"] = torch.cat([g.pop("dc"), g["shs"]], dim=1)
+        g["means2D"] = means2D.grad
+        out[mode] = g
+    for k, a in out["sh_scales"].items():
+        assert torch.equal(a, out["dc"][k]), f"{nv} views, P={p}: d{k} differs between the two kernels"
